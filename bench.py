@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Headline benchmark: SDXL 1024x1024, 20-step Euler-ancestral, CFG 8, data-parallel over N GPUs.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` (N>1 under torch.distributed.run).
+One *step* = one whole-node job of ``batch_per_gpu * N`` images (weak scaling: fixed per-GPU work):
+CLIP-L/G prompt encode -> 20 Euler-a steps with cond/uncond batched (UNet batch = 2 x images per GPU)
+-> VAE decode -> uint8 -> all-gather to rank 0 (RCCL over xGMI). Weights are random-init SDXL-base
+of the exact architecture (no network / checkpoints available); rank 0's weights are broadcast to
+every rank (R3). Timed region = exactly K steps bracketed by barrier + device synchronize; the
+reported time is the MAX over ranks. Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch-per-gpu", type=int, default=8)
+    ap.add_argument("--family", default="sdxl")
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--sampler-steps", type=int, default=20)
+    ap.add_argument("--sampler", default="euler_ancestral")
+    ap.add_argument("--cfg", type=float, default=8.0)
+    ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (use with --family tiny)")
+    ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the denoiser")
+    ap.add_argument("--profile-ops", action="store_true")
+    args = ap.parse_args()
+
+    if args.cpu:
+        os.environ["CGS_FORCE_CPU"] = "1"
+    if args.no_graph:
+        os.environ["CGS_GRAPHS"] = "0"
+    import torch
+    from comfy_gen_server_amd.parallel.comm import init_from_env
+    comm = init_from_env(backend="gloo" if args.cpu else None)
+    from comfy_gen_server_amd.runtime import device as dm
+    if not args.cpu:
+        dm.set_device_index(comm.local_rank)
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    from comfy_gen_server_amd.parallel.dp import DataParallelGenerator, Job
+    from comfy_gen_server_amd import ops
+
+    dev = dm.get_torch_device()
+    dtype = torch.float32 if args.cpu else torch.bfloat16
+    t0 = time.time()
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline(args.family, device=dev, dtype=dtype, seed=1234)
+    gen = DataParallelGenerator(patcher, clip, vae)
+    with torch.inference_mode():
+        gen.sync_weights()
+    comm.barrier()
+    t_build = time.time() - t0
+
+    N = comm.world
+    global_batch = args.batch_per_gpu * N
+    job = Job(batch=global_batch, steps=args.sampler_steps, cfg=args.cfg, sampler=args.sampler,
+              width=args.res, height=args.res)
+
+    def one_step(i):
+        j = Job(**{**job.__dict__, "seed": 1000 + i})
+        with torch.inference_mode():
+            return gen.run(j)
+
+    for i in range(args.warmup):
+        one_step(i)
+    if not args.cpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    ops.reset_stats()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        out = one_step(args.warmup + i)
+    if not args.cpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    dt = time.perf_counter() - t1
+    dt = comm.all_reduce_max(dt)
+    ms_per_step = dt * 1000.0 / max(1, args.steps)
+    imgs_per_sec = global_batch * args.steps / dt
+    if comm.rank == 0:
+        try:
+            with open(os.path.join(HERE, "BASELINE.json")) as f:
+                metric = json.load(f)["metric"]
+        except Exception:
+            metric = "images/sec (whole node), SDXL 1024 20-step Euler-a"
+        res = {
+            "metric": metric,
+            "value": round(imgs_per_sec, 4),
+            "unit": "images/s",
+            "n_gpus": N,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if args.cpu else "bf16",
+            "data": "synthetic prompts, random-init weights (exact SDXL-base architecture)",
+            "sec_per_image": round(dt / (global_batch * args.steps), 4),
+            "sec_per_image_per_gpu": round(dt * N / (global_batch * args.steps), 4),
+            "config": {"model": f"{args.family}-base" if args.family == "sdxl" else args.family,
+                       "global_batch": global_batch, "seq_len": (args.res // 8) ** 2,
+                       "resolution": args.res, "sampler_steps": args.sampler_steps, "sampler": args.sampler,
+                       "cfg": args.cfg, "unet_batch_per_gpu": 2 * args.batch_per_gpu,
+                       "parallelism": f"dp{N}"},
+            "build_s": round(t_build, 1),
+        }
+        if args.profile_ops:
+            res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
+        print(json.dumps(res), flush=True)
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()

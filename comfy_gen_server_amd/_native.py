@@ -1,0 +1,144 @@
+"""Loader for the in-tree native libraries.
+
+Two shared objects are built by ``build_native.py`` (invoked by ``__graft_entry__.build``):
+
+* ``libcgs_kernels.so`` — hand-written HIP kernels for gfx950 (MFMA GEMM / flash attention /
+  GroupNorm+SiLU / LayerNorm / fused sampler steps ...). Exposed as ``extern "C"`` launchers that
+  take raw device pointers and a ``hipStream_t``; bound here with ctypes so the kernels launch on
+  torch's current stream and are captured transparently by hipGraphs.
+* ``_cgs_runtime*.so`` — C++ runtime (safetensors mmap reader, CLIP BPE tokenizer, BLAKE3,
+  prompt priority queue) as a CPython extension module.
+
+On a GPU box the kernel library MUST load: ops fail loudly instead of silently falling back to
+PyTorch (set ``CGS_ALLOW_TORCH_FALLBACK=1`` to opt into the fallback explicitly).
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+_lock = threading.Lock()
+_kernels = None
+_kernels_err = None
+
+
+def kernel_lib_path() -> str:
+    return os.path.join(LIB_DIR, "libcgs_kernels.so")
+
+
+def load_kernels():
+    """Return the ctypes handle of libcgs_kernels.so or None if it is not built."""
+    global _kernels, _kernels_err
+    if _kernels is not None or _kernels_err is not None:
+        return _kernels
+    with _lock:
+        if _kernels is not None or _kernels_err is not None:
+            return _kernels
+        path = kernel_lib_path()
+        if not os.path.exists(path):
+            _kernels_err = f"{path} not built (run python build_native.py)"
+            return None
+        try:
+            # torch must be imported first so libamdhip64 is already resident with its symbols.
+            import torch  # noqa: F401
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+            _declare(lib)
+            _kernels = lib
+        except OSError as e:  # pragma: no cover - depends on the box
+            _kernels_err = str(e)
+            _kernels = None
+    return _kernels
+
+
+def kernels_error():
+    return _kernels_err
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_longlong
+_F = ctypes.c_float
+
+# name -> argtypes. Every launcher returns int (hipError_t) and takes the stream last.
+KERNEL_SIGNATURES = {
+    # y = GN(x + pre_add) (+SiLU); NHWC layout, x [N, HW, C]; ws = torch-allocated workspace
+    "cgs_groupnorm_nhwc_ws": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P],
+    "cgs_groupnorm_workspace": [_I, _I, _I],
+    # y = LN(x) over last dim; rows x C
+    "cgs_layernorm": [_P, _P, _P, _P, _I, _I, _F, _I, _P],
+    # flash attention forward (bf16): q,k,v,o + strides (elements) + shapes
+    "cgs_flash_attn_fwd": [_P, _P, _P, _P,
+                           _I, _I, _I, _I, _I,          # B, H, Sq, Sk, D
+                           _L, _L, _L,                  # q strides (b, s, h)
+                           _L, _L, _L,                  # k strides
+                           _L, _L, _L,                  # v strides
+                           _L, _L, _L,                  # o strides
+                           _F, _P, _I, _P],             # scale, key_mask(int8 [B,Sk] or null), causal, stream
+    # C[M,N] = A[M,K] @ W[N,K]^T (+bias) (+residual) | GEGLU epilogue; bf16 in/out, fp32 acc
+    "cgs_gemm_bf16": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
+    # out = a * gelu(g) where [a | g] = x rows of width 2*N
+    "cgs_geglu": [_P, _P, _I, _I, _I, _P],   # x [M, 2N] -> out [M, N], dtype
+    # fused CFG combine: out = u + (c - u) * scale   (fp32 or bf16 denoised)
+    "cgs_cfg_combine": [_P, _P, _P, _L, _F, _I, _P],
+    # Euler-ancestral / Euler update: x = x + d * dt (+ noise * s_up), d = (x - den)/sigma
+    "cgs_euler_step": [_P, _P, _P, _L, _F, _F, _F, _P],   # in place on x
+    # timestep sinusoidal embedding
+    "cgs_timestep_embedding": [_P, _P, _I, _I, _F, _I, _P],
+    # elementwise y = silu(x) (bf16)
+    "cgs_silu": [_P, _P, _L, _I, _P],
+    # NHWC nearest upsample x2
+    "cgs_upsample_nearest2x_nhwc": [_P, _P, _I, _I, _I, _I, _I, _P],
+    # conv implicit GEMM NHWC bf16: x[N,H,W,Cin], w[Cout,kh,kw,Cin], bias, residual, out
+    "cgs_conv2d_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+}
+
+
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong}
+
+
+def _declare(lib):
+    for name, argtypes in KERNEL_SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
+
+
+def has_kernel(name: str) -> bool:
+    lib = load_kernels()
+    return lib is not None and getattr(lib, name, None) is not None
+
+
+_runtime = None
+_runtime_err = None
+
+
+def load_runtime():
+    """Import the C++ runtime extension module (_cgs_runtime)."""
+    global _runtime, _runtime_err
+    if _runtime is not None or _runtime_err is not None:
+        return _runtime
+    import importlib.util
+    import sys
+    cands = glob.glob(os.path.join(LIB_DIR, "_cgs_runtime*.so"))
+    if not cands:
+        _runtime_err = "_cgs_runtime not built"
+        return None
+    try:
+        spec = importlib.util.spec_from_file_location("_cgs_runtime", cands[0])
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        sys.modules["_cgs_runtime"] = mod
+        _runtime = mod
+    except Exception as e:  # pragma: no cover
+        _runtime_err = str(e)
+    return _runtime
+
+
+def runtime_error():
+    return _runtime_err

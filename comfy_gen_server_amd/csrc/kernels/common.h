@@ -1,0 +1,88 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels of comfy_gen_server_amd.
+// Wave = 64 lanes. bf16 is handled as raw ushort with explicit RNE conversion so the kernels
+// never depend on host-side bf16 types.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#define CGS_EXPORT extern "C" __attribute__((visibility("default")))
+
+typedef unsigned short bf16_t;
+typedef uint16_t u16;
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+enum CgsDType { CGS_F32 = 0, CGS_BF16 = 1, CGS_F16 = 2 };
+
+__device__ __forceinline__ float bf2f(u16 v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+__device__ __forceinline__ u16 f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) {  // inf / nan: keep class
+    return (u16)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  }
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+
+__device__ __forceinline__ float h2f(u16 v) {
+  return __half2float(__ushort_as_half(v));
+}
+
+__device__ __forceinline__ u16 f2h(float f) {
+  return __half_as_ushort(__float2half(f));
+}
+
+template <int DT>
+__device__ __forceinline__ float ld_act(const u16* p) {
+  if constexpr (DT == CGS_BF16) return bf2f(*p);
+  else return h2f(*p);
+}
+
+template <int DT>
+__device__ __forceinline__ float cvt_in(u16 v) {
+  if constexpr (DT == CGS_BF16) return bf2f(v);
+  else return h2f(v);
+}
+
+template <int DT>
+__device__ __forceinline__ u16 cvt_out(float f) {
+  if constexpr (DT == CGS_BF16) return f2bf(f);
+  else return f2h(f);
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float gelu_f(float x) {  // exact erf GELU (torch default)
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective block remap (MI355X: 8 XCDs with private L2; blocks are dealt round-robin).
+// Consecutive logical tiles land on the same XCD so they share L2 panels.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return bid;
+  int q = nwg / nx, r = nwg % nx;
+  int x = bid % nx, i = bid / nx;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}

@@ -1,0 +1,162 @@
+// bf16 GEMM with fused epilogues for gfx950 (K01 Linear, K08 GEGLU, K15-style residual adds).
+//   C[M,N] = alpha * A[M,K] * W[N,K]^T (+ bias[N]) (+ residual[M,N])      (EPI_BIAS / EPI_RESIDUAL)
+//   GEGLU: W rows interleaved in 16-row groups [a0..a15 | g0..g15 | a16..]; out[M, N/2] = a*gelu(g)
+// Both operands are K-contiguous ("NT"), which is what nn.Linear weights and activations are.
+//
+// Structure: 128x128x64 block tile, 256 threads = 4 waves in 2x2, each wave 64x64 made of 4x4
+// v_mfma_f32_16x16x32_bf16 tiles (the 16x16 shape holds a higher clock than 32x32 under load,
+// MI355X_MICROARCH 'DVFS give-back' item 7). Register-staged global->LDS double buffer with the
+// next tile's global loads issued before the current tile's MFMAs (one barrier per K step).
+// LDS rows padded to 80 elements (160 B): conflict-free ds_read_b128 for the 16x16x32 operand
+// lane groups and conflict-free ds_write_b128. 1-D grid with the XCD-aware bijective remap so
+// neighbouring output tiles (sharing A / W panels) run on the same XCD L2.
+#include "common.h"
+
+#define G_BM 128
+#define G_BN 128
+#define G_BK 64
+#define G_LDW 80
+#define EPI_BIAS 1
+#define EPI_RESIDUAL 2
+#define EPI_GEGLU 4
+
+__global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) u16 As[2][G_BM * G_LDW];
+  __shared__ __attribute__((aligned(16))) u16 Ws[2][G_BN * G_LDW];
+
+  const int nwg = gridDim.x;
+  const int logical = xcd_remap(blockIdx.x, nwg);
+  const int tm = logical / tiles_n;
+  const int tn = logical % tiles_n;
+  const int m0 = tm * G_BM;
+  const int n0 = tn * G_BN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = (wave >> 1) * 64;
+  const int wn = (wave & 1) * 64;
+
+  // global -> register staging: 128 rows x 8 chunks(16B) = 1024 chunks per operand, 4 per thread
+  s16x8 ra[4], rw[4];
+  auto gload = [&](int kt) {
+    const int k0 = kt * G_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int idx = tid + i * 256;
+      int r = idx >> 3, c = (idx & 7) * 8;
+      int gk = k0 + c;
+      s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      int gm = m0 + r;
+      ra[i] = (gm < M && gk < K) ? *reinterpret_cast<const s16x8*>(A + gm * lda + gk) : z;
+      int gn = n0 + r;
+      rw[i] = (gn < N && gk < K) ? *reinterpret_cast<const s16x8*>(W + gn * ldw + gk) : z;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int idx = tid + i * 256;
+      int r = idx >> 3, c = (idx & 7) * 8;
+      *reinterpret_cast<s16x8*>(&As[buf][r * G_LDW + c]) = ra[i];
+      *reinterpret_cast<s16x8*>(&Ws[buf][r * G_LDW + c]) = rw[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + G_BK - 1) / G_BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int fr = lane & 15;
+  const int fk = (lane >> 4) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+#pragma unroll
+    for (int kk = 0; kk < G_BK / 32; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(&As[buf][(wm + i * 16 + fr) * G_LDW + kk * 32 + fk]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(&Ws[buf][(wn + j * 16 + fr) * G_LDW + kk * 32 + fk]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue. C layout (16x16x32): col = lane&15, row = (lane>>4)*4 + reg
+  const int er = (lane >> 4) * 4;
+  if (epi & EPI_GEGLU) {
+    const int NO = N >> 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        int ca = n0 + wn + (2 * jp) * 16 + fr;        // interleaved column of the "a" half
+        int cg = ca + 16;                             // matching gate column
+        int oc = (n0 + wn) / 2 + jp * 16 + fr;        // output column
+        if (cg >= N) continue;
+        float ba = 0.f, bg = 0.f;
+        if (epi & EPI_BIAS) { ba = bf2f(bias[ca]); bg = bf2f(bias[cg]); }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + i * 16 + er + r;
+          if (row < M) {
+            float a = acc[i][2 * jp][r] * alpha + ba;
+            float g = acc[i][2 * jp + 1][r] * alpha + bg;
+            C[row * ldc + oc] = f2bf(a * gelu_f(g));
+          }
+        }
+      }
+    }
+    (void)NO;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int col = n0 + wn + j * 16 + fr;
+    if (col >= N) continue;
+    float bv = (epi & EPI_BIAS) ? bf2f(bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm + i * 16 + er + r;
+        if (row < M) {
+          float v = acc[i][j][r] * alpha + bv;
+          if (epi & EPI_RESIDUAL) v += bf2f(R[row * ldr + col]);
+          C[row * ldc + col] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                             int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                             hipStream_t stream) {
+  if (K % 8 || lda % 8 || ldw % 8) return (int)hipErrorInvalidValue;
+  if ((epi & EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
+  int tiles_m = (M + G_BM - 1) / G_BM;
+  int tiles_n = (N + G_BN - 1) / G_BN;
+  long long nwg = (long long)tiles_m * tiles_n;
+  if (nwg == 0) return 0;
+  gemm_bf16_nt_kernel<<<(unsigned)nwg, 256, 0, stream>>>((const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias,
+                                                        (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+                                                        tiles_n);
+  return (int)hipGetLastError();
+}

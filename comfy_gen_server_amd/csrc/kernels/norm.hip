@@ -1,0 +1,312 @@
+// GroupNorm (+fused SiLU, +fused per-(n,c) pre-add) over NHWC activations, and LayerNorm.
+// K06 / K07 of SURVEY §2.4. Reference semantics: comfy/ldm/modules/diffusionmodules/openaimodel.py
+// ResBlock (GN -> SiLU -> conv, emb add before out_layers GN) and attention.py LayerNorms.
+//
+// GroupNorm = 3 small launches, every one fully coalesced on NHWC rows:
+//   1. gn_partial : block = (pixel chunk, n); each lane owns fixed 8-channel chunks of the row and
+//      accumulates shifted sums (shift = first pixel) -> per-wave (mean, M2) -> Chan combine over
+//      the 4 waves in LDS -> per-(n, block, c) partial.
+//   2. gn_finalize: one wave per (n, g) combines blocks x channels (Chan) -> mean/rstd -> per-(n,c)
+//      affine a, b (the pre-add shifts the channel mean only, so it folds into b).
+//   3. gn_apply   : y = x*a + b (+SiLU), 16-byte vectors.
+// LayerNorm: one wave per row, two-pass mean/var from registers, 16-byte vectors.
+#include "common.h"
+
+#define GN_THREADS 256
+#define GN_MAX_CHUNKS_PER_LANE 4   // C <= 64*4*8 = 2048 channels per row in registers
+
+static inline int gn_pix_per_block(int N, int HW) {
+  int target_blocks_per_n = (2048 + N - 1) / N;
+  int ppb = (HW + target_blocks_per_n - 1) / target_blocks_per_n;
+  if (ppb < 16) ppb = 16;
+  return ppb;
+}
+
+template <int DT>
+__global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, float* __restrict__ part,
+                                                               int HW, int C, int ppb, int nb) {
+  const int n = blockIdx.y;
+  const int blk = blockIdx.x;
+  const int p0 = blk * ppb;
+  const int p1 = min(HW, p0 + ppb);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nchunk = C >> 3;
+  float s1[GN_MAX_CHUNKS_PER_LANE][8], s2[GN_MAX_CHUNKS_PER_LANE][8], sh[GN_MAX_CHUNKS_PER_LANE][8];
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[k][j] = 0.f; s2[k][j] = 0.f; sh[k][j] = 0.f; }
+  const u16* xn = x + (size_t)n * HW * C;
+  bool first = true;
+  for (int p = p0 + wave; p < p1; p += 4) {
+    const u16* row = xn + (size_t)p * C;
+#pragma unroll
+    for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k) {
+      int ch = lane + 64 * k;
+      if (ch < nchunk) {
+        s16x8 v = *reinterpret_cast<const s16x8*>(row + ch * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float f = cvt_in<DT>((u16)v[j]);
+          if (first) sh[k][j] = f;
+          float d = f - sh[k][j];
+          s1[k][j] += d;
+          s2[k][j] += d * d;
+        }
+      }
+    }
+    first = false;
+    cnt++;
+  }
+  // per-wave (mean, M2) per channel -> LDS, then Chan-combine the 4 waves
+  extern __shared__ __attribute__((aligned(16))) float gn_smem[];
+  float* lmean = gn_smem;             // [4][C]
+  float* lm2 = gn_smem + 4 * C;       // [4][C]
+  __shared__ int lcnt[4];
+  if (lane == 0) lcnt[wave] = cnt;
+#pragma unroll
+  for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k) {
+    int ch = lane + 64 * k;
+    if (ch < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float m = 0.f, m2 = 0.f;
+        if (cnt > 0) {
+          m = sh[k][j] + s1[k][j] / cnt;
+          m2 = fmaxf(0.f, s2[k][j] - s1[k][j] * s1[k][j] / cnt);
+        }
+        lmean[wave * C + ch * 8 + j] = m;
+        lm2[wave * C + ch * 8 + j] = m2;
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += GN_THREADS) {
+    float n_a = 0.f, mean = 0.f, m2 = 0.f;
+    for (int w = 0; w < 4; ++w) {
+      float n_b = (float)lcnt[w];
+      if (n_b <= 0.f) continue;
+      float mb = lmean[w * C + c], m2b = lm2[w * C + c];
+      float nn = n_a + n_b;
+      float d = mb - mean;
+      mean += d * n_b / nn;
+      m2 += m2b + d * d * n_a * n_b / nn;
+      n_a = nn;
+    }
+    size_t o = (((size_t)n * nb + blk) * C + c) * 2;
+    part[o] = mean;
+    part[o + 1] = m2;
+  }
+}
+
+__global__ void gn_finalize_kernel(const float* __restrict__ part, const void* __restrict__ gamma,
+                                   const void* __restrict__ beta, const void* __restrict__ pre_add,
+                                   float* __restrict__ ab, int HW, int C, int G, int ppb, int nb, float eps,
+                                   int wdt) {
+  // one wave per (n, g); blockDim = 64
+  const int g = blockIdx.x;
+  const int n = blockIdx.y;
+  const int lane = threadIdx.x;
+  const int Cg = C / G;
+  const int items = Cg * nb;
+  float n_a = 0.f, mean = 0.f, m2 = 0.f;
+  for (int it = lane; it < items; it += 64) {
+    int b = it / Cg, cc = it % Cg;
+    int c = g * Cg + cc;
+    int p0 = b * ppb;
+    float n_b = (float)(min(HW, p0 + ppb) - p0);
+    if (n_b <= 0.f) continue;
+    size_t o = (((size_t)n * nb + b) * C + c) * 2;
+    float mb = part[o], m2b = part[o + 1];
+    if (pre_add) {
+      float e = (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
+                                  : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c])
+                                                     : ((const float*)pre_add)[n * C + c]);
+      mb += e;
+    }
+    float nn = n_a + n_b;
+    float d = mb - mean;
+    mean += d * n_b / nn;
+    m2 += m2b + d * d * n_a * n_b / nn;
+    n_a = nn;
+  }
+  // butterfly Chan-combine across the wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float n_b = __shfl_xor(n_a, o, 64);
+    float mb = __shfl_xor(mean, o, 64);
+    float m2b = __shfl_xor(m2, o, 64);
+    float nn = n_a + n_b;
+    if (nn > 0.f) {
+      float d = mb - mean;
+      mean += d * n_b / nn;
+      m2 += m2b + d * d * n_a * n_b / nn;
+      n_a = nn;
+    }
+  }
+  float var = m2 / fmaxf(n_a, 1.f);
+  float rstd = rsqrtf(var + eps);
+  for (int cc = lane; cc < Cg; cc += 64) {
+    int c = g * Cg + cc;
+    float gm = 1.f, bt = 0.f, e = 0.f;
+    if (gamma) gm = (wdt == CGS_BF16) ? bf2f(((const u16*)gamma)[c]) : (wdt == CGS_F16 ? h2f(((const u16*)gamma)[c]) : ((const float*)gamma)[c]);
+    if (beta) bt = (wdt == CGS_BF16) ? bf2f(((const u16*)beta)[c]) : (wdt == CGS_F16 ? h2f(((const u16*)beta)[c]) : ((const float*)beta)[c]);
+    if (pre_add) e = (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
+                                        : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c]) : ((const float*)pre_add)[n * C + c]);
+    float a = rstd * gm;
+    ab[((size_t)n * C + c) * 2] = a;
+    ab[((size_t)n * C + c) * 2 + 1] = (e - mean) * a + bt;
+  }
+}
+
+template <int DT, bool SILU>
+__global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y,
+                                                      const float* __restrict__ ab, long long total_chunks, int HW,
+                                                      int C) {
+  const int cpr = C >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_chunks;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long row = i / cpr;
+    int ch = (int)(i - row * cpr);
+    int n = (int)(row / HW);
+    s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
+    const float* abp = ab + ((size_t)n * C + ch * 8) * 2;
+    s16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = cvt_in<DT>((u16)v[j]) * abp[2 * j] + abp[2 * j + 1];
+      if (SILU) f = silu_f(f);
+      o[j] = (short)cvt_out<DT>(f);
+    }
+    reinterpret_cast<s16x8*>(y)[i] = o;
+  }
+}
+
+CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
+  int ppb = gn_pix_per_block(N, HW);
+  int nb = (HW + ppb - 1) / ppb;
+  return (long long)N * nb * C * 2 * 4 + (long long)N * C * 2 * 4 + 256;
+}
+
+// x, y: [N, HW, C] (NHWC); gamma/beta [C] in the activation dtype; pre_add [N, C] (act dtype) or null.
+// ws: workspace of cgs_groupnorm_workspace() bytes (torch-allocated so it is graph-capturable).
+CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,
+                                     void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
+                                     hipStream_t stream) {
+  if (C % 8 || C > 2048 || C % G) return (int)hipErrorInvalidValue;
+  int ppb = gn_pix_per_block(N, HW);
+  int nb = (HW + ppb - 1) / ppb;
+  float* part = (float*)ws;
+  float* ab = part + (size_t)N * nb * C * 2;
+  dim3 g1(nb, N);
+  if (dtype == CGS_BF16)
+    gn_partial_kernel<CGS_BF16><<<g1, GN_THREADS, 8 * C * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb);
+  else
+    gn_partial_kernel<CGS_F16><<<g1, GN_THREADS, 8 * C * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb);
+  gn_finalize_kernel<<<dim3(G, N), 64, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
+  long long chunks = (long long)N * HW * (C / 8);
+  long long nbk = (chunks + 255) / 256;
+  int blocks = (int)(nbk < 8192 ? nbk : 8192);
+  if (dtype == CGS_BF16) {
+    if (silu) gn_apply_kernel<CGS_BF16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
+    else gn_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
+  } else {
+    if (silu) gn_apply_kernel<CGS_F16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
+    else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
+  }
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// LayerNorm over the last dim; one wave per row.
+// ------------------------------------------------------------------------------------------------
+#define LN_MAXK 8  // chunks of 8 per lane -> C <= 4096 in registers
+
+template <int DT>
+__global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ x, u16* __restrict__ y,
+                                                       const u16* __restrict__ w, const u16* __restrict__ b, int rows,
+                                                       int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = C >> 3;
+  const u16* xr = x + (size_t)row * C;
+  float v[LN_MAXK][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    int ch = lane + 64 * k;
+    if (ch < nch) {
+      s16x8 t = reinterpret_cast<const s16x8*>(xr)[ch];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[k][j] = cvt_in<DT>((u16)t[j]); s += v[k][j]; }
+    }
+  }
+  float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    int ch = lane + 64 * k;
+    if (ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float d = v[k][j] - mean; q += d * d; }
+    }
+  }
+  float rstd = rsqrtf(wave_sum(q) / C + eps);
+  u16* yr = y + (size_t)row * C;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    int ch = lane + 64 * k;
+    if (ch < nch) {
+      s16x8 wv = reinterpret_cast<const s16x8*>(w)[ch];
+      s16x8 bv;
+      if (b) bv = reinterpret_cast<const s16x8*>(b)[ch];
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float f = (v[k][j] - mean) * rstd * cvt_in<DT>((u16)wv[j]) + (b ? cvt_in<DT>((u16)bv[j]) : 0.f);
+        o[j] = (short)cvt_out<DT>(f);
+      }
+      reinterpret_cast<s16x8*>(yr)[ch] = o;
+    }
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void layernorm_big_kernel(const u16* __restrict__ x, u16* __restrict__ y,
+                                                           const u16* __restrict__ w, const u16* __restrict__ b,
+                                                           int rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const u16* xr = x + (size_t)row * C;
+  float s = 0.f;
+  for (int i = lane; i < C; i += 64) s += cvt_in<DT>(xr[i]);
+  float mean = wave_sum(s) / C;
+  float q = 0.f;
+  for (int i = lane; i < C; i += 64) { float d = cvt_in<DT>(xr[i]) - mean; q += d * d; }
+  float rstd = rsqrtf(wave_sum(q) / C + eps);
+  u16* yr = y + (size_t)row * C;
+  for (int i = lane; i < C; i += 64)
+    yr[i] = cvt_out<DT>((cvt_in<DT>(xr[i]) - mean) * rstd * cvt_in<DT>(w[i]) + (b ? cvt_in<DT>(b[i]) : 0.f));
+}
+
+CGS_EXPORT int cgs_layernorm(const void* x, void* y, const void* w, const void* b, int rows, int C, float eps,
+                             int dtype, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4);
+  if (C <= 64 * 8 * LN_MAXK) {
+    if (dtype == CGS_BF16)
+      layernorm_kernel<CGS_BF16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
+    else
+      layernorm_kernel<CGS_F16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
+  } else {
+    if (dtype == CGS_BF16)
+      layernorm_big_kernel<CGS_BF16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
+    else
+      layernorm_big_kernel<CGS_F16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,263 @@
+"""Transformer blocks of the latent-diffusion UNet.
+
+Behavioural parity with ``comfy/ldm/modules/attention.py:386-640`` (CrossAttention,
+BasicTransformerBlock incl. every ``transformer_options`` patch point, SpatialTransformer).
+MI355X design:
+  * self-attention q/k/v come from ONE fused GEMM (weight rows [Wq;Wk;Wv]); the flash kernel
+    reads q, k, v as strided views of that buffer — no head split/permute copies;
+  * cross-attention k/v are one fused GEMM over the context; within a sampling run the context
+    is constant, so its k/v are cached per (context tensor, block) (``ctx_cache``);
+  * residual adds ``x + attn(...)``/``x + ff(...)`` are fused into the out-projection GEMM epilogue;
+  * GEGLU's gate is fused into the projection GEMM epilogue (interleaved weight rows).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import DerivedMixin, GroupNorm, LayerNorm, Linear, Conv2d
+
+
+class _Seq(nn.Module):
+    """nn.Sequential-compatible container whose forward forwards extra kwargs to element 0."""
+
+    def __init__(self, *mods):
+        super().__init__()
+        for i, m in enumerate(mods):
+            if m is not None:
+                self.add_module(str(i), m)
+
+    def __getitem__(self, i):
+        return self._modules[str(i)]
+
+
+class CrossAttention(nn.Module, DerivedMixin):
+    def __init__(self, query_dim, context_dim=None, heads=8, dim_head=64, dtype=None, device=None):
+        super().__init__()
+        inner = heads * dim_head
+        context_dim = query_dim if context_dim is None else context_dim
+        self.heads = heads
+        self.dim_head = dim_head
+        self.is_cross = context_dim != query_dim
+        self.to_q = Linear(query_dim, inner, bias=False, dtype=dtype, device=device)
+        self.to_k = Linear(context_dim, inner, bias=False, dtype=dtype, device=device)
+        self.to_v = Linear(context_dim, inner, bias=False, dtype=dtype, device=device)
+        self.to_out = _Seq(Linear(inner, query_dim, dtype=dtype, device=device))
+
+    def _w_qkv(self):
+        return self._derived_get("w_qkv", lambda: torch.cat(
+            [self.to_q.weight, self.to_k.weight, self.to_v.weight], 0).contiguous())
+
+    def _w_kv(self):
+        return self._derived_get("w_kv", lambda: torch.cat([self.to_k.weight, self.to_v.weight], 0).contiguous())
+
+    def project_kv(self, context, value=None, ctx_cache=None, cache_key=None):
+        """k, v for ``context`` (and optional separate ``value`` source)."""
+        if value is not None and value is not context:
+            return self.to_k(context), self.to_v(value)
+        if ctx_cache is not None and cache_key is not None:
+            hit = ctx_cache.get(cache_key)
+            if hit is not None and hit[0] is context:
+                return hit[1], hit[2]
+        inner = self.heads * self.dim_head
+        if context.dtype == self.to_k.weight.dtype and context.device == self.to_k.weight.device:
+            kv = ops.linear(context, self._w_kv())
+            k, v = kv[..., :inner], kv[..., inner:]
+        else:
+            k, v = self.to_k(context), self.to_v(context)
+        if ctx_cache is not None and cache_key is not None:
+            ctx_cache[cache_key] = (context, k, v)
+        return k, v
+
+    def forward(self, x, context=None, value=None, mask=None, residual=None, ctx_cache=None, cache_key=None):
+        inner = self.heads * self.dim_head
+        if context is None and value is None and x.dtype == self.to_q.weight.dtype \
+                and x.device == self.to_q.weight.device:
+            qkv = ops.linear(x, self._w_qkv())
+            q, k, v = qkv[..., :inner], qkv[..., inner:2 * inner], qkv[..., 2 * inner:]
+        else:
+            q = self.to_q(x)
+            ctx = x if context is None else context
+            k, v = self.project_kv(ctx, value, ctx_cache, cache_key)
+        o = ops.attention(q, k, v, self.heads, mask=mask)
+        return self.to_out[0](o, residual=residual)
+
+
+class GEGLU(nn.Module, DerivedMixin):
+    def __init__(self, dim_in, dim_out, dtype=None, device=None):
+        super().__init__()
+        self.proj = Linear(dim_in, dim_out * 2, dtype=dtype, device=device)
+
+    def forward(self, x):
+        if x.is_cuda and x.dtype == self.proj.weight.dtype:
+            w = self._derived_get("w_il", lambda: ops.core.geglu_interleave(self.proj.weight))
+            b = self._derived_get("b_il", lambda: ops.core.geglu_interleave(self.proj.bias))
+            return ops.linear_geglu(x, w, b)
+        h = self.proj(x)
+        a, g = h.chunk(2, dim=-1)
+        return a * torch.nn.functional.gelu(g)
+
+
+class GELUProj(nn.Module):
+    def __init__(self, dim_in, dim_out, dtype=None, device=None):
+        super().__init__()
+        self.proj = Linear(dim_in, dim_out, dtype=dtype, device=device)
+
+    def forward(self, x):
+        return torch.nn.functional.gelu(self.proj(x))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, dim_out=None, mult=4, glu=True, dtype=None, device=None):
+        super().__init__()
+        inner = int(dim * mult)
+        dim_out = dim if dim_out is None else dim_out
+        proj = GEGLU(dim, inner, dtype=dtype, device=device) if glu else GELUProj(dim, inner, dtype=dtype, device=device)
+        self.net = _Seq(proj, nn.Identity(), Linear(inner, dim_out, dtype=dtype, device=device))
+
+    def forward(self, x, residual=None):
+        return self.net[2](self.net[0](x), residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, n_heads, d_head, context_dim=None, gated_ff=True, disable_self_attn=False,
+                 dtype=None, device=None):
+        super().__init__()
+        self.disable_self_attn = disable_self_attn
+        self.n_heads = n_heads
+        self.d_head = d_head
+        self.attn1 = CrossAttention(dim, context_dim if disable_self_attn else None, n_heads, d_head,
+                                    dtype=dtype, device=device)
+        self.ff = FeedForward(dim, glu=gated_ff, dtype=dtype, device=device)
+        self.attn2 = CrossAttention(dim, context_dim, n_heads, d_head, dtype=dtype, device=device)
+        self.norm1 = LayerNorm(dim, dtype=dtype, device=device)
+        self.norm2 = LayerNorm(dim, dtype=dtype, device=device)
+        self.norm3 = LayerNorm(dim, dtype=dtype, device=device)
+
+    def forward(self, x, context=None, transformer_options=None):
+        to = transformer_options or {}
+        patches = to.get("patches", {})
+        replace = to.get("patches_replace", {})
+        if not patches and not replace:
+            return self._forward_fast(x, context, to)
+        return self._forward_patched(x, context, to, patches, replace)
+
+    def _forward_fast(self, x, context, to):
+        """Hook-free path: residual adds fused into the out-projection / FF-out GEMM epilogues."""
+        cache = to.get("ctx_cache")
+        key = id(self)
+        n = self.norm1(x)
+        if self.disable_self_attn:
+            x = self.attn1(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 1))
+        else:
+            x = self.attn1(n, residual=x)
+        n = self.norm2(x)
+        x = self.attn2(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 2))
+        return self.ff(self.norm3(x), residual=x)
+
+    def _forward_patched(self, x, context, to, patches, replace):
+        extra = {k: v for k, v in to.items() if k not in ("patches", "patches_replace")}
+        extra["n_heads"] = self.n_heads
+        extra["dim_head"] = self.d_head
+        block = to.get("block")
+        block_index = to.get("block_index", 0)
+        tblock = (block[0], block[1], block_index) if block is not None else None
+
+        n = self.norm1(x)
+        ctx1 = context if self.disable_self_attn else None
+        val1 = None
+        if "attn1_patch" in patches:
+            if ctx1 is None:
+                ctx1 = n
+            val1 = ctx1
+            for p in patches["attn1_patch"]:
+                n, ctx1, val1 = p(n, ctx1, val1, extra)
+        r1 = replace.get("attn1", {})
+        key1 = tblock if tblock in r1 else block
+        if key1 in r1:
+            if ctx1 is None:
+                ctx1 = n
+                val1 = n
+            q = self.attn1.to_q(n)
+            k = self.attn1.to_k(ctx1)
+            v = self.attn1.to_v(val1)
+            n = self.attn1.to_out[0](r1[key1](q, k, v, extra))
+        else:
+            n = self.attn1(n, context=ctx1, value=val1)
+        for p in patches.get("attn1_output_patch", []):
+            n = p(n, extra)
+        x = x + n
+        for p in patches.get("middle_patch", []):
+            x = p(x, extra)
+
+        n = self.norm2(x)
+        ctx2 = context
+        val2 = None
+        if "attn2_patch" in patches:
+            val2 = ctx2
+            for p in patches["attn2_patch"]:
+                n, ctx2, val2 = p(n, ctx2, val2, extra)
+        r2 = replace.get("attn2", {})
+        key2 = tblock if tblock in r2 else block
+        if key2 in r2:
+            if val2 is None:
+                val2 = ctx2
+            q = self.attn2.to_q(n)
+            k = self.attn2.to_k(ctx2)
+            v = self.attn2.to_v(val2)
+            n = self.attn2.to_out[0](r2[key2](q, k, v, extra))
+        else:
+            n = self.attn2(n, context=ctx2, value=val2)
+        for p in patches.get("attn2_output_patch", []):
+            n = p(n, extra)
+        x = x + n
+        return self.ff(self.norm3(x), residual=x)
+
+
+class SpatialTransformer(nn.Module):
+    def __init__(self, in_channels, n_heads, d_head, depth=1, context_dim=None, disable_self_attn=False,
+                 use_linear=False, dtype=None, device=None):
+        super().__init__()
+        if not isinstance(context_dim, (list, tuple)):
+            context_dim = [context_dim] * depth
+        inner = n_heads * d_head
+        self.in_channels = in_channels
+        self.use_linear = use_linear
+        self.norm = GroupNorm(32, in_channels, eps=1e-6, dtype=dtype, device=device)
+        if use_linear:
+            self.proj_in = Linear(in_channels, inner, dtype=dtype, device=device)
+            self.proj_out = Linear(inner, in_channels, dtype=dtype, device=device)
+        else:
+            self.proj_in = Conv2d(in_channels, inner, 1, dtype=dtype, device=device)
+            self.proj_out = Conv2d(inner, in_channels, 1, dtype=dtype, device=device)
+        self.transformer_blocks = nn.ModuleList([
+            BasicTransformerBlock(inner, n_heads, d_head, context_dim=context_dim[d],
+                                  disable_self_attn=disable_self_attn, dtype=dtype, device=device)
+            for d in range(depth)])
+
+    def forward(self, x, context=None, transformer_options=None):
+        to = transformer_options if transformer_options is not None else {}
+        if not isinstance(context, list):
+            context = [context] * len(self.transformer_blocks)
+        b, c, h, w = x.shape
+        x_in = x
+        x = self.norm(x)
+        if not self.use_linear:
+            x = self.proj_in(x)
+        # NHWC storage makes this a view on the device
+        x = x.permute(0, 2, 3, 1).reshape(b, h * w, -1)
+        if self.use_linear:
+            x = self.proj_in(x)
+        for i, blk in enumerate(self.transformer_blocks):
+            to["block_index"] = i
+            x = blk(x, context=context[i], transformer_options=to)
+        if self.use_linear:
+            res = x_in.permute(0, 2, 3, 1).reshape(b, h * w, c)
+            if res.is_contiguous():
+                x = self.proj_out(x, residual=res)   # fused "+ x_in"
+                return x.reshape(b, h, w, c).permute(0, 3, 1, 2)
+            x = self.proj_out(x)
+            return x.reshape(b, h, w, c).permute(0, 3, 1, 2) + x_in
+        x = x.reshape(b, h, w, -1).permute(0, 3, 1, 2)
+        return self.proj_out(x, residual=x_in)

@@ -1,0 +1,256 @@
+"""Latent-diffusion UNet for SD1.x / SD2.x / SDXL (+ refiner, SSD-1B, Vega, KOALA, IP2P, x4).
+
+Behavioural parity with ``comfy/ldm/modules/diffusionmodules/openaimodel.py:366-890``
+(UNetModel: time/label embeddings, input/middle/output blocks with skip concat, ControlNet
+residual injection ``apply_control`` at :356-364, patch hooks input_block_patch /
+input_block_patch_after_skip / output_block_patch at :852-877, transformer_options block
+addressing at :828-870). State-dict keys are identical to ldm checkpoints.
+
+MI355X design choices:
+  * activations stay NHWC (channels_last) for the whole forward on the device;
+  * ResBlock: GroupNorm+SiLU is one kernel; the timestep-embedding add ``h + emb[..., None, None]``
+    is folded into the second GroupNorm (per-(n, c) pre-add), and the skip connection add is
+    fused into the last conv's epilogue;
+  * SiLU(emb) is computed once per forward and shared by every ResBlock;
+  * all embedding projections (time/label/ResBlock emb layers) are host-launch-bound at
+    M = batch, so the forward is meant to be replayed from a hipGraph (``runtime/graphs.py``).
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .attention import SpatialTransformer, _Seq
+from .layers import Conv2d, GroupNorm, Linear
+
+
+class ResBlock(nn.Module):
+    def __init__(self, channels, emb_channels, out_channels=None, dtype=None, device=None,
+                 kernel_size=3, skip_t_emb=False):
+        super().__init__()
+        out_channels = out_channels or channels
+        self.channels = channels
+        self.out_channels = out_channels
+        self.skip_t_emb = skip_t_emb
+        pad = kernel_size // 2
+        self.in_layers = _Seq(GroupNorm(32, channels, dtype=dtype, device=device), nn.SiLU(),
+                              Conv2d(channels, out_channels, kernel_size, padding=pad, dtype=dtype, device=device))
+        if not skip_t_emb:
+            self.emb_layers = _Seq(nn.SiLU(), Linear(emb_channels, out_channels, dtype=dtype, device=device))
+        self.out_layers = _Seq(GroupNorm(32, out_channels, dtype=dtype, device=device), nn.SiLU(), nn.Dropout(0.0),
+                               Conv2d(out_channels, out_channels, kernel_size, padding=pad, dtype=dtype, device=device))
+        if out_channels == channels:
+            self.skip_connection = nn.Identity()
+        else:
+            self.skip_connection = Conv2d(channels, out_channels, 1, dtype=dtype, device=device)
+
+    def forward(self, x, emb_silu, transformer_options=None):
+        h = self.in_layers[0](x, silu=True)
+        h = self.in_layers[2](h)
+        pre = None
+        if not self.skip_t_emb and emb_silu is not None:
+            pre = self.emb_layers[1](emb_silu).to(h.dtype)          # [B, C]
+        h = ops.group_norm(h, 32, self.out_layers[0].weight, self.out_layers[0].bias,
+                           self.out_layers[0].eps, silu=True, pre_add=pre)
+        skip = x if isinstance(self.skip_connection, nn.Identity) else self.skip_connection(x)
+        return self.out_layers[3](h, residual=skip)
+
+
+class Downsample(nn.Module):
+    def __init__(self, channels, out_channels=None, dtype=None, device=None):
+        super().__init__()
+        self.op = Conv2d(channels, out_channels or channels, 3, stride=2, padding=1, dtype=dtype, device=device)
+
+    def forward(self, x, *a, **k):
+        return self.op(x)
+
+
+class Upsample(nn.Module):
+    def __init__(self, channels, out_channels=None, dtype=None, device=None):
+        super().__init__()
+        self.conv = Conv2d(channels, out_channels or channels, 3, padding=1, dtype=dtype, device=device)
+
+    def forward(self, x, *a, output_shape=None, **k):
+        if output_shape is not None and (output_shape[2] != 2 * x.shape[2] or output_shape[3] != 2 * x.shape[3]):
+            x = torch.nn.functional.interpolate(x, size=output_shape[2:], mode="nearest")
+        else:
+            x = ops.upsample_nearest2x(x)
+        return self.conv(x)
+
+
+class TimestepEmbedSequential(nn.ModuleList):
+    def forward(self, x, emb_silu, context, transformer_options, output_shape=None):
+        for layer in self:
+            if isinstance(layer, ResBlock):
+                x = layer(x, emb_silu, transformer_options)
+            elif isinstance(layer, SpatialTransformer):
+                x = layer(x, context, transformer_options)
+                if "transformer_index" in transformer_options:
+                    transformer_options["transformer_index"] += 1
+            elif isinstance(layer, Upsample):
+                x = layer(x, output_shape=output_shape)
+            else:
+                x = layer(x)
+        return x
+
+
+def _apply_control(h, control, name):
+    if control is not None and name in control and len(control[name]) > 0:
+        ctrl = control[name].pop()
+        if ctrl is not None:
+            if ctrl.shape == h.shape:
+                h = h + ctrl.to(h.dtype)
+            else:
+                logging.warning("warning control could not be applied %s %s", h.shape, ctrl.shape)
+    return h
+
+
+class UNetModel(nn.Module):
+    def __init__(self, in_channels=4, model_channels=320, out_channels=4, num_res_blocks=2,
+                 channel_mult=(1, 2, 4, 4), transformer_depth=1, transformer_depth_middle=None,
+                 transformer_depth_output=None, context_dim=None, num_heads=-1, num_head_channels=-1,
+                 use_linear_in_transformer=False, adm_in_channels=None, num_classes=None,
+                 disable_self_attentions=None, use_temporal_attention=False, dtype=torch.float32,
+                 device=None, **unused):
+        super().__init__()
+        nl = len(channel_mult)
+        if isinstance(num_res_blocks, int):
+            num_res_blocks = [num_res_blocks] * nl
+        if isinstance(transformer_depth, int):
+            transformer_depth = [transformer_depth] * (nl * max(num_res_blocks))
+        transformer_depth = list(transformer_depth)
+        if transformer_depth_output is None:
+            transformer_depth_output = []
+            for lvl in range(nl):
+                d = transformer_depth[lvl * num_res_blocks[lvl]] if lvl * num_res_blocks[lvl] < len(transformer_depth) else 0
+                transformer_depth_output += [d] * (num_res_blocks[lvl] + 1)
+        transformer_depth_output = list(transformer_depth_output)
+        if transformer_depth_middle is None:
+            transformer_depth_middle = transformer_depth[-1]
+        self.dtype = dtype
+        self.in_channels = in_channels
+        self.model_channels = model_channels
+        self.out_channels = out_channels
+        self.num_classes = num_classes
+        ted = model_channels * 4
+
+        def heads_for(ch):
+            if num_head_channels == -1:
+                return num_heads, ch // num_heads
+            return ch // num_head_channels, num_head_channels
+
+        def dsa(i):
+            return bool(disable_self_attentions[i]) if disable_self_attentions is not None else False
+
+        kw = dict(dtype=dtype, device=device)
+        self.time_embed = _Seq(Linear(model_channels, ted, **kw), nn.SiLU(), Linear(ted, ted, **kw))
+        if num_classes is not None:
+            if num_classes == "sequential":
+                self.label_emb = _Seq(_Seq(Linear(adm_in_channels, ted, **kw), nn.SiLU(), Linear(ted, ted, **kw)))
+            elif num_classes == "continuous":
+                self.label_emb = nn.Linear(1, ted)
+            else:
+                self.label_emb = nn.Embedding(num_classes, ted)
+
+        self.input_blocks = nn.ModuleList([TimestepEmbedSequential([Conv2d(in_channels, model_channels, 3, padding=1, **kw)])])
+        chans = [model_channels]
+        ch = model_channels
+        td = list(transformer_depth)
+        for level, mult in enumerate(channel_mult):
+            for _ in range(num_res_blocks[level]):
+                layers = [ResBlock(ch, ted, mult * model_channels, **kw)]
+                ch = mult * model_channels
+                nt = td.pop(0) if td else 0
+                if nt > 0:
+                    h, dh = heads_for(ch)
+                    layers.append(SpatialTransformer(ch, h, dh, depth=nt, context_dim=context_dim,
+                                                     disable_self_attn=dsa(level), use_linear=use_linear_in_transformer, **kw))
+                self.input_blocks.append(TimestepEmbedSequential(layers))
+                chans.append(ch)
+            if level != nl - 1:
+                self.input_blocks.append(TimestepEmbedSequential([Downsample(ch, ch, **kw)]))
+                chans.append(ch)
+
+        self.middle_block = None
+        if transformer_depth_middle >= -1:
+            mid = [ResBlock(ch, ted, ch, **kw)]
+            if transformer_depth_middle >= 0:
+                h, dh = heads_for(ch)
+                mid += [SpatialTransformer(ch, h, dh, depth=transformer_depth_middle, context_dim=context_dim,
+                                           disable_self_attn=False, use_linear=use_linear_in_transformer, **kw),
+                        ResBlock(ch, ted, ch, **kw)]
+            self.middle_block = TimestepEmbedSequential(mid)
+
+        self.output_blocks = nn.ModuleList([])
+        tdo = list(transformer_depth_output)
+        for level, mult in list(enumerate(channel_mult))[::-1]:
+            for i in range(num_res_blocks[level] + 1):
+                ich = chans.pop()
+                layers = [ResBlock(ch + ich, ted, model_channels * mult, **kw)]
+                ch = model_channels * mult
+                nt = tdo.pop() if tdo else 0
+                if nt > 0:
+                    h, dh = heads_for(ch)
+                    layers.append(SpatialTransformer(ch, h, dh, depth=nt, context_dim=context_dim,
+                                                     disable_self_attn=dsa(level), use_linear=use_linear_in_transformer, **kw))
+                if level and i == num_res_blocks[level]:
+                    layers.append(Upsample(ch, ch, **kw))
+                self.output_blocks.append(TimestepEmbedSequential(layers))
+        self.out = _Seq(GroupNorm(32, ch, **kw), nn.SiLU(), Conv2d(model_channels, out_channels, 3, padding=1, **kw))
+
+    # ------------------------------------------------------------------------------------------
+    def forward(self, x, timesteps=None, context=None, y=None, control=None, transformer_options=None, **kwargs):
+        to = transformer_options if transformer_options is not None else {}
+        to["original_shape"] = list(x.shape)
+        to["transformer_index"] = 0
+        patches = to.get("patches", {})
+        if control is not None:  # never mutate the caller's lists
+            control = {k: list(v) for k, v in control.items()}
+        dt = self.dtype
+        if x.is_cuda:
+            x = x.to(dt).contiguous(memory_format=torch.channels_last)
+        else:
+            x = x.to(dt)
+        if context is not None:
+            context = context.to(dt)
+        t_emb = ops.timestep_embedding(timesteps, self.model_channels).to(dt)
+        emb = self.time_embed[2](ops.silu(self.time_embed[0](t_emb)))
+        if self.num_classes is not None:
+            assert y is not None and y.shape[0] == x.shape[0]
+            le = self.label_emb[0]
+            emb = le[2](ops.silu(le[0](y.to(dt))), residual=emb)
+        emb_silu = ops.silu(emb)
+
+        hs = []
+        h = x
+        for i, mod in enumerate(self.input_blocks):
+            to["block"] = ("input", i)
+            h = mod(h, emb_silu, context, to)
+            h = _apply_control(h, control, "input")
+            for p in patches.get("input_block_patch", []):
+                h = p(h, to)
+            hs.append(h)
+            for p in patches.get("input_block_patch_after_skip", []):
+                h = p(h, to)
+
+        to["block"] = ("middle", 0)
+        if self.middle_block is not None:
+            h = self.middle_block(h, emb_silu, context, to)
+        h = _apply_control(h, control, "middle")
+
+        for i, mod in enumerate(self.output_blocks):
+            to["block"] = ("output", i)
+            hsp = hs.pop()
+            hsp = _apply_control(hsp, control, "output")
+            for p in patches.get("output_block_patch", []):
+                h, hsp = p(h, hsp, to)
+            h = torch.cat([h, hsp], dim=1)
+            if x.is_cuda:
+                h = h.contiguous(memory_format=torch.channels_last)
+            out_shape = hs[-1].shape if hs else None
+            h = mod(h, emb_silu, context, to, output_shape=out_shape)
+        h = self.out[0](h, silu=True)
+        return self.out[2](h)

@@ -1,0 +1,19 @@
+"""Op layer: the compute backend of every model in ``models/``.
+
+Each op has two implementations:
+  * ``hip``   — hand-written gfx950 kernels from ``csrc/kernels`` (bf16 activations, fp32 accumulate,
+                NHWC layout for image tensors). Used for every tensor on a ROCm device.
+  * ``torch`` — a plain PyTorch fp32 reference used on the CPU (tests, plumbing slice) and as the
+                numerics oracle for the kernel tests.
+
+Reference call sites this replaces: ``comfy/ops.py:39-163`` (casting ops),
+``comfy/ldm/modules/attention.py:88-383`` (attention backends: basic / sub-quad / split /
+xformers / SDPA) — on MI355X all of them collapse to one LDS-tiled MFMA flash-attention kernel.
+"""
+from .dispatch import (  # noqa: F401
+    backend_for, set_backend_override, native_required, NativeMissingError, stats, reset_stats,
+)
+from .core import (  # noqa: F401
+    linear, linear_geglu, attention, group_norm, layer_norm, conv2d, silu, gelu,
+    upsample_nearest2x, timestep_embedding, cfg_combine, euler_step,
+)

@@ -1,0 +1,387 @@
+"""Op implementations: HIP launchers (device) and fp32 torch references (CPU / oracle).
+
+Tensor conventions
+  * token tensors: ``[B, S, C]`` with unit stride on C.
+  * image tensors on the device: logical NCHW, physically NHWC (``torch.channels_last``), so a
+    SpatialTransformer's ``b c h w -> b (h w) c`` is a free view and GroupNorm / conv kernels read
+    rows of C contiguously.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+from .dispatch import backend_for, count
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+EPI_BIAS = 1
+EPI_RESIDUAL = 2
+EPI_GEGLU = 4
+EPI_SILU_IN = 8   # reserved
+
+
+def _stream():
+    return ctypes_stream(torch.cuda.current_stream())
+
+
+def ctypes_stream(s):
+    return s.cuda_stream
+
+
+def _lib():
+    return _native.load_kernels()
+
+
+def _check(err: int, name: str):
+    if err != 0:
+        raise RuntimeError(f"{name} failed with hipError {err}")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+# ----------------------------------------------------------------------------------------------
+# GEMM family
+# ----------------------------------------------------------------------------------------------
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
+           residual: torch.Tensor | None = None) -> torch.Tensor:
+    """y = x @ weight^T (+ bias) (+ residual). ``residual`` has y's shape (fused epilogue add)."""
+    be = backend_for("gemm", x, "cgs_gemm_bf16")
+    if be == "hip" and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
+        count("gemm", "hip")
+        K = x.shape[-1]
+        N = weight.shape[0]
+        a = x.reshape(-1, K)
+        if a.stride(-1) != 1 or (a.shape[0] > 1 and a.stride(0) < K):
+            a = a.contiguous()
+        M = a.shape[0]
+        out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+        epi = 0
+        r = None
+        if bias is not None:
+            epi |= EPI_BIAS
+        if residual is not None:
+            epi |= EPI_RESIDUAL
+            r = residual.reshape(M, N)
+            if not r.is_contiguous():
+                r = r.contiguous()
+        w = weight if weight.is_contiguous() else weight.contiguous()
+        _check(_lib().cgs_gemm_bf16(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
+                                    M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
+                                    _stream()), "cgs_gemm_bf16")
+        return out.view(*x.shape[:-1], N)
+    count("gemm", "torch" if be == "torch" else "lib")
+    if be == "torch":
+        y = F.linear(x.float(), weight.float(), None if bias is None else bias.float())
+        if residual is not None:
+            y = y + residual.float()
+        return y.to(x.dtype)
+    y = F.linear(x, weight, bias)
+    if residual is not None:
+        y = y + residual
+    return y
+
+
+def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    """GEGLU (comfy/ldm/modules/attention.py:56-63): [a | g] = x W^T + b ; out = a * gelu(g).
+
+    The device path fuses the gate into the GEMM epilogue; it needs the weight rows interleaved
+    in 16-row groups [a0..a15, g0..g15, a16..] (``geglu_interleave``) — models keep that copy.
+    """
+    be = backend_for("gemm", x, "cgs_gemm_bf16")
+    N2 = weight.shape[0]
+    if be == "hip" and x.dtype == torch.bfloat16:
+        count("gemm_geglu", "hip")
+        K = x.shape[-1]
+        a = x.reshape(-1, K)
+        if not a.is_contiguous():
+            a = a.contiguous()
+        M = a.shape[0]
+        out = torch.empty((M, N2 // 2), device=x.device, dtype=x.dtype)
+        epi = EPI_GEGLU | (EPI_BIAS if bias is not None else 0)
+        _check(_lib().cgs_gemm_bf16(a.data_ptr(), weight.data_ptr(), out.data_ptr(), _ptr(bias), None,
+                                    M, N2, K, K, K, N2 // 2, 0, epi, 1.0, _stream()), "cgs_gemm_bf16")
+        return out.view(*x.shape[:-1], N2 // 2)
+    count("gemm_geglu", be)
+    # reference path expects the *interleaved* weight too, undo it
+    w = geglu_deinterleave(weight)
+    b = None if bias is None else geglu_deinterleave(bias)
+    if be == "torch":
+        h = F.linear(x.float(), w.float(), None if b is None else b.float())
+        a, g = h.chunk(2, dim=-1)
+        return (a * F.gelu(g)).to(x.dtype)
+    h = F.linear(x, w, b)
+    a, g = h.chunk(2, dim=-1)
+    return a * F.gelu(g)
+
+
+GEGLU_GROUP = 16
+
+
+def geglu_interleave(w: torch.Tensor) -> torch.Tensor:
+    """[a ; g] (2N rows) -> rows interleaved in groups of 16: a[0:16], g[0:16], a[16:32], ..."""
+    n2 = w.shape[0]
+    n = n2 // 2
+    a, g = w[:n], w[n:]
+    shp = (n // GEGLU_GROUP, GEGLU_GROUP) + tuple(w.shape[1:])
+    return torch.stack([a.reshape(shp), g.reshape(shp)], dim=1).reshape(w.shape).contiguous()
+
+
+def geglu_deinterleave(w: torch.Tensor) -> torch.Tensor:
+    n2 = w.shape[0]
+    shp = (n2 // (2 * GEGLU_GROUP), 2, GEGLU_GROUP) + tuple(w.shape[1:])
+    v = w.reshape(shp)
+    a = v[:, 0].reshape((n2 // 2,) + tuple(w.shape[1:]))
+    g = v[:, 1].reshape((n2 // 2,) + tuple(w.shape[1:]))
+    return torch.cat([a, g], dim=0)
+
+
+# ----------------------------------------------------------------------------------------------
+# Attention
+# ----------------------------------------------------------------------------------------------
+_FLASH_HEAD_DIMS = (32, 40, 64, 80, 96, 128, 160)
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+              mask: torch.Tensor | None = None, causal: bool = False,
+              key_padding: torch.Tensor | None = None) -> torch.Tensor:
+    """softmax(q k^T / sqrt(d)) v over ``heads`` heads. q [B,Sq,H*D], k/v [B,Sk,H*D] -> [B,Sq,H*D].
+
+    Softmax is accumulated in fp32 (reference upcast semantics, attention.py:104-107).
+    ``mask``: additive float mask broadcastable to [B,H,Sq,Sk] (rare: torch path);
+    ``causal``: CLIP causal mask; ``key_padding``: bool [B,Sk] True = attend.
+    """
+    B, Sq, HD = q.shape
+    Sk = k.shape[1]
+    D = HD // heads
+    be = backend_for("attention", q, "cgs_flash_attn_fwd")
+    if (be == "hip" and mask is None and D in _FLASH_HEAD_DIMS and q.dtype == torch.bfloat16
+            and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1):
+        count("attention", "hip")
+        o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
+        kp = None
+        if key_padding is not None:
+            kp = key_padding.to(torch.int8).contiguous()
+        _check(_lib().cgs_flash_attn_fwd(
+            q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+            B, heads, Sq, Sk, D,
+            q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
+            o.stride(0), o.stride(1), D,
+            1.0 / math.sqrt(D), _ptr(kp), 1 if causal else 0, _stream()), "cgs_flash_attn_fwd")
+        return o
+    count("attention", "torch" if q.device.type == "cpu" else "lib")
+    return attention_reference(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
+
+
+def attention_reference(q, k, v, heads, mask=None, causal=False, key_padding=None):
+    B, Sq, HD = q.shape
+    Sk = k.shape[1]
+    D = HD // heads
+    qh = q.reshape(B, Sq, heads, D).transpose(1, 2).float()
+    kh = k.reshape(B, Sk, heads, D).transpose(1, 2).float()
+    vh = v.reshape(B, Sk, heads, D).transpose(1, 2).float()
+    s = torch.matmul(qh, kh.transpose(-1, -2)) * (1.0 / math.sqrt(D))
+    if mask is not None:
+        m = mask
+        if m.dtype == torch.bool:
+            m = torch.zeros_like(m, dtype=s.dtype).masked_fill(~m, float("-inf"))
+        while m.ndim < 4:
+            m = m.unsqueeze(0) if m.ndim < 3 else m.unsqueeze(1)
+        s = s + m.float()
+    if causal:
+        cm = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(cm, float("-inf"))
+    if key_padding is not None:
+        s = s.masked_fill(~key_padding.bool()[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, vh)
+    return o.transpose(1, 2).reshape(B, Sq, HD).to(q.dtype)
+
+
+# ----------------------------------------------------------------------------------------------
+# Normalisation
+# ----------------------------------------------------------------------------------------------
+def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: torch.Tensor | None,
+               eps: float, silu: bool = False, pre_add: torch.Tensor | None = None) -> torch.Tensor:
+    """GroupNorm (+ fused SiLU) over a 4-D image tensor (K06).
+
+    ``pre_add`` ([N, C]) is added per (sample, channel) BEFORE normalising — this is how the
+    ResBlock timestep-embedding add (openaimodel.py:245-264) is fused into the GroupNorm kernel.
+    """
+    be = backend_for("groupnorm", x, "cgs_groupnorm_nhwc_ws")
+    if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16) and \
+            weight is not None and x.shape[1] % 8 == 0 and x.shape[1] <= 2048 and x.shape[1] % groups == 0:
+        count("groupnorm", "hip")
+        N, C, H, W = x.shape
+        xc = x.contiguous(memory_format=torch.channels_last)
+        y = torch.empty_like(xc, memory_format=torch.channels_last)
+        pa = None
+        if pre_add is not None:
+            pa = pre_add.to(x.dtype).contiguous()
+        wsb = int(_lib().cgs_groupnorm_workspace(N, H * W, C))
+        ws = torch.empty((wsb + 3) // 4, device=x.device, dtype=torch.float32)
+        _check(_lib().cgs_groupnorm_nhwc_ws(xc.data_ptr(), y.data_ptr(), weight.data_ptr(),
+                                            _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups, float(eps),
+                                            1 if silu else 0, _DT[x.dtype], _stream()),
+               "cgs_groupnorm_nhwc_ws")
+        return y
+    count("groupnorm", "torch" if x.device.type == "cpu" else "lib")
+    if pre_add is not None:
+        x = x + pre_add.to(x.dtype)[:, :, None, None]
+    y = F.group_norm(x.float(), groups, None if weight is None else weight.float(),
+                     None if bias is None else bias.float(), eps)
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype)
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor | None,
+               eps: float = 1e-5) -> torch.Tensor:
+    be = backend_for("layernorm", x, "cgs_layernorm")
+    C = x.shape[-1]
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and weight is not None and C % 8 == 0:
+        count("layernorm", "hip")
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        rows = xc.numel() // C
+        _check(_lib().cgs_layernorm(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
+                                    rows, C, float(eps), _DT[x.dtype], _stream()), "cgs_layernorm")
+        return y
+    count("layernorm", "torch" if x.device.type == "cpu" else "lib")
+    return F.layer_norm(x.float(), (C,), None if weight is None else weight.float(),
+                        None if bias is None else bias.float(), eps).to(x.dtype)
+
+
+# ----------------------------------------------------------------------------------------------
+# Convolution
+# ----------------------------------------------------------------------------------------------
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
+           residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
+           groups: int = 1) -> torch.Tensor:
+    """2-D convolution (K09/K10). Device path: implicit-GEMM NHWC kernel on MFMA with fused
+    bias + residual epilogue (``weight_nhwc`` = weight permuted to [Cout, kh, kw, Cin])."""
+    if isinstance(stride, (tuple, list)):
+        stride = stride[0]
+    if isinstance(padding, (tuple, list)):
+        padding = padding[0]
+    be = backend_for("conv", x, "cgs_conv2d_nhwc")
+    Cout, Cin_g, kh, kw = weight.shape
+    if (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
+            and x.shape[1] % 8 == 0 and Cout % 16 == 0):
+        count("conv", "hip")
+        N, Cin, H, W = x.shape
+        Ho = (H + 2 * padding - kh) // stride + 1
+        Wo = (W + 2 * padding - kw) // stride + 1
+        xc = x.contiguous(memory_format=torch.channels_last)
+        out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype,
+                          memory_format=torch.channels_last)
+        r = None
+        if residual is not None:
+            r = residual.contiguous(memory_format=torch.channels_last)
+        _check(_lib().cgs_conv2d_nhwc(xc.data_ptr(), weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
+                                      out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
+                                      Ho, Wo, _stream()), "cgs_conv2d_nhwc")
+        return out
+    if be == "torch":
+        count("conv", "torch")
+        y = F.conv2d(x.float(), weight.float(), None if bias is None else bias.float(), stride, padding,
+                     groups=groups)
+        if residual is not None:
+            y = y + residual.float()
+        return y.to(x.dtype)
+    count("conv", "lib")
+    y = F.conv2d(x, weight, bias, stride, padding, groups=groups)
+    if residual is not None:
+        y = y + residual
+    return y
+
+
+def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
+    be = backend_for("upsample", x, "cgs_upsample_nearest2x_nhwc")
+    if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16):
+        count("upsample", "hip")
+        N, C, H, W = x.shape
+        xc = x.contiguous(memory_format=torch.channels_last)
+        y = torch.empty((N, C, 2 * H, 2 * W), device=x.device, dtype=x.dtype,
+                        memory_format=torch.channels_last)
+        _check(_lib().cgs_upsample_nearest2x_nhwc(xc.data_ptr(), y.data_ptr(), N, H, W, C,
+                                                  _DT[x.dtype], _stream()), "cgs_upsample")
+        return y
+    count("upsample", "torch" if x.device.type == "cpu" else "lib")
+    return F.interpolate(x, scale_factor=2.0, mode="nearest")
+
+
+# ----------------------------------------------------------------------------------------------
+# Elementwise
+# ----------------------------------------------------------------------------------------------
+def silu(x: torch.Tensor) -> torch.Tensor:
+    be = backend_for("silu", x, "cgs_silu")
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous():
+        count("silu", "hip")
+        y = torch.empty_like(x)
+        _check(_lib().cgs_silu(x.data_ptr(), y.data_ptr(), x.numel(), _DT[x.dtype], _stream()), "cgs_silu")
+        return y
+    return F.silu(x.float()).to(x.dtype) if x.device.type == "cpu" else F.silu(x)
+
+
+def gelu(x: torch.Tensor, approximate: str = "none") -> torch.Tensor:
+    return F.gelu(x, approximate=approximate)
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, max_period: float = 10000.0,
+                       flip_sin_to_cos: bool = True) -> torch.Tensor:
+    """Sinusoidal timestep embedding: [cos | sin] (util.py:229-249 semantics), fp32 out."""
+    be = backend_for("timestep_embedding", t, "cgs_timestep_embedding")
+    if be == "hip" and dim % 2 == 0:
+        count("timestep_embedding", "hip")
+        tt = t.float().contiguous()
+        out = torch.empty((t.shape[0], dim), device=t.device, dtype=torch.float32)
+        _check(_lib().cgs_timestep_embedding(tt.data_ptr(), out.data_ptr(), t.shape[0], dim,
+                                             float(max_period), 1 if flip_sin_to_cos else 0, _stream()),
+               "cgs_timestep_embedding")
+        return out
+    half = dim // 2
+    freqs = torch.exp(-math.log(max_period) * torch.arange(half, dtype=torch.float32, device=t.device) / half)
+    args = t[:, None].float() * freqs[None]
+    emb = torch.cat([torch.cos(args), torch.sin(args)], dim=-1) if flip_sin_to_cos else \
+        torch.cat([torch.sin(args), torch.cos(args)], dim=-1)
+    if dim % 2:
+        emb = torch.cat([emb, torch.zeros_like(emb[:, :1])], dim=-1)
+    return emb
+
+
+def cfg_combine(cond: torch.Tensor, uncond: torch.Tensor, scale: float) -> torch.Tensor:
+    """uncond + (cond - uncond) * scale (samplers.py:240), fused on device."""
+    be = backend_for("cfg", cond, "cgs_cfg_combine")
+    if be == "hip" and cond.dtype == torch.float32 and cond.is_contiguous() and uncond.is_contiguous():
+        out = torch.empty_like(cond)
+        _check(_lib().cgs_cfg_combine(cond.data_ptr(), uncond.data_ptr(), out.data_ptr(), cond.numel(),
+                                      float(scale), 0, _stream()), "cgs_cfg_combine")
+        return out
+    return uncond + (cond - uncond) * scale
+
+
+def euler_step(x: torch.Tensor, denoised: torch.Tensor, noise: torch.Tensor | None, sigma: float,
+               sigma_down: float, sigma_up: float) -> torch.Tensor:
+    """Fused Euler(-ancestral) update (sampling.py:148-164):
+    d = (x - denoised)/sigma ; x = x + d*(sigma_down - sigma) ; x += noise*sigma_up."""
+    be = backend_for("euler", x, "cgs_euler_step")
+    if be == "hip" and x.dtype == torch.float32 and denoised.dtype == torch.float32 and x.is_contiguous() \
+            and denoised.is_contiguous() and (noise is None or noise.is_contiguous()):
+        count("euler", "hip")
+        x = x.clone()  # the kernel updates in place; keep the caller's tensor intact
+        _check(_lib().cgs_euler_step(x.data_ptr(), denoised.data_ptr(),
+                                     _ptr(noise) if (noise is not None and sigma_up > 0) else None,
+                                     x.numel(), float(sigma), float(sigma_down), float(sigma_up), _stream()),
+               "cgs_euler_step")
+        return x
+    d = (x - denoised) / sigma
+    x = x + d * (sigma_down - sigma)
+    if noise is not None and sigma_up > 0:
+        x = x + noise * sigma_up
+    return x

@@ -1,0 +1,137 @@
+"""Communicator: one process per GPU over RCCL/xGMI (``torch.distributed`` backend ``nccl`` IS RCCL
+on ROCm), Gloo on the CPU for tests. The reference has no collective call sites;
+the new ones are:
+
+  R1 job broadcast      ``broadcast_object`` (workflow JSON / seeds / prompts, rank 0 -> all)
+  R2 result gather      ``all_gather_uint8`` images / latents into rank 0's output
+  R3 weight broadcast   ``broadcast_module`` — bucketed (256 MB default) in-place broadcast of every
+                        parameter from rank 0 so only one rank reads a checkpoint from disk
+  R6 control            ``barrier`` / ``heartbeat`` (all-reduce of a liveness counter)
+
+xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL picks ring/tree per size. Buckets are
+sized so a collective is bandwidth-bound (hundreds of MB), not latency-bound.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self):
+        self.rank = 0
+        self.world = 1
+        self.local_rank = 0
+        self.backend = None
+        self.device = torch.device("cpu")
+
+    @property
+    def enabled(self):
+        return self.world > 1
+
+    def barrier(self):
+        if self.enabled:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def broadcast_object(self, obj, src=0):
+        if not self.enabled:
+            return obj
+        lst = [obj if self.rank == src else None]
+        dist.broadcast_object_list(lst, src=src, device=self.device if self.backend == "nccl" else None)
+        return lst[0]
+
+    def broadcast_tensor(self, t, src=0):
+        if self.enabled:
+            dist.broadcast(t, src=src)
+        return t
+
+    @torch.no_grad()
+    def broadcast_module(self, module, src=0, bucket_bytes=256 << 20):
+        """Bucketed parameter/buffer broadcast (R3): flatten same-dtype tensors into buckets."""
+        if not self.enabled:
+            return module
+        tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]
+        groups = {}
+        for t in tensors:
+            groups.setdefault((t.dtype, t.device), []).append(t)
+        for (dt, dev), ts in groups.items():
+            bucket, size = [], 0
+            for t in ts + [None]:
+                if t is not None and (size + t.numel() * t.element_size() <= bucket_bytes or not bucket):
+                    bucket.append(t)
+                    size += t.numel() * t.element_size()
+                    continue
+                if bucket:
+                    flat = torch.cat([b.reshape(-1) for b in bucket])
+                    dist.broadcast(flat, src=src)
+                    off = 0
+                    for b in bucket:
+                        n = b.numel()
+                        b.copy_(flat[off:off + n].view_as(b))
+                        off += n
+                bucket, size = ([t], t.numel() * t.element_size()) if t is not None else ([], 0)
+        return module
+
+    def all_gather(self, t):
+        """Concatenate ``t`` (same shape on every rank) along dim 0 across ranks."""
+        if not self.enabled:
+            return t
+        t = t.contiguous()
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t)
+        return out
+
+    def all_reduce_max(self, x: float) -> float:
+        if not self.enabled:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def heartbeat(self) -> int:
+        """R6: returns the number of live ranks (all-reduce of ones)."""
+        if not self.enabled:
+            return 1
+        t = torch.ones(1, dtype=torch.int32, device=self.device)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    def shutdown(self):
+        if self.enabled and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+_COMM = Comm()
+
+
+def get_comm() -> Comm:
+    return _COMM
+
+
+def init_from_env(backend=None, timeout_s=600) -> Comm:
+    """Initialise from torchrun env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT)."""
+    c = _COMM
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    c.rank = int(os.environ.get("RANK", "0"))
+    c.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    c.world = world
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu:
+        torch.cuda.set_device(c.local_rank)
+        c.device = torch.device("cuda", c.local_rank)
+    if world > 1 and not dist.is_initialized():
+        c.backend = backend or ("nccl" if use_gpu else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=c.backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if c.backend == "nccl":
+            kw["device_id"] = c.device
+        dist.init_process_group(**kw)
+    elif dist.is_initialized():
+        c.backend = dist.get_backend()
+    return c

@@ -1,0 +1,112 @@
+"""Data-parallel text-to-image across the GPUs of a node (BASELINE config 5).
+
+One process per GPU. A job = (prompt, negative, batch, seed, steps, cfg, sampler, scheduler, size).
+Rank 0 owns the job and broadcasts it (R1); each rank generates its slice of the batch with the
+reference's per-index noise replay (``prepare_noise`` with ``batch_index`` = the image's global
+index, so the DP result is bit-identical in noise to a single-GPU run of the whole batch); the
+decoded uint8 images are all-gathered (R2) so rank 0 can encode/save them.
+
+Everything per rank is the standard single-GPU path (CLIP -> CFGGuider/KSampler -> VAE), so the
+DP engine scales whatever the kernels deliver on one GPU.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import torch
+
+from ..runtime import device as dm
+from ..sampling import sample as S
+from .comm import get_comm
+
+
+@dataclasses.dataclass
+class Job:
+    prompt: str = "a photo of an astronaut riding a horse on mars, highly detailed"
+    negative: str = "blurry, low quality"
+    batch: int = 8
+    seed: int = 0
+    steps: int = 20
+    cfg: float = 8.0
+    sampler: str = "euler_ancestral"
+    scheduler: str = "normal"
+    width: int = 1024
+    height: int = 1024
+
+
+def encode_prompt(clip, text, width, height):
+    """CLIPTextEncode (+ SDXL size conds) -> CONDITIONING list."""
+    tokens = clip.tokenize(text)
+    cond, pooled = clip.encode_from_tokens(tokens, return_pooled=True)
+    meta = {"pooled_output": pooled}
+    return [[cond, meta]]
+
+
+def generate_local(patcher, clip, vae, job: Job, index_offset: int, local_batch: int, conds=None):
+    """Generate images [index_offset, index_offset+local_batch) of ``job`` on this rank."""
+    lat_c = 4
+    latent = torch.zeros([local_batch, lat_c, job.height // 8, job.width // 8])
+    if conds is None:
+        pos = encode_prompt(clip, job.prompt, job.width, job.height)
+        neg = encode_prompt(clip, job.negative, job.width, job.height)
+    else:
+        pos, neg = conds
+    # per-image noise replay (latent "batch_index" semantics): identical for any rank split
+    inds = list(range(index_offset, index_offset + local_batch))
+    noise = S.prepare_noise(latent, job.seed, noise_inds=inds)
+    samples = S.sample(patcher, noise, job.steps, job.cfg, job.sampler, job.scheduler, pos, neg, latent,
+                       denoise=1.0, seed=job.seed)
+    return vae.decode(samples)
+
+
+def to_uint8(images: torch.Tensor) -> torch.Tensor:
+    return (images.clamp(0, 1) * 255.0 + 0.5).to(torch.uint8)
+
+
+class DataParallelGenerator:
+    def __init__(self, patcher, clip, vae):
+        self.patcher, self.clip, self.vae = patcher, clip, vae
+        self.comm = get_comm()
+
+    def sync_weights(self):
+        """R3: make every rank's weights identical to rank 0's (one disk read per node)."""
+        c = self.comm
+        if not c.enabled:
+            return
+        c.broadcast_module(self.patcher.model.diffusion_model)
+        if self.clip is not None:
+            c.broadcast_module(self.clip.cond_stage_model)
+        if self.vae is not None:
+            c.broadcast_module(self.vae.first_stage_model)
+
+    def run(self, job: Job, gather=True):
+        """Whole-node job: ``job.batch`` images split evenly across ranks -> uint8 [B,H,W,3] on rank 0."""
+        c = self.comm
+        job = c.broadcast_object(job)
+        per = job.batch // c.world
+        rem = job.batch % c.world
+        local = per + (1 if c.rank < rem else 0)
+        offset = c.rank * per + min(c.rank, rem)
+        imgs = generate_local(self.patcher, self.clip, self.vae, job, offset, local)
+        u8 = to_uint8(imgs)
+        if gather and c.enabled:
+            if rem:
+                pad = torch.zeros((per + 1 - local,) + tuple(u8.shape[1:]), dtype=u8.dtype, device=u8.device)
+                u8 = torch.cat([u8, pad])
+            allimgs = c.all_gather(u8.to(c.device))
+            if rem:
+                keep = []
+                for r in range(c.world):
+                    n = per + (1 if r < rem else 0)
+                    keep.append(allimgs[r * (per + (1 if rem else 0)): r * (per + (1 if rem else 0)) + n])
+                allimgs = torch.cat(keep)
+            return allimgs
+        return u8
+
+
+def images_per_sec(batch, seconds):
+    return batch / seconds if seconds > 0 else 0.0
+
+
+def device_sync():
+    dm.synchronize()

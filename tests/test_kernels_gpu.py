@@ -1,0 +1,150 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (SURVEY §7.4 'Kernel unit tests').
+
+Every test asserts the native path actually ran (ops.stats) so a silent fallback fails."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from comfy_gen_server_amd import ops, _native
+from comfy_gen_server_amd.ops import core
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _native_loaded(cuda):
+    assert _native.load_kernels() is not None, _native.kernels_error()
+    ops.reset_stats()
+    yield
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N,C,H,W,G", [(2, 320, 32, 32, 32), (2, 640, 16, 16, 32), (1, 1280, 8, 8, 32),
+                                       (2, 960, 16, 16, 32), (1, 128, 64, 64, 32), (3, 64, 5, 7, 32)])
+@pytest.mark.parametrize("silu", [False, True])
+def test_groupnorm(cuda, N, C, H, W, G, silu):
+    torch.manual_seed(0)
+    x = (torch.randn(N, C, H, W, device=cuda) * 3 + 1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(C, device=cuda).to(torch.bfloat16)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16)
+    pre = torch.randn(N, C, device=cuda).to(torch.bfloat16)
+    y = ops.group_norm(x, G, w, b, 1e-5, silu=silu, pre_add=pre)
+    ref = F.group_norm(x.float() + pre.float()[:, :, None, None], G, w.float(), b.float(), 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    assert ops.stats().get(("groupnorm", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("rows,C", [(100, 640), (4096, 1280), (77, 768), (33, 2048), (5, 5120)])
+def test_layernorm(cuda, rows, C):
+    torch.manual_seed(0)
+    x = (torch.randn(rows, C, device=cuda) * 2 + 0.5).to(torch.bfloat16)
+    w = torch.randn(C, device=cuda).to(torch.bfloat16)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16)
+    y = ops.layer_norm(x, w, b, 1e-5)
+    ref = F.layer_norm(x.float(), (C,), w.float(), b.float(), 1e-5)
+    assert ops.stats().get(("layernorm", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,Sq,Sk,D", [(2, 10, 256, 256, 64), (2, 20, 100, 77, 64), (1, 8, 300, 300, 40),
+                                         (2, 8, 128, 77, 80), (1, 8, 64, 64, 160), (1, 4, 96, 200, 128)])
+def test_flash_attention(cuda, B, H, Sq, Sk, D):
+    torch.manual_seed(0)
+    q = torch.randn(B, Sq, H * D, device=cuda).to(torch.bfloat16)
+    k = torch.randn(B, Sk, H * D, device=cuda).to(torch.bfloat16)
+    v = torch.randn(B, Sk, H * D, device=cuda).to(torch.bfloat16)
+    o = ops.attention(q, k, v, H)
+    ref = core.attention_reference(q.float(), k.float(), v.float(), H)
+    assert ops.stats().get(("attention", "hip"), 0) == 1
+    assert _rel(o, ref) < 2e-2
+
+
+def test_flash_attention_strided_qkv(cuda):
+    """q, k, v as views of one fused QKV projection (stride 3C), as the UNet uses them."""
+    torch.manual_seed(1)
+    B, S, H, D = 2, 200, 5, 64
+    qkv = torch.randn(B, S, 3 * H * D, device=cuda).to(torch.bfloat16)
+    C = H * D
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    o = ops.attention(q, k, v, H)
+    ref = core.attention_reference(q.float(), k.float(), v.float(), H)
+    assert _rel(o, ref) < 2e-2
+
+
+def test_flash_attention_causal_and_spike(cuda):
+    """Causal CLIP mask + a spiked key forcing large running-max jumps (rescale path)."""
+    torch.manual_seed(2)
+    B, S, H, D = 2, 77, 12, 64
+    q = torch.randn(B, S, H * D, device=cuda)
+    k = torch.randn(B, S, H * D, device=cuda)
+    k[:, 70, :] *= 8.0
+    v = torch.randn(B, S, H * D, device=cuda)
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    o = ops.attention(q, k, v, H, causal=True)
+    ref = core.attention_reference(q.float(), k.float(), v.float(), H, causal=True)
+    assert _rel(o, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 320, 640), (154, 1280, 2048), (4096, 1280, 1280),
+                                   (77, 768, 768), (2, 1280, 2816)])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
+def test_gemm(cuda, M, N, K, epi):
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
+    y = ops.linear(a, w, b, residual=r)
+    ref = a.float() @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if r is not None:
+        ref = ref + r.float()
+    assert ops.stats().get(("gemm", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N2,K", [(256, 512, 128), (333, 2560, 320), (64, 10240, 1280)])
+def test_gemm_geglu(cuda, M, N2, K):
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N2, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N2, device=cuda).to(torch.bfloat16)
+    y = ops.linear_geglu(a, core.geglu_interleave(w), core.geglu_interleave(b))
+    h = a.float() @ w.float().t() + b.float()
+    x1, g = h.chunk(2, dim=-1)
+    ref = x1 * F.gelu(g)
+    assert ops.stats().get(("gemm_geglu", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
+def test_elementwise(cuda):
+    torch.manual_seed(0)
+    x = torch.randn(1000, 40, device=cuda).to(torch.bfloat16)
+    assert _rel(ops.silu(x), F.silu(x.float())) < 1e-2
+    t = torch.tensor([1.0, 500.0, 999.0], device=cuda)
+    e = ops.timestep_embedding(t, 320)
+    half = 160
+    freqs = torch.exp(-math.log(10000.0) * torch.arange(half, device=cuda) / half)
+    args = t[:, None] * freqs[None]
+    ref = torch.cat([torch.cos(args), torch.sin(args)], -1)
+    assert (e - ref).abs().max().item() < 2e-3
+    c = torch.randn(2, 4, 16, 16, device=cuda)
+    u = torch.randn(2, 4, 16, 16, device=cuda)
+    assert torch.allclose(ops.cfg_combine(c, u, 7.5), u + (c - u) * 7.5, atol=1e-5)
+    xx = torch.randn(2, 4, 16, 16, device=cuda)
+    den = torch.randn(2, 4, 16, 16, device=cuda)
+    nz = torch.randn(2, 4, 16, 16, device=cuda)
+    out = ops.euler_step(xx, den, nz, 3.0, 2.0, 0.5)
+    ref = xx + (xx - den) / 3.0 * (2.0 - 3.0) + nz * 0.5
+    assert torch.allclose(out, ref, atol=1e-5)
+    im = torch.randn(2, 64, 8, 8, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    up = ops.upsample_nearest2x(im)
+    assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
