@@ -131,14 +131,36 @@ class VAE:
                 ddconfig = dict(double_z=True, z_channels=4, resolution=256, in_channels=3, out_ch=3, ch=128,
                                 ch_mult=[1, 2, 4, 4], num_res_blocks=2, attn_resolutions=[], dropout=0.0)
                 if sd is not None:
-                    if "encoder.down.2.downsample.conv.weight" not in sd and "decoder.up.3.block.0.conv1.weight" not in sd:
-                        ddconfig["ch_mult"] = [1, 2, 4]
-                        self.downscale_ratio = self.upscale_ratio = 4
+                    # sniff the KL config from key names / shapes (levels, widths, res blocks)
+                    if "decoder.conv_out.weight" in sd:
+                        ddconfig["ch"] = sd["decoder.conv_out.weight"].shape[1]
+                    elif "encoder.conv_in.weight" in sd:
+                        ddconfig["ch"] = sd["encoder.conv_in.weight"].shape[0]
+                    ch = ddconfig["ch"]
+                    nlev = 0
+                    while f"decoder.up.{nlev}.block.0.conv1.weight" in sd or f"encoder.down.{nlev}.block.0.conv1.weight" in sd:
+                        nlev += 1
+                    if nlev:
+                        mult = []
+                        for i in range(nlev):
+                            k = f"decoder.up.{i}.block.0.conv2.weight"
+                            k2 = f"encoder.down.{i}.block.0.conv2.weight"
+                            w = sd.get(k, sd.get(k2))
+                            mult.append(int(w.shape[0] // ch))
+                        ddconfig["ch_mult"] = mult
+                        self.downscale_ratio = self.upscale_ratio = 2 ** (nlev - 1)
+                        nrb = 0
+                        while f"decoder.up.0.block.{nrb}.conv1.weight" in sd:
+                            nrb += 1
+                        if nrb:
+                            ddconfig["num_res_blocks"] = nrb - 1
+                        else:
+                            while f"encoder.down.0.block.{nrb}.conv1.weight" in sd:
+                                nrb += 1
+                            ddconfig["num_res_blocks"] = max(1, nrb)
                     if "decoder.conv_in.weight" in sd:
                         ddconfig["z_channels"] = sd["decoder.conv_in.weight"].shape[1]
                         self.latent_channels = ddconfig["z_channels"]
-                    if "encoder.conv_in.weight" in sd:
-                        ddconfig["ch"] = sd["encoder.conv_in.weight"].shape[0]
                 self.first_stage_model = V.AutoencoderKL(embed_dim=ddconfig["z_channels"], ddconfig=ddconfig,
                                                          device=torch.device("meta"))
                 self.first_stage_model.to_empty(device="cpu")

@@ -1,0 +1,111 @@
+"""Image I/O at the node boundary (PIL codecs; SURVEY §2.3 'keep PIL for codecs').
+
+* ``save_png_batch`` — PNG with ``prompt`` / workflow tEXt chunks (``nodes.py:1810-1837``); the
+  batch is converted to uint8 on the device in one op and encoded by a thread pool (PNG encode of
+  large batches is CPU-heavy: SURVEY §7.5 item 6).
+* ``load_image_frames`` — multi-frame images, EXIF transpose, alpha -> inverted MASK
+  (``nodes.py:1866-1893``).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+
+import numpy as np
+import torch
+from PIL import Image, ImageOps, ImageSequence
+from PIL.PngImagePlugin import PngInfo
+
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        _POOL = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
+    return _POOL
+
+
+def to_uint8_cpu(images: torch.Tensor) -> np.ndarray:
+    u8 = (images.detach().clamp(0, 1) * 255.0 + 0.5).to(torch.uint8)
+    return u8.cpu().numpy()
+
+
+def encode_png(arr: np.ndarray, metadata: dict | None = None, compress_level=4) -> bytes:
+    import io
+    img = Image.fromarray(arr)
+    info = None
+    if metadata:
+        info = PngInfo()
+        for k, v in metadata.items():
+            info.add_text(k, v)
+    bio = io.BytesIO()
+    img.save(bio, format="PNG", pnginfo=info, compress_level=compress_level)
+    return bio.getvalue()
+
+
+def save_png_batch(images, folder, filename, counter, metadata=None, compress_level=4):
+    arrs = to_uint8_cpu(images)
+    names = []
+    jobs = []
+    for i, arr in enumerate(arrs):
+        name = f"{filename}_{counter + i:05}_.png"
+        names.append(name)
+        path = os.path.join(folder, name)
+
+        def work(a=arr, p=path):
+            img = Image.fromarray(a)
+            info = None
+            if metadata:
+                info = PngInfo()
+                for k, v in metadata.items():
+                    info.add_text(k, v)
+            img.save(p, pnginfo=info, compress_level=compress_level)
+        jobs.append(_pool().submit(work))
+    for j in jobs:
+        j.result()
+    return names
+
+
+def load_image_frames(image_path):
+    img = Image.open(image_path)
+    output_images, output_masks = [], []
+    w = h = None
+    excluded = ["MPO"]
+    for i in ImageSequence.Iterator(img):
+        i = ImageOps.exif_transpose(i)
+        if i.mode == "I":
+            i = i.point(lambda v: v * (1 / 255))
+        image = i.convert("RGB")
+        if len(output_images) == 0:
+            w, h = image.size
+        if image.size[0] != w or image.size[1] != h:
+            continue
+        image = torch.from_numpy(np.array(image).astype(np.float32) / 255.0)[None,]
+        if "A" in i.getbands():
+            mask = np.array(i.getchannel("A")).astype(np.float32) / 255.0
+            mask = 1.0 - torch.from_numpy(mask)
+        else:
+            mask = torch.zeros((64, 64), dtype=torch.float32, device="cpu")
+        output_images.append(image)
+        output_masks.append(mask.unsqueeze(0))
+    if len(output_images) > 1 and img.format not in excluded:
+        return torch.cat(output_images, dim=0), torch.cat(output_masks, dim=0)
+    return output_images[0], output_masks[0]
+
+
+def load_mask_channel(image_path, channel):
+    i = Image.open(image_path)
+    i = ImageOps.exif_transpose(i)
+    if i.getbands() != ("R", "G", "B", "A"):
+        if i.mode == "I":
+            i = i.point(lambda v: v * (1 / 255))
+        i = i.convert("RGBA")
+    c = channel[0].upper()
+    if c in i.getbands():
+        mask = torch.from_numpy(np.array(i.getchannel(c)).astype(np.float32) / 255.0)
+        if c == "A":
+            mask = 1.0 - mask
+    else:
+        mask = torch.zeros((64, 64), dtype=torch.float32, device="cpu")
+    return mask.unsqueeze(0)
