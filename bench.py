@@ -39,6 +39,9 @@ def main():
 
     if args.cpu:
         os.environ["CGS_FORCE_CPU"] = "1"
+    # MIOpen (only used for convs not yet on the HIP kernel): heuristic solver choice, no
+    # exhaustive first-call search on a fresh box.
+    os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
     if args.no_graph:
         os.environ["CGS_GRAPHS"] = "0"
     import torch
@@ -67,10 +70,21 @@ def main():
     job = Job(batch=global_batch, steps=args.sampler_steps, cfg=args.cfg, sampler=args.sampler,
               width=args.res, height=args.res)
 
+    def log(msg):
+        if comm.rank == 0:
+            print(f"[bench {time.time() - t0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+    log(f"built pipeline in {t_build:.1f}s")
+
     def one_step(i):
         j = Job(**{**job.__dict__, "seed": 1000 + i})
+        ts = time.perf_counter()
         with torch.inference_mode():
-            return gen.run(j)
+            r = gen.run(j)
+        if not args.cpu:
+            torch.cuda.synchronize()
+        log(f"step {i}: {time.perf_counter() - ts:.2f}s")
+        return r
 
     for i in range(args.warmup):
         one_step(i)
@@ -116,6 +130,9 @@ def main():
                        "parallelism": f"dp{N}"},
             "build_s": round(t_build, 1),
         }
+        from comfy_gen_server_amd.parallel import dp as _dp
+        if _dp.STAGE_TIMES:
+            res["stage_seconds"] = {k: [round(x, 3) for x in v] for k, v in _dp.STAGE_TIMES.items()}
         if args.profile_ops:
             res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
         print(json.dumps(res), flush=True)

@@ -90,7 +90,8 @@ class GEGLU(nn.Module, DerivedMixin):
         self.proj = Linear(dim_in, dim_out * 2, dtype=dtype, device=device)
 
     def forward(self, x):
-        if x.is_cuda and x.dtype == self.proj.weight.dtype:
+        if x.is_cuda and x.dtype == self.proj.weight.dtype and \
+                ops.dispatch.backend_for("gemm", x, "cgs_gemm_bf16") == "hip":
             w = self._derived_get("w_il", lambda: ops.core.geglu_interleave(self.proj.weight))
             b = self._derived_get("b_il", lambda: ops.core.geglu_interleave(self.proj.bias))
             return ops.linear_geglu(x, w, b)

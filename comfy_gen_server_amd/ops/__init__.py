@@ -10,6 +10,7 @@ Reference call sites this replaces: ``comfy/ops.py:39-163`` (casting ops),
 ``comfy/ldm/modules/attention.py:88-383`` (attention backends: basic / sub-quad / split /
 xformers / SDPA) — on MI355X all of them collapse to one LDS-tiled MFMA flash-attention kernel.
 """
+from . import dispatch  # noqa: F401
 from .dispatch import (  # noqa: F401
     backend_for, set_backend_override, native_required, NativeMissingError, stats, reset_stats,
 )

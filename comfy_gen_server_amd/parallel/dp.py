@@ -12,6 +12,8 @@ DP engine scales whatever the kernels deliver on one GPU.
 from __future__ import annotations
 
 import dataclasses
+import os
+import time
 
 import torch
 
@@ -42,21 +44,45 @@ def encode_prompt(clip, text, width, height):
     return [[cond, meta]]
 
 
+STAGE_TIMES: dict = {}
+
+
+class _stage:
+    """Optional per-stage wall time (CGS_STAGE_TIMING=1): synchronises the device at both ends."""
+
+    def __init__(self, name):
+        self.name = name
+        self.on = os.environ.get("CGS_STAGE_TIMING", "0") == "1"
+
+    def __enter__(self):
+        if self.on:
+            dm.synchronize()
+            self.t = time.perf_counter()
+
+    def __exit__(self, *a):
+        if self.on:
+            dm.synchronize()
+            STAGE_TIMES.setdefault(self.name, []).append(time.perf_counter() - self.t)
+
+
 def generate_local(patcher, clip, vae, job: Job, index_offset: int, local_batch: int, conds=None):
     """Generate images [index_offset, index_offset+local_batch) of ``job`` on this rank."""
     lat_c = 4
     latent = torch.zeros([local_batch, lat_c, job.height // 8, job.width // 8])
-    if conds is None:
-        pos = encode_prompt(clip, job.prompt, job.width, job.height)
-        neg = encode_prompt(clip, job.negative, job.width, job.height)
-    else:
-        pos, neg = conds
+    with _stage("clip"):
+        if conds is None:
+            pos = encode_prompt(clip, job.prompt, job.width, job.height)
+            neg = encode_prompt(clip, job.negative, job.width, job.height)
+        else:
+            pos, neg = conds
     # per-image noise replay (latent "batch_index" semantics): identical for any rank split
     inds = list(range(index_offset, index_offset + local_batch))
     noise = S.prepare_noise(latent, job.seed, noise_inds=inds)
-    samples = S.sample(patcher, noise, job.steps, job.cfg, job.sampler, job.scheduler, pos, neg, latent,
-                       denoise=1.0, seed=job.seed)
-    return vae.decode(samples)
+    with _stage("sample"):
+        samples = S.sample(patcher, noise, job.steps, job.cfg, job.sampler, job.scheduler, pos, neg, latent,
+                           denoise=1.0, seed=job.seed)
+    with _stage("vae"):
+        return vae.decode(samples)
 
 
 def to_uint8(images: torch.Tensor) -> torch.Tensor:
