@@ -1,0 +1,218 @@
+// NHWC implicit-GEMM convolution for gfx950 (K09 conv3x3 s1/s2, K10 conv1x1, K12 upsample+conv,
+// K14 skip-concat + conv, K15 residual epilogue). Reference semantics: torch.nn.Conv2d as used by
+// comfy/ldm/modules/diffusionmodules/openaimodel.py (ResBlock, Down/Upsample) and model.py (VAE).
+//
+//   out[n,oy,ox,co] = bias[co] + sum_{ky,kx,ci} in[n, oy*s+ky-p, ox*s+kx-p, ci] * w[co,ky,kx,ci] (+ res)
+// GEMM view: M = N*Ho*Wo output pixels, Ncols = Cout, K = kh*kw*Cin; weights pre-permuted to
+// [Cout][kh][kw][Cin] (K-contiguous, like nn.Linear). Cin % 64 == 0 so every 64-wide K step lies in
+// one filter tap: per step each lane computes ONE source pixel address (or the zero page for
+// padding) and the 8-row x 128-B LDS-DMA pieces stream straight from the NHWC activation — im2col
+// is never materialised. Same 256 x BN x 64 tile, 8 waves, MFMA 16x16x32, swizzled LDS ring and
+// epilogue as the GEMM v2 kernel.
+//
+// Fusions (flags):
+//   CONV_UP2X  : the input is read through a nearest-2x upsample (Upsample + conv, no 4x tensor);
+//   dual input : channels [0, C1) come from in, [C1, Cin) from in2 — torch.cat([h, skip], 1) + conv
+//                (the UNet decoder's skip concat is never materialised).
+#include "common.h"
+
+#define EPI_BIAS 1
+#define EPI_RESIDUAL 2
+#define CONV_UP2X 16
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __attribute__((aligned(16))) unsigned char g_conv_zero_page[256];
+
+struct ConvArgs {
+  const u16* in;
+  const u16* in2;      // second input for the fused channel concat (or null)
+  const u16* w;        // [Cout][kh][kw][Cin]
+  const u16* bias;
+  const u16* res;
+  u16* out;
+  int N, H, W, Cin, C1, Cout, kh, kw, stride, pad, Ho, Wo;
+  int flags;
+  int tiles_n;
+};
+
+template <int BN>
+__global__ __launch_bounds__(512, 1) void conv_nhwc_v2_kernel(ConvArgs a) {
+  constexpr int BM = 256, BK = 64;
+  constexpr int WN = BN / 4;
+  constexpr int NJ = WN / 16;
+  constexpr int NI = 8;
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 8 / 8;
+  constexpr int B_INSTR = BN / 8 / 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  const int nwg = gridDim.x;
+  const int logical = xcd_remap(blockIdx.x, nwg);
+  const int tm = logical / a.tiles_n;
+  const int tn = logical % a.tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave >> 2) * 128;
+  const int wn = (wave & 3) * WN;
+  const int prow = lane >> 3;
+  const int pchunk = lane & 7;
+  const bool up = (a.flags & CONV_UP2X) != 0;
+  const int Hin = up ? (a.H << 1) : a.H;   // logical (upsampled) input extent
+  const int Win = up ? (a.W << 1) : a.W;
+
+  // per-lane output pixel of each A piece
+  int pn[A_INSTR], py[A_INSTR], px[A_INSTR], pswz[A_INSTR];
+  bool pvalid[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    int r = (wave * A_INSTR + i) * 8 + prow;
+    int m = m0 + r;
+    pvalid[i] = m < M;
+    m = min(m, M - 1);
+    pn[i] = m / (a.Ho * a.Wo);
+    int rem = m - pn[i] * a.Ho * a.Wo;
+    py[i] = (rem / a.Wo) * a.stride - a.pad;
+    px[i] = (rem % a.Wo) * a.stride - a.pad;
+    pswz[i] = pchunk ^ ((r >> 1) & 7);
+  }
+  const u16* bsrc[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    int r = (wave * B_INSTR + i) * 8 + prow;
+    int gr = min(n0 + r, a.Cout - 1);
+    bsrc[i] = a.w + (long long)gr * K + 8 * (pchunk ^ ((r >> 1) & 7));
+  }
+  const int C2 = a.Cin - a.C1;
+  auto issue = [&](int kt, int stage) {
+    unsigned char* base = smem + stage * STAGE;
+    const int k0 = kt * BK;
+    const int tap = k0 / a.Cin;
+    const int ci0 = k0 - tap * a.Cin;
+    const int ky = tap / a.kw;
+    const int kx = tap - ky * a.kw;
+    const bool second = ci0 >= a.C1;
+    const u16* src_t = second ? a.in2 : a.in;
+    const int cstride = second ? C2 : a.C1;
+    const int cbase = second ? ci0 - a.C1 : ci0;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      int iy = py[i] + ky, ix = px[i] + kx;
+      bool ok = pvalid[i] && iy >= 0 && iy < Hin && ix >= 0 && ix < Win;
+      if (up) { iy >>= 1; ix >>= 1; }
+      const void* src = ok ? (const void*)(src_t + (((long long)pn[i] * a.H + iy) * a.W + ix) * cstride + cbase + 8 * pswz[i])
+                           : (const void*)(g_conv_zero_page + 16 * (lane & 15));
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(base + ((wave * A_INSTR + i) * 8) * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + k0),
+                                       (lds_void*)(base + A_BYTES + ((wave * B_INSTR + i) * 8) * 128), 16, 0, 0);
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+    const unsigned char* As = smem + st * STAGE;
+    const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[NI], bfr[NJ];
+      const int c = kk * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        int r = wm + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        int r = wn + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const int er = fq * 4;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    int col = n0 + wn + j * 16 + fr;
+    if (col >= a.Cout) continue;
+    float bv = (a.flags & EPI_BIAS) ? bf2f(a.bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm + i * 16 + er + r;
+        if (row < M) {
+          float v = acc[i][j][r] + bv;
+          if (a.flags & EPI_RESIDUAL) v += bf2f(a.res[(long long)row * a.Cout + col]);
+          a.out[(long long)row * a.Cout + col] = f2bf(v);
+        }
+      }
+  }
+}
+
+static int conv_launch(ConvArgs& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_nhwc_v2_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * (256 * 64 * 2 + 256 * 64 * 2));
+    hipFuncSetAttribute((const void*)conv_nhwc_v2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * (256 * 64 * 2 + 128 * 64 * 2));
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  const bool wide = a.Cout >= 1024;
+  const int BN = wide ? 256 : 128;
+  a.tiles_n = (a.Cout + BN - 1) / BN;
+  long long nwg = (long long)((M + 255) / 256) * a.tiles_n;
+  size_t lds = 2 * (256 * 64 * 2 + BN * 64 * 2);
+  if (wide) conv_nhwc_v2_kernel<256><<<(unsigned)nwg, 512, lds, stream>>>(a);
+  else conv_nhwc_v2_kernel<128><<<(unsigned)nwg, 512, lds, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// x [N,H,W,Cin] NHWC bf16, w [Cout,kh,kw,Cin], bias [Cout] | null, res [N,Ho,Wo,Cout] | null.
+CGS_EXPORT int cgs_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* res, void* out, int N, int H,
+                               int W, int Cin, int Cout, int kh, int kw, int stride, int pad, int Ho, int Wo,
+                               hipStream_t stream) {
+  if (Cin % 64 || Cout < 1) return (int)hipErrorInvalidValue;
+  ConvArgs a{(const u16*)x, nullptr, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W, Cin, Cin,
+             Cout, kh, kw, stride, pad, Ho, Wo, (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0), 0};
+  return conv_launch(a, stream);
+}
+
+// Fused variants: flags may carry CONV_UP2X (input read through nearest-2x upsample); x2 != null
+// concatenates x2's C2 = Cin - C1 channels after x's C1 channels (skip concat).
+CGS_EXPORT int cgs_conv2d_nhwc_ex(const void* x, const void* x2, int C1, const void* w, const void* bias,
+                                  const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
+                                  int stride, int pad, int Ho, int Wo, int flags, hipStream_t stream) {
+  if (Cin % 64 || (x2 && (C1 % 64)) || Cout < 1) return (int)hipErrorInvalidValue;
+  ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
+             Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
+             (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0};
+  return conv_launch(a, stream);
+}

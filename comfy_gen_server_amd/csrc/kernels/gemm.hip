@@ -146,15 +146,209 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(
   }
 }
 
+
+// ================================================================================================
+// v2: 256 x BN x 64 block tile, 512 threads = 8 waves (2 in M x 4 in N), each wave 128 x BN/4 built
+// from v_mfma_f32_16x16x32_bf16 tiles. Operands stream global -> LDS with global_load_lds
+// (LDS-DMA, 16 B per lane, no VGPR round trip) into a 2-deep LDS ring; one barrier per K step.
+// LDS image is lane-linear per wave-instruction (8 rows x 128 B); the bank-conflict swizzle is
+// applied on the SOURCE address (LDS chunk c of row r holds logical chunk c ^ ((r >> 1) & 7)) and
+// undone on the ds_read_b128 fragment reads — conflict-free for the 16x16x32 operand lane groups.
+// ================================================================================================
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int BN>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_nt_v2_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_n) {
+  constexpr int BM = 256, BK = 64;
+  constexpr int WN = BN / 4;          // wave N extent
+  constexpr int NJ = WN / 16;         // 16-wide n tiles per wave
+  constexpr int NI = 8;               // 16-high m tiles per wave (128 rows)
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 8 / 8;   // glds instrs per wave for A (8 rows each, 8 waves)
+  constexpr int B_INSTR = BN / 8 / 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int nwg = gridDim.x;
+  const int logical = xcd_remap(blockIdx.x, nwg);
+  const int tm = logical / tiles_n;
+  const int tn = logical % tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave >> 2) * 128;
+  const int wn = (wave & 3) * WN;
+
+  // per-lane source pointers for the glds pieces (row within the 8-row piece, swizzled chunk)
+  const int prow = lane >> 3;
+  const int pchunk = lane & 7;
+  const u16* asrc[A_INSTR];
+  const u16* bsrc[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    int r = (wave * A_INSTR + i) * 8 + prow;
+    int gr = min(m0 + r, M - 1);
+    asrc[i] = A + gr * lda + 8 * (pchunk ^ ((r >> 1) & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    int r = (wave * B_INSTR + i) * 8 + prow;
+    int gr = min(n0 + r, N - 1);
+    bsrc[i] = W + gr * ldw + 8 * (pchunk ^ ((r >> 1) & 7));
+  }
+  auto issue = [&](int kt, int stage) {
+    unsigned char* base = smem + stage * STAGE;
+    const int koff = kt * BK;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + koff),
+                                       (lds_void*)(base + ((wave * A_INSTR + i) * 8) * 128), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + koff),
+                                       (lds_void*)(base + A_BYTES + ((wave * B_INSTR + i) * 8) * 128), 16, 0, 0);
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+    const unsigned char* As = smem + st * STAGE;
+    const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[NI], bfr[NJ];
+      const int c = kk * 4 + fq;   // logical 16-B chunk of the row
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        int r = wm + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        int r = wn + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue (16x16x32 C layout: col = lane&15, row = (lane>>4)*4 + reg)
+  const int er = fq * 4;
+  if (epi & EPI_GEGLU) {
+#pragma unroll
+    for (int jp = 0; jp < NJ / 2; ++jp) {
+      int ca = n0 + wn + (2 * jp) * 16 + fr;
+      int cg = ca + 16;
+      int oc = (n0 + wn) / 2 + jp * 16 + fr;
+      if (cg >= N) continue;
+      float ba = 0.f, bg = 0.f;
+      if (epi & EPI_BIAS) { ba = bf2f(bias[ca]); bg = bf2f(bias[cg]); }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm + i * 16 + er + r;
+          if (row < M) {
+            float a = acc[i][2 * jp][r] * alpha + ba;
+            float g = acc[i][2 * jp + 1][r] * alpha + bg;
+            C[row * ldc + oc] = f2bf(a * gelu_f(g));
+          }
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    int col = n0 + wn + j * 16 + fr;
+    if (col >= N) continue;
+    float bv = (epi & EPI_BIAS) ? bf2f(bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm + i * 16 + er + r;
+        if (row < M) {
+          float v = acc[i][j][r] * alpha + bv;
+          if (epi & EPI_RESIDUAL) v += bf2f(R[row * ldr + col]);
+          C[row * ldc + col] = f2bf(v);
+        }
+      }
+  }
+}
+
+static int gemm_v2_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream) {
+  const bool wide = N >= 1024;
+  const int BN = wide ? 256 : 128;
+  int tiles_m = (M + 255) / 256;
+  int tiles_n = (N + BN - 1) / BN;
+  long long nwg = (long long)tiles_m * tiles_n;
+  size_t lds = 2 * (256 * 64 * 2 + BN * 64 * 2);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_bf16_nt_v2_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * (256 * 64 * 2 + 256 * 64 * 2));
+    hipFuncSetAttribute((const void*)gemm_bf16_nt_v2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * (256 * 64 * 2 + 128 * 64 * 2));
+    attr_set = true;
+  }
+  if (wide) {
+    gemm_bf16_nt_v2_kernel<256><<<(unsigned)nwg, 512, lds, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
+        alpha, tiles_n);
+  } else {
+    gemm_bf16_nt_v2_kernel<128><<<(unsigned)nwg, 512, lds, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
+        alpha, tiles_n);
+  }
+  return (int)hipGetLastError();
+}
+
+static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2 where legal
+
+CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
+
 CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                              int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                              hipStream_t stream) {
   if (K % 8 || lda % 8 || ldw % 8) return (int)hipErrorInvalidValue;
   if ((epi & EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0) return 0;
+  // v2 needs K % 64 == 0 and 16-B aligned rows; it pays off once there are >= ~256 big tiles'
+  // worth of work (otherwise the 128x128 kernel keeps more CUs busy).
+  bool v2_ok = (K % 64 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M >= 256 && N >= 128 &&
+               (((uintptr_t)A | (uintptr_t)W) % 16 == 0);
+  if (v2_ok && g_gemm_variant != 1) {
+    const int BN = N >= 1024 ? 256 : 128;
+    long long t2 = (long long)((M + 255) / 256) * ((N + BN - 1) / BN);
+    if (g_gemm_variant == 2 || t2 >= 128)
+      return gemm_v2_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  }
   int tiles_m = (M + G_BM - 1) / G_BM;
   int tiles_n = (N + G_BN - 1) / G_BN;
   long long nwg = (long long)tiles_m * tiles_n;
-  if (nwg == 0) return 0;
   gemm_bf16_nt_kernel<<<(unsigned)nwg, 256, 0, stream>>>((const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias,
                                                         (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
                                                         tiles_n);

@@ -78,7 +78,7 @@ class Conv2d(nn.Module, DerivedMixin):
     def weight_nhwc(self):
         return self._derived_get("w_nhwc", lambda: self.weight.permute(0, 2, 3, 1).contiguous())
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, upsample2x=False):
         w, b = self.weight, self.bias
         wn = None
         if w.dtype != x.dtype or w.device != x.device:
@@ -87,7 +87,7 @@ class Conv2d(nn.Module, DerivedMixin):
         elif x.is_cuda and self.groups == 1:
             wn = self.weight_nhwc()
         return ops.conv2d(x, w, b, self.stride, self.padding, residual=residual, weight_nhwc=wn,
-                          groups=self.groups)
+                          groups=self.groups, upsample2x=upsample2x)
 
 
 class GroupNorm(nn.Module):

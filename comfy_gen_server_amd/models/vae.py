@@ -96,7 +96,7 @@ class Upsample(nn.Module):
         self.conv = Conv2d(c, c, 3, padding=1, dtype=dtype, device=device)
 
     def forward(self, x):
-        return self.conv(ops.upsample_nearest2x(x))
+        return self.conv(x, upsample2x=True)
 
 
 class _Level(nn.Module):

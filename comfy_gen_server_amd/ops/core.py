@@ -262,9 +262,11 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor 
 # ----------------------------------------------------------------------------------------------
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
            residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
-           groups: int = 1) -> torch.Tensor:
-    """2-D convolution (K09/K10). Device path: implicit-GEMM NHWC kernel on MFMA with fused
-    bias + residual epilogue (``weight_nhwc`` = weight permuted to [Cout, kh, kw, Cin])."""
+           groups: int = 1, upsample2x: bool = False) -> torch.Tensor:
+    """2-D convolution (K09/K10/K12). Device path: implicit-GEMM NHWC kernel on MFMA
+    (csrc/kernels/conv.hip) with fused bias + residual epilogue; ``weight_nhwc`` = weight permuted
+    to [Cout, kh, kw, Cin]. ``upsample2x`` reads the input through a nearest-2x upsample inside the
+    kernel (openaimodel.py Upsample: interpolate + conv) so the 4x tensor is never written."""
     if isinstance(stride, (tuple, list)):
         stride = stride[0]
     if isinstance(padding, (tuple, list)):
@@ -272,21 +274,29 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
     be = backend_for("conv", x, "cgs_conv2d_nhwc")
     Cout, Cin_g, kh, kw = weight.shape
     if (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
-            and x.shape[1] % 8 == 0 and Cout % 16 == 0):
+            and x.shape[1] % 64 == 0 and x.dim() == 4):
         count("conv", "hip")
         N, Cin, H, W = x.shape
-        Ho = (H + 2 * padding - kh) // stride + 1
-        Wo = (W + 2 * padding - kw) // stride + 1
+        Hl, Wl = (2 * H, 2 * W) if upsample2x else (H, W)
+        Ho = (Hl + 2 * padding - kh) // stride + 1
+        Wo = (Wl + 2 * padding - kw) // stride + 1
         xc = x.contiguous(memory_format=torch.channels_last)
         out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype,
                           memory_format=torch.channels_last)
         r = None
         if residual is not None:
             r = residual.contiguous(memory_format=torch.channels_last)
-        _check(_lib().cgs_conv2d_nhwc(xc.data_ptr(), weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
-                                      out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
-                                      Ho, Wo, _stream()), "cgs_conv2d_nhwc")
+        if upsample2x:
+            _check(_lib().cgs_conv2d_nhwc_ex(xc.data_ptr(), None, Cin, weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
+                                             out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
+                                             Ho, Wo, 16, _stream()), "cgs_conv2d_nhwc_ex")
+        else:
+            _check(_lib().cgs_conv2d_nhwc(xc.data_ptr(), weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
+                                          out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
+                                          Ho, Wo, _stream()), "cgs_conv2d_nhwc")
         return out
+    if upsample2x:
+        x = upsample_nearest2x(x)
     if be == "torch":
         count("conv", "torch")
         y = F.conv2d(x.float(), weight.float(), None if bias is None else bias.float(), stride, padding,

@@ -30,7 +30,7 @@ _stats_lock = threading.Lock()
 
 # Ops whose default device path is the vendor library until the hand-written kernel beats it.
 # Filled in from measurements (profiles/): see ops/core.py docstrings.
-_DEFAULT_DEVICE_BACKEND: dict[str, str] = {"conv": "lib"}
+_DEFAULT_DEVICE_BACKEND: dict[str, str] = {}
 
 
 def set_backend_override(op: str, backend: str | None):

@@ -49,10 +49,16 @@ def main(quick=False):
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(torch.bfloat16)
         bias = torch.randn(N, device=dev).to(torch.bfloat16)
         fl = 2.0 * M * N * K
-        t_hip = _time(lambda: ops.linear(a, w, bias))
+        lib = ops.dispatch._native.load_kernels()
+        ent = dict(M=M, N=N, K=K)
+        for var in (1, 2):
+            lib.cgs_gemm_set_variant(var)
+            t = _time(lambda: ops.linear(a, w, bias))
+            ent[f"v{var}_tflops"] = fl / t / 1e9
+        lib.cgs_gemm_set_variant(-1)
         t_lib = _time(lambda: F.linear(a, w, bias))
-        res["gemm"].append(dict(M=M, N=N, K=K, hip_ms=t_hip, lib_ms=t_lib, hip_tflops=fl / t_hip / 1e9,
-                                lib_tflops=fl / t_lib / 1e9))
+        ent["lib_tflops"] = fl / t_lib / 1e9
+        res["gemm"].append(ent)
     att_shapes = [(B, 20, 1024, 1024, 64), (B, 10, 4096, 4096, 64), (B, 20, 1024, 77, 64), (B, 10, 4096, 77, 64)]
     if quick:
         att_shapes = att_shapes[:2]

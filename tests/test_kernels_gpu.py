@@ -92,10 +92,18 @@ def test_flash_attention_causal_and_spike(cuda):
     assert _rel(o, ref) < 2e-2
 
 
+@pytest.fixture(params=[1, 2], ids=["v1", "v2"])
+def gemm_variant(request):
+    lib = _native.load_kernels()
+    lib.cgs_gemm_set_variant(request.param)
+    yield request.param
+    lib.cgs_gemm_set_variant(-1)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 320, 640), (154, 1280, 2048), (4096, 1280, 1280),
-                                   (77, 768, 768), (2, 1280, 2816)])
+                                   (77, 768, 768), (2, 1280, 2816), (1000, 640, 320), (512, 3840, 1280)])
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
-def test_gemm(cuda, M, N, K, epi):
+def test_gemm(cuda, M, N, K, epi, gemm_variant):
     torch.manual_seed(0)
     a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
     w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
@@ -111,8 +119,8 @@ def test_gemm(cuda, M, N, K, epi):
     assert _rel(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,N2,K", [(256, 512, 128), (333, 2560, 320), (64, 10240, 1280)])
-def test_gemm_geglu(cuda, M, N2, K):
+@pytest.mark.parametrize("M,N2,K", [(256, 512, 128), (333, 2560, 320), (64, 10240, 1280), (600, 10240, 1280)])
+def test_gemm_geglu(cuda, M, N2, K, gemm_variant):
     torch.manual_seed(0)
     a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
     w = (torch.randn(N2, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
@@ -148,3 +156,37 @@ def test_elementwise(cuda):
     im = torch.randn(2, 64, 8, 8, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     up = ops.upsample_nearest2x(im)
     assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,k,s,p", [(2, 64, 16, 16, 64, 3, 1, 1), (2, 320, 32, 32, 320, 3, 1, 1),
+                                                  (1, 640, 16, 16, 1280, 3, 1, 1), (2, 320, 32, 32, 320, 3, 2, 1),
+                                                  (1, 128, 7, 9, 256, 1, 1, 0), (3, 256, 11, 5, 4, 3, 1, 1),
+                                                  (1, 1920, 8, 8, 1280, 1, 1, 0), (2, 512, 12, 12, 3, 3, 1, 1)])
+@pytest.mark.parametrize("epi", ["bias", "bias_res", "none"])
+def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi):
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, k, k, device=cuda) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
+    b = torch.randn(Cout, device=cuda).to(torch.bfloat16) if epi != "none" else None
+    ref = F.conv2d(x.float(), w.float(), None if b is None else b.float(), s, p)
+    r = None
+    if epi == "bias_res":
+        r = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        ref = ref + r.float()
+    y = ops.conv2d(x, w, b, s, p, residual=r, weight_nhwc=w.permute(0, 2, 3, 1).contiguous())
+    assert ops.stats().get(("conv", "hip"), 0) == 1
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(2, 320, 8, 8, 320), (1, 640, 5, 7, 640), (2, 128, 16, 16, 128)])
+def test_conv2d_fused_upsample(cuda, N, C, H, W, Cout):
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, device=cuda) / math.sqrt(C * 9)).to(torch.bfloat16)
+    b = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    ref = F.conv2d(F.interpolate(x.float(), scale_factor=2.0, mode="nearest"), w.float(), b.float(), 1, 1)
+    y = ops.conv2d(x, w, b, 1, 1, weight_nhwc=w.permute(0, 2, 3, 1).contiguous(), upsample2x=True)
+    assert ops.stats().get(("conv", "hip"), 0) == 1
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
