@@ -80,7 +80,10 @@ KERNEL_SIGNATURES = {
                            _F, _P, _I, _P],             # scale, key_mask(int8 [B,Sk] or null), causal, stream
     # C[M,N] = A[M,K] @ W[N,K]^T (+bias) (+residual) | GEGLU epilogue; bf16 in/out, fp32 acc
     "cgs_gemm_bf16": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
-    "cgs_gemm_set_variant": [_I],   # -1 auto, 1 force 128x128 register-staged, 2 force 256-tile glds
+    "cgs_gemm_set_variant": [_I],   # -1 auto, 1 force 128x128 register-staged, 2 force 256-tile glds, 3 mfma32 4-stage
+    "cgs_conv_set_variant": [_I],
+    "cgs_set_tile_group": [_I],       # grouped tile order for GEMM v2/v3 (tile rows per group)
+    "cgs_conv_set_tile_group": [_I],   # -1 auto (v3 where legal), 2 force the 8-wave 2-stage kernel
     # out = a * gelu(g) where [a | g] = x rows of width 2*N
     "cgs_geglu": [_P, _P, _I, _I, _I, _P],   # x [M, 2N] -> out [M, N], dtype
     # fused CFG combine: out = u + (c - u) * scale   (fp32 or bf16 denoised)
@@ -95,11 +98,14 @@ KERNEL_SIGNATURES = {
     "cgs_upsample_nearest2x_nhwc": [_P, _P, _I, _I, _I, _I, _I, _P],
     # conv implicit GEMM NHWC bf16: x[N,H,W,Cin], w[Cout,kh,kw,Cin], bias, residual, out
     "cgs_conv2d_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "cgs_gemm_bf16_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
+    "cgs_conv2d_nhwc_v": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cgs_conv2d_nhwc_ex": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_gemm_set_variant": None}
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_gemm_set_variant": None,
+            "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None}
 
 
 def _declare(lib):

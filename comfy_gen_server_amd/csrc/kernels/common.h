@@ -86,3 +86,21 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   int x = bid % nx, i = bid / nx;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
+
+// Grouped tile order on top of xcd_remap: logical tile index -> (tm, tn), walking `gm_max` tile
+// rows at a time, so the ~32 tiles an XCD runs together form a gm x (32/gm) block that shares A
+// row-panels and B col-panels in that XCD's L2 instead of streaming 32 distinct B panels.
+__device__ __forceinline__ void grouped_tile(int logical, int tiles_m, int tiles_n, int gm_max, int& tm, int& tn) {
+  if (gm_max <= 1) {
+    tm = logical / tiles_n;
+    tn = logical % tiles_n;
+    return;
+  }
+  const int group = gm_max * tiles_n;
+  const int gid = logical / group;
+  const int first = gid * gm_max;
+  const int gm = (tiles_m - first) < gm_max ? (tiles_m - first) : gm_max;
+  const int in = logical - gid * group;
+  tm = first + in % gm;
+  tn = in / gm;
+}

@@ -15,6 +15,8 @@
 //   dual input : channels [0, C1) come from in, [C1, Cin) from in2 — torch.cat([h, skip], 1) + conv
 //                (the UNet decoder's skip concat is never materialised).
 #include "common.h"
+#include "mfma_core.h"
+#include "mfma_pp.h"
 
 #define EPI_BIAS 1
 #define EPI_RESIDUAL 2
@@ -34,6 +36,7 @@ struct ConvArgs {
   int N, H, W, Cin, C1, Cout, kh, kw, stride, pad, Ho, Wo;
   int flags;
   int tiles_n;
+  int group_m;
 };
 
 template <int BN>
@@ -53,8 +56,8 @@ __global__ __launch_bounds__(512, 1) void conv_nhwc_v2_kernel(ConvArgs a) {
   const int K = a.kh * a.kw * a.Cin;
   const int nwg = gridDim.x;
   const int logical = xcd_remap(blockIdx.x, nwg);
-  const int tm = logical / a.tiles_n;
-  const int tn = logical % a.tiles_n;
+  int tm, tn;
+  grouped_tile(logical, nwg / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
   const int m0 = tm * BM;
   const int n0 = tn * BN;
   const int tid = threadIdx.x;
@@ -175,7 +178,159 @@ __global__ __launch_bounds__(512, 1) void conv_nhwc_v2_kernel(ConvArgs a) {
   }
 }
 
-static int conv_launch(ConvArgs& a, hipStream_t stream) {
+// ------------------------------------------------------------------------------------------------
+// v3: the shared MFMA core (mfma_core.h) with an NHWC gather loader. BK = 32, so Cin % 32 == 0 and
+// a 32-wide K step lies in one filter tap (and, for the fused concat, in one of the two inputs).
+struct ConvGatherA {
+  const ConvArgs* a;
+  int pn[4], py[4], px[4];
+  bool ok[4];
+  int choff;   // this lane's source chunk (elements)
+  __device__ __forceinline__ void setup(int p, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    ok[p] = row < M;
+    row = row < M ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    pn[p] = row / hw;
+    const int rem = row - pn[p] * hw;
+    py[p] = (rem / a->Wo) * a->stride - a->pad;
+    px[p] = (rem % a->Wo) * a->stride - a->pad;
+    choff = 8 * mc::src_chunk(threadIdx.x & 63);
+  }
+  __device__ __forceinline__ const void* src(int p, int k0) const {
+    const int tap = k0 / a->Cin;
+    const int ci0 = k0 - tap * a->Cin;
+    const int ky = tap / a->kw;
+    const int kx = tap - ky * a->kw;
+    const bool up = (a->flags & CONV_UP2X) != 0;
+    const int Hin = up ? 2 * a->H : a->H, Win = up ? 2 * a->W : a->W;
+    int iy = py[p] + ky, ix = px[p] + kx;
+    const bool in = ok[p] && iy >= 0 && iy < Hin && ix >= 0 && ix < Win;
+    if (!in) return (const void*)(g_conv_zero_page + 16 * (threadIdx.x & 15));
+    if (up) { iy >>= 1; ix >>= 1; }
+    const bool second = ci0 >= a->C1;
+    const u16* t = second ? a->in2 : a->in;
+    const int cs = second ? a->Cin - a->C1 : a->C1;
+    const int cb = second ? ci0 - a->C1 : ci0;
+    return (const void*)(t + (((long long)pn[p] * a->H + iy) * a->W + ix) * cs + cb + choff);
+  }
+};
+
+template <int BN, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void conv_nhwc_v3_kernel(
+    ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
+  ConvGatherA al;
+  al.a = &a;
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  mc::tile<BN, NW>(al, a.w, K, M, a.Cout, K, tm * mc::BM, tn * BN, e, smem);
+}
+
+template <int BN, int NW>
+static void conv_v3_go(ConvArgs& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v3_kernel<BN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              mc::Cfg<BN, NW>::LDS);
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = (a.Cout + BN - 1) / BN;
+  const long long nwg = (long long)((M + mc::BM - 1) / mc::BM) * a.tiles_n;
+  conv_nhwc_v3_kernel<BN, NW><<<(unsigned)nwg, 64 * NW, mc::Cfg<BN, NW>::LDS, stream>>>(a);
+}
+
+// v5: ping-pong schedule (mfma_pp.h), 256 x 256 x 64 tiles; Cin % 64 == 0 (one tap per K-tile).
+struct ConvGatherA8 {
+  const ConvArgs* a;
+  int pn[4], py[4], px[4];
+  bool ok[4];
+  int choff[2];
+  __device__ __forceinline__ void setup(int s, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    ok[s] = row < M;
+    row = row < M ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    pn[s] = row / hw;
+    const int rem = row - pn[s] * hw;
+    py[s] = (rem / a->Wo) * a->stride - a->pad;
+    px[s] = (rem % a->Wo) * a->stride - a->pad;
+    choff[s & 1] = 8 * pp::src_chunk8(s & 1);
+  }
+  __device__ __forceinline__ const void* src(int s, int k0) const {
+    const int tap = k0 / a->Cin;
+    const int ci0 = k0 - tap * a->Cin;
+    const int ky = tap / a->kw;
+    const int kx = tap - ky * a->kw;
+    const bool up = (a->flags & CONV_UP2X) != 0;
+    const int Hin = up ? 2 * a->H : a->H, Win = up ? 2 * a->W : a->W;
+    int iy = py[s] + ky, ix = px[s] + kx;
+    const bool in = ok[s] && iy >= 0 && iy < Hin && ix >= 0 && ix < Win;
+    if (!in) return (const void*)(g_conv_zero_page + 16 * (threadIdx.x & 15));
+    if (up) { iy >>= 1; ix >>= 1; }
+    const bool second = ci0 >= a->C1;
+    const u16* t = second ? a->in2 : a->in;
+    const int cs = second ? a->Cin - a->C1 : a->C1;
+    const int cb = second ? ci0 - a->C1 : ci0;
+    return (const void*)(t + (((long long)pn[s] * a->H + iy) * a->W + ix) * cs + cb + choff[s & 1]);
+  }
+};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v5_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
+  ConvGatherA8 al;
+  al.a = &a;
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
+}
+
+static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v5_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, pp::LDS);
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = (a.Cout + pp::BN - 1) / pp::BN;
+  const long long nwg = (long long)((M + pp::BM - 1) / pp::BM) * a.tiles_n;
+  conv_nhwc_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+}
+
+static int g_conv_group = 8;
+CGS_EXPORT void cgs_conv_set_tile_group(int g) { g_conv_group = g < 1 ? 1 : g; }
+static int g_conv_variant = -1;   // -1 auto (v3/8 waves where legal), 2 = v2 only, 3 = v3/4 waves, 4 = v3/8 waves
+CGS_EXPORT void cgs_conv_set_variant(int v) { g_conv_variant = v; }
+
+static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
+  a.group_m = g_conv_group;
+  if (variant == 5 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0)) {
+    conv_v5_go(a, stream);
+    return (int)hipGetLastError();
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  const int BN = mc::pick_bn(M, a.Cout);
+  const bool w8 = variant != 3;
+  if (BN == 256) { if (w8) conv_v3_go<256, 8>(a, stream); else conv_v3_go<256, 4>(a, stream); }
+  else { if (w8) conv_v3_go<128, 8>(a, stream); else conv_v3_go<128, 4>(a, stream); }
+  return (int)hipGetLastError();
+}
+
+static int conv_launch(ConvArgs& a, hipStream_t stream, int variant = -2) {
+  if (variant == -2) variant = g_conv_variant;
+  // v3 needs Cout % 8 == 0 for the 16-B epilogue stores (SD/SDXL/VAE convs: all but the 3/4-channel
+  // heads, which take v2).
+  if (variant != 2 && a.Cout % 8 == 0) return conv_v3_launch(a, variant, stream);
+  a.group_m = g_conv_group;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)conv_nhwc_v2_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -199,9 +354,9 @@ static int conv_launch(ConvArgs& a, hipStream_t stream) {
 CGS_EXPORT int cgs_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* res, void* out, int N, int H,
                                int W, int Cin, int Cout, int kh, int kw, int stride, int pad, int Ho, int Wo,
                                hipStream_t stream) {
-  if (Cin % 64 || Cout < 1) return (int)hipErrorInvalidValue;
+  if (Cin % 32 || Cout < 1 || (Cout % 8 && Cin % 64)) return (int)hipErrorInvalidValue;
   ConvArgs a{(const u16*)x, nullptr, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W, Cin, Cin,
-             Cout, kh, kw, stride, pad, Ho, Wo, (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0), 0};
+             Cout, kh, kw, stride, pad, Ho, Wo, (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0), 0, 1};
   return conv_launch(a, stream);
 }
 
@@ -210,9 +365,22 @@ CGS_EXPORT int cgs_conv2d_nhwc(const void* x, const void* w, const void* bias, c
 CGS_EXPORT int cgs_conv2d_nhwc_ex(const void* x, const void* x2, int C1, const void* w, const void* bias,
                                   const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
                                   int stride, int pad, int Ho, int Wo, int flags, hipStream_t stream) {
-  if (Cin % 64 || (x2 && (C1 % 64)) || Cout < 1) return (int)hipErrorInvalidValue;
+  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && (Cin % 64 || (x2 && C1 % 64))))
+    return (int)hipErrorInvalidValue;
   ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
              Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
-             (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0};
+             (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0, 1};
   return conv_launch(a, stream);
+}
+
+// Per-call kernel choice for the autotuner (variant as in cgs_conv_set_variant; flags as _ex).
+CGS_EXPORT int cgs_conv2d_nhwc_v(const void* x, const void* x2, int C1, const void* w, const void* bias,
+                                 const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
+                                 int stride, int pad, int Ho, int Wo, int flags, int variant, hipStream_t stream) {
+  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && (Cin % 64 || (x2 && C1 % 64))))
+    return (int)hipErrorInvalidValue;
+  ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
+             Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
+             (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0, 1};
+  return conv_launch(a, stream, variant);
 }

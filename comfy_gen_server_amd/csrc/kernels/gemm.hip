@@ -11,6 +11,8 @@
 // lane groups and conflict-free ds_write_b128. 1-D grid with the XCD-aware bijective remap so
 // neighbouring output tiles (sharing A / W panels) run on the same XCD L2.
 #include "common.h"
+#include "mfma_core.h"
+#include "mfma_pp.h"
 
 #define G_BM 128
 #define G_BN 128
@@ -161,7 +163,7 @@ template <int BN>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_nt_v2_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_n) {
+    int epi, float alpha, int tiles_n, int group_m) {
   constexpr int BM = 256, BK = 64;
   constexpr int WN = BN / 4;          // wave N extent
   constexpr int NJ = WN / 16;         // 16-wide n tiles per wave
@@ -175,8 +177,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_nt_v2_kernel(
 
   const int nwg = gridDim.x;
   const int logical = xcd_remap(blockIdx.x, nwg);
-  const int tm = logical / tiles_n;
-  const int tn = logical % tiles_n;
+  int tm, tn;
+  grouped_tile(logical, nwg / tiles_n, tiles_n, group_m, tm, tn);
   const int m0 = tm * BM;
   const int n0 = tn * BN;
   const int tid = threadIdx.x;
@@ -297,6 +299,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_nt_v2_kernel(
   }
 }
 
+static int g_tile_group = 8;   // grouped tile order (rows per group); 1 = row-major
+CGS_EXPORT void cgs_set_tile_group(int g) { g_tile_group = g < 1 ? 1 : g; }
+
 static int gemm_v2_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                           long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                           hipStream_t stream) {
@@ -317,22 +322,126 @@ static int gemm_v2_launch(const void* A, const void* W, void* C, const void* bia
   if (wide) {
     gemm_bf16_nt_v2_kernel<256><<<(unsigned)nwg, 512, lds, stream>>>(
         (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_n);
+        alpha, tiles_n, g_tile_group);
   } else {
     gemm_bf16_nt_v2_kernel<128><<<(unsigned)nwg, 512, lds, stream>>>(
         (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_n);
+        alpha, tiles_n, g_tile_group);
   }
   return (int)hipGetLastError();
 }
 
-static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2 where legal
+// ------------------------------------------------------------------------------------------------
+// v3: 256 x BN x 32 tiles, 4 waves x (128 x BN/2) on 32x32x16 MFMA, 4-stage LDS-DMA ring
+// (mfma_core.h). Needs K % 32 == 0 and 16-B aligned rows.
+struct DenseA {
+  const u16* A;
+  long long lda;
+  int M;
+  const u16* p[4];
+  __device__ __forceinline__ void setup(int pi, int row) {
+    row = row < M ? row : M - 1;
+    p[pi] = A + (long long)row * lda + 8 * mc::src_chunk(threadIdx.x & 63);
+  }
+  __device__ __forceinline__ const void* src(int pi, int k0) const { return p[pi] + k0; }
+};
+
+template <int BN, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void gemm_bf16_nt_v3_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
+  DenseA al{A, lda, M, {}};
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
+  mc::tile<BN, NW>(al, W, ldw, M, N, K, tm * mc::BM, tn * BN, e, smem);
+}
+
+template <int BN, int NW>
+static void gemm_v3_go(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                       long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                       hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v3_kernel<BN, NW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, mc::Cfg<BN, NW>::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + BN - 1) / BN;
+  const long long nwg = (long long)((M + mc::BM - 1) / mc::BM) * tiles_n;
+  gemm_bf16_nt_v3_kernel<BN, NW><<<(unsigned)nwg, 64 * NW, mc::Cfg<BN, NW>::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+      tiles_n, g_tile_group);
+}
+
+static int gemm_v3_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha, int nw,
+                          hipStream_t stream) {
+  const int BN = mc::pick_bn(M, N);
+  if (nw == 8) {
+    if (BN == 256) gemm_v3_go<256, 8>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    else gemm_v3_go<128, 8>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  } else {
+    if (BN == 256) gemm_v3_go<256, 4>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    else gemm_v3_go<128, 4>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  }
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// v5: 256 x 256 x 64 ping-pong schedule (mfma_pp.h). Needs K % 64 == 0, N % 8 == 0, aligned rows.
+struct DenseA8 {
+  const u16* A;
+  long long lda;
+  int M;
+  const u16* p[4];
+  __device__ __forceinline__ void setup(int slot, int row) {
+    row = row < M ? row : M - 1;
+    p[slot] = A + (long long)row * lda + 8 * pp::src_chunk8(slot & 1);
+  }
+  __device__ __forceinline__ const void* src(int slot, int k0) const { return p[slot] + k0; }
+};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v5_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
+  DenseA8 al{A, lda, M, {}};
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
+  pp::tile(al, W, ldw, M, N, K, tm * pp::BM, tn * pp::BN, e, smem);
+}
+
+static int gemm_v5_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v5_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pp::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + pp::BN - 1) / pp::BN;
+  const long long nwg = (long long)((M + pp::BM - 1) / pp::BM) * tiles_n;
+  gemm_bf16_nt_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+      tiles_n, g_tile_group);
+  return (int)hipGetLastError();
+}
+
+static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 waves), 4 = v3 (8 waves), 5 = v5 ping-pong
 
 CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
 
-CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
-                             int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                             hipStream_t stream) {
+static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                         long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                         int variant, hipStream_t stream) {
   if (K % 8 || lda % 8 || ldw % 8) return (int)hipErrorInvalidValue;
   if ((epi & EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
@@ -340,10 +449,22 @@ CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* 
   // worth of work (otherwise the 128x128 kernel keeps more CUs busy).
   bool v2_ok = (K % 64 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M >= 256 && N >= 128 &&
                (((uintptr_t)A | (uintptr_t)W) % 16 == 0);
-  if (v2_ok && g_gemm_variant != 1) {
+  const int nout = (epi & EPI_GEGLU) ? N / 2 : N;
+  bool v3_ok = (K % 32 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && (nout % 8 == 0) && (ldc % 8 == 0) &&
+               (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
+               ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
+  if (v3_ok && K % 64 == 0 && variant == 5)
+    return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  if (v3_ok && (variant >= 3 || variant == -1)) {
+    long long t3 = (long long)((M + 255) / 256) * ((N + 127) / 128);
+    if (variant >= 3 || t3 >= 128)
+      return gemm_v3_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+                            variant == 3 ? 4 : 8, stream);
+  }
+  if (v2_ok && variant != 1 && variant < 3) {
     const int BN = N >= 1024 ? 256 : 128;
     long long t2 = (long long)((M + 255) / 256) * ((N + BN - 1) / BN);
-    if (g_gemm_variant == 2 || t2 >= 128)
+    if (variant == 2 || t2 >= 128)
       return gemm_v2_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   }
   int tiles_m = (M + G_BM - 1) / G_BM;
@@ -353,4 +474,17 @@ CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* 
                                                         (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
                                                         tiles_n);
   return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                             int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                             hipStream_t stream) {
+  return gemm_dispatch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, g_gemm_variant, stream);
+}
+
+// Per-call kernel choice (used by the op-layer autotuner): variant as in cgs_gemm_set_variant.
+CGS_EXPORT int cgs_gemm_bf16_v(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                               int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                               int variant, hipStream_t stream) {
+  return gemm_dispatch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, variant, stream);
 }

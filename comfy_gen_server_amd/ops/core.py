@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native
+from . import autotune
 from .dispatch import backend_for, count
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -50,17 +51,18 @@ def _ptr(t):
 # ----------------------------------------------------------------------------------------------
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            residual: torch.Tensor | None = None) -> torch.Tensor:
-    """y = x @ weight^T (+ bias) (+ residual). ``residual`` has y's shape (fused epilogue add)."""
+    """y = x @ weight^T (+ bias) (+ residual). ``residual`` has y's shape (fused epilogue add).
+
+    Device path: the HIP GEMM family (v5 ping-pong 256x256x64, v3 8-wave 32x32 MFMA, v1 128x128),
+    the kernel picked per shape by ``ops.autotune`` among those and hipBLASLt (through ATen)."""
     be = backend_for("gemm", x, "cgs_gemm_bf16")
     if be == "hip" and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
-        count("gemm", "hip")
         K = x.shape[-1]
         N = weight.shape[0]
         a = x.reshape(-1, K)
         if a.stride(-1) != 1 or (a.shape[0] > 1 and a.stride(0) < K):
             a = a.contiguous()
         M = a.shape[0]
-        out = torch.empty((M, N), device=x.device, dtype=x.dtype)
         epi = 0
         r = None
         if bias is not None:
@@ -71,10 +73,34 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             if not r.is_contiguous():
                 r = r.contiguous()
         w = weight if weight.is_contiguous() else weight.contiguous()
-        _check(_lib().cgs_gemm_bf16(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
-                                    M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
-                                    _stream()), "cgs_gemm_bf16")
-        return out.view(*x.shape[:-1], N)
+
+        def run_hip(variant):
+            out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+            _check(_lib().cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
+                                          M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
+                                          variant, _stream()), "cgs_gemm_bf16")
+            return out
+
+        def run_lib():
+            y = F.linear(a, w, bias)
+            return y if r is None else y.add_(r)
+
+        choice = "hip"
+        if M * N * K >= (1 << 27):
+            cands = []
+            if K % 64 == 0 and N % 8 == 0:
+                cands.append(("v5", lambda: run_hip(5)))
+            if K % 32 == 0 and N % 8 == 0:
+                cands.append(("v4", lambda: run_hip(4)))
+            cands.append(("hip", lambda: run_hip(-1)))
+            cands.append(("lib", run_lib))
+            choice = autotune.choose(("gemm", M, N, K, epi), cands, default="hip")
+        if choice == "lib":
+            count("gemm", "lib")
+            return run_lib().view(*x.shape[:-1], N)
+        count("gemm", "hip")
+        variant = {"v5": 5, "v4": 4}.get(choice, -1)
+        return run_hip(variant).view(*x.shape[:-1], N)
     count("gemm", "torch" if be == "torch" else "lib")
     if be == "torch":
         y = F.linear(x.float(), weight.float(), None if bias is None else bias.float())
@@ -102,11 +128,25 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
         if not a.is_contiguous():
             a = a.contiguous()
         M = a.shape[0]
-        out = torch.empty((M, N2 // 2), device=x.device, dtype=x.dtype)
         epi = EPI_GEGLU | (EPI_BIAS if bias is not None else 0)
-        _check(_lib().cgs_gemm_bf16(a.data_ptr(), weight.data_ptr(), out.data_ptr(), _ptr(bias), None,
-                                    M, N2, K, K, K, N2 // 2, 0, epi, 1.0, _stream()), "cgs_gemm_bf16")
-        return out.view(*x.shape[:-1], N2 // 2)
+
+        def run_hip(variant):
+            out = torch.empty((M, N2 // 2), device=x.device, dtype=x.dtype)
+            _check(_lib().cgs_gemm_bf16_v(a.data_ptr(), weight.data_ptr(), out.data_ptr(), _ptr(bias), None,
+                                          M, N2, K, K, K, N2 // 2, 0, epi, 1.0, variant, _stream()),
+                   "cgs_gemm_bf16")
+            return out
+
+        choice = "hip"
+        if M * N2 * K >= (1 << 27) and K % 32 == 0:
+            cands = []
+            if K % 64 == 0:
+                cands.append(("v5", lambda: run_hip(5)))
+            cands.append(("v4", lambda: run_hip(4)))
+            cands.append(("hip", lambda: run_hip(-1)))
+            choice = autotune.choose(("gemm_geglu", M, N2, K, epi), cands, default="hip")
+        variant = {"v5": 5, "v4": 4}.get(choice, -1)
+        return run_hip(variant).view(*x.shape[:-1], N2 // 2)
     count("gemm_geglu", be)
     # reference path expects the *interleaved* weight too, undo it
     w = geglu_deinterleave(weight)
@@ -162,20 +202,47 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     be = backend_for("attention", q, "cgs_flash_attn_fwd")
     if (be == "hip" and mask is None and D in _FLASH_HEAD_DIMS and q.dtype == torch.bfloat16
             and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1):
-        count("attention", "hip")
-        o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
         kp = None
         if key_padding is not None:
             kp = key_padding.to(torch.int8).contiguous()
-        _check(_lib().cgs_flash_attn_fwd(
-            q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
-            B, heads, Sq, Sk, D,
-            q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
-            o.stride(0), o.stride(1), D,
-            1.0 / math.sqrt(D), _ptr(kp), 1 if causal else 0, _stream()), "cgs_flash_attn_fwd")
-        return o
+
+        def run_hip():
+            o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
+            _check(_lib().cgs_flash_attn_fwd(
+                q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                B, heads, Sq, Sk, D,
+                q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
+                o.stride(0), o.stride(1), D,
+                1.0 / math.sqrt(D), _ptr(kp), 1 if causal else 0, _stream()), "cgs_flash_attn_fwd")
+            return o
+
+        choice = "hip"
+        if kp is None and B * heads * Sq * Sk >= (1 << 22):
+            choice = autotune.choose(("attention", B, heads, Sq, Sk, D, int(causal)),
+                                     [("hip", run_hip), ("lib", lambda: _sdpa(q, k, v, heads, causal))],
+                                     default="hip")
+        if choice == "lib":
+            count("attention", "lib")
+            return _sdpa(q, k, v, heads, causal)
+        count("attention", "hip")
+        return run_hip()
+    if q.device.type != "cpu" and mask is None and key_padding is None:
+        count("attention", "lib")
+        return _sdpa(q, k, v, heads, causal)
     count("attention", "torch" if q.device.type == "cpu" else "lib")
     return attention_reference(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
+
+
+def _sdpa(q, k, v, heads, causal=False):
+    """Vendor attention through ATen (ROCm SDPA); layout [B,S,H*D] in and out."""
+    B, Sq, HD = q.shape
+    Sk = k.shape[1]
+    D = HD // heads
+    qh = q.view(B, Sq, heads, D).transpose(1, 2)
+    kh = k.view(B, Sk, heads, D).transpose(1, 2) if k.is_contiguous() else k.reshape(B, Sk, heads, D).transpose(1, 2)
+    vh = v.view(B, Sk, heads, D).transpose(1, 2) if v.is_contiguous() else v.reshape(B, Sk, heads, D).transpose(1, 2)
+    o = F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal)
+    return o.transpose(1, 2).reshape(B, Sq, HD)
 
 
 def attention_reference(q, k, v, heads, mask=None, causal=False, key_padding=None):
@@ -274,7 +341,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
     be = backend_for("conv", x, "cgs_conv2d_nhwc")
     Cout, Cin_g, kh, kw = weight.shape
     if (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
-            and x.shape[1] % 64 == 0 and x.dim() == 4):
+            and x.dim() == 4 and x.shape[1] % 32 == 0 and (Cout % 8 == 0 or x.shape[1] % 64 == 0)):
         count("conv", "hip")
         N, Cin, H, W = x.shape
         Hl, Wl = (2 * H, 2 * W) if upsample2x else (H, W)
@@ -286,15 +353,26 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         r = None
         if residual is not None:
             r = residual.contiguous(memory_format=torch.channels_last)
-        if upsample2x:
-            _check(_lib().cgs_conv2d_nhwc_ex(xc.data_ptr(), None, Cin, weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
-                                             out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
-                                             Ho, Wo, 16, _stream()), "cgs_conv2d_nhwc_ex")
-        else:
-            _check(_lib().cgs_conv2d_nhwc(xc.data_ptr(), weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
-                                          out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
-                                          Ho, Wo, _stream()), "cgs_conv2d_nhwc")
-        return out
+        flags = 16 if upsample2x else 0
+
+        def run(variant):
+            out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype,
+                              memory_format=torch.channels_last)
+            _check(_lib().cgs_conv2d_nhwc_v(xc.data_ptr(), None, Cin, weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
+                                            out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding, Ho, Wo,
+                                            flags, variant, _stream()), "cgs_conv2d_nhwc")
+            return out
+
+        variant = -1
+        M = N * Ho * Wo
+        if M * Cout * Cin * kh * kw >= (1 << 27):
+            cands = [("v4", lambda: run(4))]
+            if Cin % 64 == 0:
+                cands += [("v5", lambda: run(5)), ("v2", lambda: run(2))]
+            choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None)),
+                                     cands, default="v4")
+            variant = {"v2": 2, "v4": 4, "v5": 5}[choice]
+        return run(variant)
     if upsample2x:
         x = upsample_nearest2x(x)
     if be == "torch":

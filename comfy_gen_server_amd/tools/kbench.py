@@ -51,10 +51,13 @@ def main(quick=False):
         fl = 2.0 * M * N * K
         lib = ops.dispatch._native.load_kernels()
         ent = dict(M=M, N=N, K=K)
-        for var in (1, 2):
+        for var in (1, 2, 3, 4, 5):
             lib.cgs_gemm_set_variant(var)
-            t = _time(lambda: ops.linear(a, w, bias))
-            ent[f"v{var}_tflops"] = fl / t / 1e9
+            for g in ((1, 8) if var >= 3 else (8,)):
+                lib.cgs_set_tile_group(g)
+                t = _time(lambda: ops.linear(a, w, bias))
+                ent[f"v{var}g{g}_tflops"] = fl / t / 1e9
+        lib.cgs_set_tile_group(8)
         lib.cgs_gemm_set_variant(-1)
         t_lib = _time(lambda: F.linear(a, w, bias))
         ent["lib_tflops"] = fl / t_lib / 1e9
@@ -90,7 +93,8 @@ def main(quick=False):
         t_lib = _time(lambda: F.layer_norm(x, (C,), wt, bt))
         res["layernorm"].append(dict(rows=rows, C=C, hip_ms=t_hip, lib_ms=t_lib, hip_GBps=nbytes / t_hip / 1e6,
                                      lib_GBps=nbytes / t_lib / 1e6))
-    for N, Ci, H, W, Co in [(B, 320, 128, 128, 320), (B, 640, 64, 64, 640), (B, 1280, 32, 32, 1280)]:
+    for N, Ci, H, W, Co in [(B, 320, 128, 128, 320), (B, 640, 64, 64, 640), (B, 1280, 32, 32, 1280),
+                            (B, 1920, 32, 32, 1280), (1, 256, 512, 512, 256), (1, 128, 1024, 1024, 128)]:
         x = torch.randn(N, Ci, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         wt = (torch.randn(Co, Ci, 3, 3, device=dev) / math.sqrt(Ci * 9)).to(torch.bfloat16)
         bt = torch.randn(Co, device=dev).to(torch.bfloat16)
@@ -100,9 +104,16 @@ def main(quick=False):
         if ops.dispatch._native.has_kernel("cgs_conv2d_nhwc"):
             wn = wt.permute(0, 2, 3, 1).contiguous()
             set_backend_override("conv", "hip")
-            t_hip = _time(lambda: ops.conv2d(x, wt, bt, 1, 1, weight_nhwc=wn))
+            lib = ops.dispatch._native.load_kernels()
+            for var in (2, 3, 4, 5):
+                lib.cgs_conv_set_variant(var)
+                for g in (8,):
+                    lib.cgs_conv_set_tile_group(g)
+                    t_hip = _time(lambda: ops.conv2d(x, wt, bt, 1, 1, weight_nhwc=wn))
+                    entry.update({f"v{var}g{g}_tflops": fl / t_hip / 1e9})
+            lib.cgs_conv_set_tile_group(8)
+            lib.cgs_conv_set_variant(-1)
             set_backend_override("conv", None)
-            entry.update(hip_ms=t_hip, hip_tflops=fl / t_hip / 1e9)
         res["conv"].append(entry)
     print(json.dumps(res, indent=1))
     return res

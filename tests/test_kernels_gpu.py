@@ -14,8 +14,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _native_loaded(cuda):
+def _native_loaded(cuda, monkeypatch):
     assert _native.load_kernels() is not None, _native.kernels_error()
+    monkeypatch.setenv("CGS_AUTOTUNE", "0")    # variant fixtures pick the kernel explicitly
     ops.reset_stats()
     yield
 
@@ -92,7 +93,7 @@ def test_flash_attention_causal_and_spike(cuda):
     assert _rel(o, ref) < 2e-2
 
 
-@pytest.fixture(params=[1, 2], ids=["v1", "v2"])
+@pytest.fixture(params=[1, 2, 3, 4, 5], ids=["v1", "v2", "v3w4", "v3w8", "v5pp"])
 def gemm_variant(request):
     lib = _native.load_kernels()
     lib.cgs_gemm_set_variant(request.param)
@@ -101,7 +102,8 @@ def gemm_variant(request):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 320, 640), (154, 1280, 2048), (4096, 1280, 1280),
-                                   (77, 768, 768), (2, 1280, 2816), (1000, 640, 320), (512, 3840, 1280)])
+                                   (77, 768, 768), (2, 1280, 2816), (1000, 640, 320), (512, 3840, 1280),
+                                   (1100, 328, 96), (513, 2560, 32), (700, 1280, 640), (2048, 2048, 2048)])
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
 def test_gemm(cuda, M, N, K, epi, gemm_variant):
     torch.manual_seed(0)
@@ -158,12 +160,23 @@ def test_elementwise(cuda):
     assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
 
 
+@pytest.fixture(params=[2, 3, 4, 5], ids=["cv2", "cv3w4", "cv3w8", "cv5pp"])
+def conv_variant(request):
+    lib = _native.load_kernels()
+    lib.cgs_conv_set_variant(request.param)
+    yield request.param
+    lib.cgs_conv_set_variant(-1)
+
+
 @pytest.mark.parametrize("N,Cin,H,W,Cout,k,s,p", [(2, 64, 16, 16, 64, 3, 1, 1), (2, 320, 32, 32, 320, 3, 1, 1),
                                                   (1, 640, 16, 16, 1280, 3, 1, 1), (2, 320, 32, 32, 320, 3, 2, 1),
                                                   (1, 128, 7, 9, 256, 1, 1, 0), (3, 256, 11, 5, 4, 3, 1, 1),
-                                                  (1, 1920, 8, 8, 1280, 1, 1, 0), (2, 512, 12, 12, 3, 3, 1, 1)])
+                                                  (1, 1920, 8, 8, 1280, 1, 1, 0), (2, 512, 12, 12, 3, 3, 1, 1),
+                                                  (2, 96, 20, 20, 160, 3, 1, 1), (1, 320, 33, 17, 640, 3, 2, 1)])
 @pytest.mark.parametrize("epi", ["bias", "bias_res", "none"])
-def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi):
+def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi, conv_variant):
+    if conv_variant in (2, 5) and Cin % 64:
+        pytest.skip("v2/v5 need Cin % 64")
     torch.manual_seed(0)
     x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Cout, Cin, k, k, device=cuda) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
@@ -180,7 +193,7 @@ def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi):
 
 
 @pytest.mark.parametrize("N,C,H,W,Cout", [(2, 320, 8, 8, 320), (1, 640, 5, 7, 640), (2, 128, 16, 16, 128)])
-def test_conv2d_fused_upsample(cuda, N, C, H, W, Cout):
+def test_conv2d_fused_upsample(cuda, N, C, H, W, Cout, conv_variant):
     torch.manual_seed(0)
     x = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Cout, C, 3, 3, device=cuda) / math.sqrt(C * 9)).to(torch.bfloat16)
@@ -190,3 +203,27 @@ def test_conv2d_fused_upsample(cuda, N, C, H, W, Cout):
     assert ops.stats().get(("conv", "hip"), 0) == 1
     assert y.shape == ref.shape
     assert _rel(y, ref) < 1e-2
+
+
+def test_autotuned_ops_match_reference(cuda, monkeypatch):
+    """With the measured dispatch on, whatever candidate wins must still be numerically right."""
+    from comfy_gen_server_amd.ops import autotune
+    monkeypatch.setenv("CGS_AUTOTUNE", "1")
+    autotune.reset()
+    torch.manual_seed(0)
+    M, N, K = 4096, 1280, 1280
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16)
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    y = ops.linear(a, w, b, residual=r)
+    assert _rel(y, a.float() @ w.float().t() + b.float() + r.float()) < 1e-2
+    x = torch.randn(4, 320, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    cw = (torch.randn(320, 320, 3, 3, device=cuda) / math.sqrt(320 * 9)).to(torch.bfloat16)
+    yc = ops.conv2d(x, cw, None, 1, 1, weight_nhwc=cw.permute(0, 2, 3, 1).contiguous())
+    assert _rel(yc, F.conv2d(x.float(), cw.float(), None, 1, 1)) < 1e-2
+    q = torch.randn(4, 1024, 640, device=cuda).to(torch.bfloat16)
+    o = ops.attention(q, q, q, 10)
+    assert _rel(o, core.attention_reference(q.float(), q.float(), q.float(), 10)) < 2e-2
+    t = autotune.table()
+    assert any(k.startswith("gemm|") for k in t) and any(k.startswith("conv|") for k in t)
