@@ -72,7 +72,10 @@ def load_custom_node(module_path, ignore=set(), module_parent="custom_nodes"):
         return False
 
 
-def execute_prestartup_scripts(custom_node_dirs):
+def execute_prestartup_scripts(custom_node_dirs=None):
+    if custom_node_dirs is None:
+        from ..utils import folder_paths
+        custom_node_dirs = folder_paths.get_folder_paths("custom_nodes")
     for d in custom_node_dirs:
         if not os.path.isdir(d):
             continue
