@@ -155,3 +155,15 @@ def tensor_to_pil(t):
     from PIL import Image
     arr = np.clip(255.0 * t.detach().float().cpu().numpy(), 0, 255).astype(np.uint8)
     return Image.fromarray(arr)
+
+
+def repeat_to_batch_size(tensor, batch_size, dim=0):
+    """Tile (then truncate) along ``dim`` to ``batch_size`` (comfy/utils.py repeat_to_batch_size)."""
+    n = tensor.shape[dim]
+    if n > batch_size:
+        return tensor.narrow(dim, 0, batch_size)
+    if n < batch_size:
+        reps = [1] * tensor.ndim
+        reps[dim] = math.ceil(batch_size / n)
+        return tensor.repeat(reps).narrow(dim, 0, batch_size)
+    return tensor

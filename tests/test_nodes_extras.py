@@ -1,0 +1,101 @@
+"""CPU unit tests for the extra node modules (reference: comfy_extras/*)."""
+import math
+
+import pytest
+import torch
+
+from comfy_gen_server_amd.runtime import device as dm
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _cpu():
+    dm.set_cpu_mode(True)
+    from comfy_gen_server_amd.graph import registry
+    registry.init_nodes(custom_nodes=False)
+
+
+def N(name):
+    from comfy_gen_server_amd.graph import registry
+    return registry.NODE_CLASS_MAPPINGS[name]()
+
+
+def test_registry_has_extras():
+    from comfy_gen_server_amd.graph import registry
+    for n in ("SamplerCustomAdvanced", "KarrasScheduler", "LatentInterpolate", "RebatchLatents", "GrowMask",
+              "PorterDuffImageComposite", "Canny", "Morphology", "ImageBlend", "AlignYourStepsScheduler"):
+        assert n in registry.NODE_CLASS_MAPPINGS, n
+
+
+def test_schedulers_and_sigma_ops():
+    s = N("KarrasScheduler").get_sigmas(10, 14.6, 0.03, 7.0)[0]
+    assert s.shape[0] == 11 and s[-1] == 0 and torch.all(s[:-1] > s[1:-1].min() - 1)
+    a, b = N("SplitSigmas").get_sigmas(s, 4)
+    assert torch.equal(torch.cat([a, b[1:]]), s)
+    f = N("FlipSigmas").get_sigmas(s)[0]
+    assert f[0] > 0 and f[-1] == s[0]
+    ays = N("AlignYourStepsScheduler").get_sigmas("SDXL", 10, 1.0)[0]
+    assert ays.shape[0] == 11 and ays[-1] == 0
+
+
+def test_latent_ops():
+    a = {"samples": torch.randn(2, 4, 8, 8)}
+    b = {"samples": torch.randn(1, 4, 4, 4)}
+    s = N("LatentAdd").op(a, b)[0]["samples"]
+    assert s.shape == (2, 4, 8, 8)
+    i = N("LatentInterpolate").op(a, a, 0.3)[0]["samples"]
+    assert torch.allclose(i, a["samples"], atol=1e-5)
+    bt = N("LatentBatch").batch(a, a)[0]
+    assert bt["samples"].shape[0] == 4 and bt["batch_index"] == [0, 1, 0, 1]
+    rb = N("RebatchLatents").rebatch([a, a, {"samples": torch.zeros(3, 4, 16, 16)}], [3])[0]
+    assert [r["samples"].shape[0] for r in rb] == [3, 1, 3]
+
+
+def test_mask_ops():
+    m = torch.zeros(1, 9, 9)
+    m[0, 4, 4] = 1.0
+    g = N("GrowMask").expand_mask(m, 1, True)[0]
+    assert g.sum() == 5            # cross footprint
+    g2 = N("GrowMask").expand_mask(m, 1, False)[0]
+    assert g2.sum() == 9
+    assert N("GrowMask").expand_mask(g2, -1, False)[0].sum() == 1
+    f = N("FeatherMask").feather(torch.ones(1, 4, 8), 0, 0, 4, 0)[0]
+    assert f[0, 0, -1] == pytest.approx(0.25) and f[0, 0, 0] == 1.0
+    c = N("MaskComposite").combine(torch.ones(1, 4, 4), torch.zeros(1, 2, 2), 1, 1, "multiply")[0]
+    assert c.sum() == 12
+    img = torch.rand(1, 8, 8, 3)
+    d = {"samples": torch.zeros(1, 4, 8, 8)}
+    out = N("LatentCompositeMasked").composite(d, {"samples": torch.ones(1, 4, 2, 2)}, 16, 8, False)[0]
+    assert out["samples"].sum() == 16 and out["samples"][0, 0, 1, 2] == 1
+    assert N("ImageCompositeMasked").composite(img, img, 0, 0, False)[0].shape == img.shape
+
+
+def test_image_postprocessing():
+    img = torch.rand(2, 16, 16, 3)
+    assert N("ImageBlur").blur(img, 2, 1.0)[0].shape == img.shape
+    const = torch.full((1, 8, 8, 3), 0.5)
+    assert torch.allclose(N("ImageSharpen").sharpen(const, 1, 1.0, 1.0)[0], const, atol=1e-5)
+    assert torch.allclose(N("ImageBlend").blend_images(img, img, 0.5, "normal")[0], img, atol=1e-6)
+    q = N("ImageQuantize").quantize(img, 4, "bayer-4")[0]
+    assert all(len(torch.unique(q[b].reshape(-1, 3), dim=0)) <= 4 for b in range(2))
+    mp = N("ImageScaleToTotalPixels").upscale(img, "bilinear", 0.0625)[0]
+    assert mp.shape[1] * mp.shape[2] == pytest.approx(0.0625 * 1024 * 1024, rel=0.05)
+    rgb, a = N("SplitImageWithAlpha").split_image_with_alpha(torch.rand(1, 4, 4, 4))
+    j = N("JoinImageWithAlpha").join_image_with_alpha(rgb, a)[0]
+    assert j.shape[-1] == 4
+    pd = N("PorterDuffImageComposite").composite(img, torch.ones(2, 16, 16), img * 0, torch.ones(2, 16, 16),
+                                                 "SRC_OVER")
+    assert torch.allclose(pd[0], img)
+
+
+def test_morphology_and_canny():
+    img = torch.zeros(1, 32, 32, 3)
+    img[:, 8:24, 8:24, :] = 1.0
+    d = N("Morphology").process(img, "dilate", 3)[0]
+    assert d[0, 7, 7, 0] == 1 and d[0, 6, 6, 0] == 0
+    e = N("Morphology").process(img, "erode", 3)[0]
+    assert e[0, 8, 8, 0] == 0 and e[0, 9, 9, 0] == 1
+    grad = N("Morphology").process(img, "gradient", 3)[0]
+    assert grad[0, 16, 16, 0] == 0 and grad[0, 8, 16, 0] == 1
+    edges = N("Canny").detect_edge(img, 0.2, 0.5)[0]
+    assert edges[0, 16, 16, 0] == 0 and edges[0, 2, 2, 0] == 0
+    assert edges[0, :, 7:9, 0].sum() > 8            # left border of the square is an edge
