@@ -372,13 +372,8 @@ class Guider_PerpNeg(SM.CFGGuider):
 
 
 def perp_neg_combine(x, pos_out, neg_out, empty_out, neg_scale, cond_scale):
-    pos = pos_out - empty_out
-    neg = neg_out - empty_out
-    dims = tuple(range(1, pos.ndim))
-    perp = neg - (torch.mul(neg, pos).sum(dim=dims, keepdim=True) /
-                  (torch.norm(pos, dim=dims, keepdim=True) ** 2).clamp_min(1e-12)) * pos
-    perp_neg = perp * neg_scale
-    return empty_out + cond_scale * (pos - perp_neg)
+    from .extras_model import perp_neg
+    return perp_neg(x, pos_out, neg_out, empty_out, neg_scale, cond_scale)
 
 
 class BasicGuider:

@@ -197,6 +197,11 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     ``causal``: CLIP causal mask; ``key_padding``: bool [B,Sk] True = attend.
     """
     B, Sq, HD = q.shape
+    if k.shape[0] != B:
+        # reference semantics when a patch re-batched the queries only (e.g. HyperTile): keys/values
+        # are re-viewed with the query batch, i.e. split into contiguous token chunks (attention.py:337-350)
+        k = k.reshape(B, -1, k.shape[-1])
+        v = v.reshape(B, -1, v.shape[-1])
     Sk = k.shape[1]
     D = HD // heads
     be = backend_for("attention", q, "cgs_flash_attn_fwd")

@@ -99,3 +99,78 @@ def test_morphology_and_canny():
     edges = N("Canny").detect_edge(img, 0.2, 0.5)[0]
     assert edges[0, 16, 16, 0] == 0 and edges[0, 2, 2, 0] == 0
     assert edges[0, :, 7:9, 0].sum() > 8            # left border of the square is an edge
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    patcher, clip, vae = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=0)
+    pos = N("CLIPTextEncode").encode(clip, "a cat")[0]
+    neg = N("CLIPTextEncode").encode(clip, "")[0]
+    return patcher, clip, vae, pos, neg
+
+
+def _sample(model, pos, neg, steps=2, sampler="euler", latent=None):
+    latent = latent or {"samples": torch.zeros(2, 4, 16, 16)}
+    return N("KSampler").sample(model, 1, steps, 5.0, sampler, "normal", pos, neg, latent, 1.0)[0]["samples"]
+
+
+@pytest.mark.parametrize("patch", ["freeu", "freeu2", "rescale", "sag", "pag", "perpneg", "hypertile", "tome",
+                                   "downscale", "msd_v", "msd_lcm_zsnr", "edm", "video_lin", "video_tri"])
+def test_model_patches_run(tiny, patch):
+    patcher, clip, vae, pos, neg = tiny
+    base = _sample(patcher, pos, neg)
+    if patch == "freeu":
+        m = N("FreeU").patch(patcher, 1.1, 1.2, 0.9, 0.2)[0]
+    elif patch == "freeu2":
+        m = N("FreeU_V2").patch(patcher, 1.3, 1.4, 0.9, 0.2)[0]
+    elif patch == "rescale":
+        m = N("RescaleCFG").patch(patcher, 0.7)[0]
+    elif patch == "sag":
+        m = N("SelfAttentionGuidance").patch(patcher, 0.5, 2.0)[0]
+    elif patch == "pag":
+        m = N("PerturbedAttentionGuidance").patch(patcher, 3.0)[0]
+    elif patch == "perpneg":
+        m = N("PerpNeg").patch(patcher, neg, 1.0)[0]
+    elif patch == "hypertile":
+        m = N("HyperTile").patch(patcher, 64, 2, 0, False)[0]
+    elif patch == "tome":
+        m = N("TomePatchModel").patch(patcher, 0.3)[0]
+    elif patch == "downscale":
+        m = N("PatchModelAddDownscale").patch(patcher, 1, 2.0, 0.0, 1.0, True, "bicubic", "bicubic")[0]
+    elif patch == "msd_v":
+        m = N("ModelSamplingDiscrete").patch(patcher, "v_prediction", False)[0]
+    elif patch == "msd_lcm_zsnr":
+        m = N("ModelSamplingDiscrete").patch(patcher, "lcm", True)[0]
+    elif patch == "edm":
+        m = N("ModelSamplingContinuousEDM").patch(patcher, "v_prediction", 120.0, 0.002)[0]
+    elif patch == "video_lin":
+        m = N("VideoLinearCFGGuidance").patch(patcher, 1.0)[0]
+    else:
+        m = N("VideoTriangleCFGGuidance").patch(patcher, 1.0)[0]
+    out = _sample(m, pos, neg)
+    assert out.shape == base.shape and torch.isfinite(out).all()
+    # the base patcher is untouched (clone semantics)
+    assert torch.allclose(_sample(patcher, pos, neg), base)
+
+
+def test_differential_diffusion_and_custom_sampler(tiny):
+    patcher, clip, vae, pos, neg = tiny
+    m = N("DifferentialDiffusion").apply(patcher)[0]
+    lat = {"samples": torch.zeros(1, 4, 16, 16), "noise_mask": torch.linspace(0, 1, 256).reshape(1, 16, 16)}
+    out = N("KSampler").sample(m, 1, 3, 5.0, "euler", "normal", pos, neg, lat, 1.0)[0]["samples"]
+    assert torch.isfinite(out).all()
+    sig = N("BasicScheduler").get_sigmas(patcher, "karras", 3, 1.0)[0]
+    for guider in (N("CFGGuider").get_guider(patcher, pos, neg, 5.0)[0],
+                   N("DualCFGGuider").get_guider(patcher, pos, pos, neg, 5.0, 3.0)[0],
+                   N("BasicGuider").get_guider(patcher, pos)[0],
+                   N("PerpNegGuider").get_guider(patcher, pos, neg, neg, 5.0, 1.0)[0]):
+        out, den = N("SamplerCustomAdvanced").sample(N("RandomNoise").get_noise(3)[0], guider,
+                                                     N("KSamplerSelect").get_sampler("dpmpp_2m")[0], sig,
+                                                     {"samples": torch.zeros(1, 4, 16, 16)})
+        assert out["samples"].shape == (1, 4, 16, 16) and torch.isfinite(den["samples"]).all()
+    o1, _ = N("SamplerCustom").sample(patcher, True, 5, 5.0, pos, neg,
+                                      N("SamplerEulerAncestral").get_sampler(1.0, 1.0)[0], sig,
+                                      {"samples": torch.zeros(1, 4, 16, 16)})
+    noisy = N("AddNoise").add_noise(patcher, N("RandomNoise").get_noise(3)[0], sig, o1)[0]
+    assert noisy["samples"].shape == o1["samples"].shape
