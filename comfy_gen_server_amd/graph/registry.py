@@ -21,7 +21,7 @@ NODE_DISPLAY_NAME_MAPPINGS: dict = {}
 EXTENSION_WEB_DIRS: dict = {}
 LOADED_MODULE_DIRS: dict = {}
 
-_CORE_MODULES = ["core", "extras_sampling", "extras_latent", "extras_image", "extras_mask", "extras_model",
+_CORE_MODULES = ["core", "extras_sampling", "extras_latent", "extras_image", "extras_mask", "extras_model", "extras_merge",
                  "extras_conditioning", "extras_cascade", "extras_video", "extras_upscale", "extras_misc"]
 _initialized = False
 

@@ -174,3 +174,62 @@ def test_differential_diffusion_and_custom_sampler(tiny):
                                       {"samples": torch.zeros(1, 4, 16, 16)})
     noisy = N("AddNoise").add_noise(patcher, N("RandomNoise").get_noise(3)[0], sig, o1)[0]
     assert noisy["samples"].shape == o1["samples"].shape
+
+
+def test_clip_vision_and_image_conditioning(tiny, tmp_path):
+    from comfy_gen_server_amd.models.layers import init_random_
+    from comfy_gen_server_amd.runtime import clip_vision as CV
+    patcher, clip, vae, pos, neg = tiny
+    cfg = dict(hidden_size=64, intermediate_size=128, num_attention_heads=2, num_hidden_layers=3,
+               hidden_act="gelu", projection_dim=32, patch_size=14, image_size=224)
+    cv = CV.ClipVisionModel(cfg)
+    init_random_(cv.model, seed=1)
+    img = torch.rand(1, 300, 200, 3)
+    out = cv.encode_image(img)
+    assert out.image_embeds.shape == (1, 32) and out.last_hidden_state.shape == (1, 257, 64)
+    assert out.penultimate_hidden_states.shape == (1, 257, 64)
+    px = CV.clip_preprocess(img)
+    assert px.shape == (1, 3, 224, 224)
+    # OpenCLIP-layout round trip through the converter (H/G/L detection needs full depth; check keys)
+    sd = {f"visual.transformer.resblocks.0.attn.in_proj_weight": torch.zeros(192, 64),
+          "visual.conv1.weight": torch.zeros(64, 3, 14, 14), "visual.proj": torch.zeros(64, 32)}
+    conv = CV.convert_to_transformers(dict(sd), "visual.")
+    assert "vision_model.encoder.layers.0.self_attn.q_proj.weight" in conv
+    assert conv["visual_projection.weight"].shape == (32, 64)
+    p2, n2, lat = N("StableZero123_Conditioning").encode(cv, img, vae, 64, 64, 2, 10.0, 30.0)
+    assert p2[0][0].shape == (1, 1, 36) and lat["samples"].shape == (2, 4, 8, 8)
+    p3, _, lat3 = N("SV3D_Conditioning").encode(cv, img, vae, 64, 64, 5, 10.0)
+    assert len(p3[0][1]["azimuth"]) == 5 and lat3["samples"].shape[0] == 5
+    p4, _, lat4 = N("SVD_img2vid_Conditioning").encode(cv, img, vae, 64, 64, 3, 127, 6, 0.0)
+    assert p4[0][1]["motion_bucket_id"] == 127 and lat4["samples"].shape == (3, 4, 8, 8)
+    ip, _, il = N("InstructPixToPixConditioning").encode(pos, neg, torch.rand(1, 67, 65, 3), vae)
+    assert ip[0][1]["concat_latent_image"].shape[-2:] == (8, 8)
+    sx = N("CLIPTextEncodeSDXLRefiner").encode(clip, 6.0, 1024, 1024, "x")[0]
+    assert sx[0][1]["aesthetic_score"] == 6.0
+
+
+def test_merge_and_save_roundtrip(tiny, tmp_path):
+    import os
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    from comfy_gen_server_amd.utils import folder_paths
+    patcher, clip, vae, pos, neg = tiny
+    other, _, _ = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=7, with_clip=False,
+                                 with_vae=False)
+    ref1 = _sample(patcher, pos, neg)
+    ref2 = _sample(other, pos, neg)
+    m1 = N("ModelMergeSimple").merge(patcher, other, 1.0)[0]       # ratio 1.0 keeps model1
+    assert torch.allclose(_sample(m1, pos, neg), ref1, atol=1e-5)
+    m0 = N("ModelMergeSimple").merge(patcher, other, 0.0)[0]       # ratio 0.0 -> model2 weights
+    assert torch.allclose(_sample(m0, pos, neg), ref2, atol=1e-4)
+    mb = N("ModelMergeBlocks").merge(patcher, other, input=1.0, middle=1.0, out=1.0)[0]
+    assert torch.allclose(_sample(mb, pos, neg), ref1, atol=1e-5)
+    folder_paths.set_output_directory(str(tmp_path))
+    N("CheckpointSave").save(patcher, clip, vae, "checkpoints/rt")
+    files = os.listdir(tmp_path / "checkpoints")
+    assert len(files) == 1 and files[0].endswith(".safetensors")
+    from comfy_gen_server_amd.runtime import sd as sdl
+    mp, cl, va, _ = sdl.load_checkpoint_guess_config(str(tmp_path / "checkpoints" / files[0]))
+    assert torch.allclose(_sample(mp, pos, neg), ref1, atol=1e-4)
+    N("VAESave").save(vae, "vae/v")
+    N("CLIPSave").save(clip, "clip/c")
+    assert os.listdir(tmp_path / "vae") and os.listdir(tmp_path / "clip")
