@@ -31,6 +31,12 @@ class _Seq(nn.Module):
     def __getitem__(self, i):
         return self._modules[str(i)]
 
+    def __iter__(self):
+        return iter(self._modules.values())
+
+    def __len__(self):
+        return len(self._modules)
+
 
 class CrossAttention(nn.Module, DerivedMixin):
     def __init__(self, query_dim, context_dim=None, heads=8, dim_head=64, dtype=None, device=None):

@@ -114,7 +114,7 @@ class UNetModel(nn.Module):
                  transformer_depth_output=None, context_dim=None, num_heads=-1, num_head_channels=-1,
                  use_linear_in_transformer=False, adm_in_channels=None, num_classes=None,
                  disable_self_attentions=None, use_temporal_attention=False, dtype=torch.float32,
-                 device=None, **unused):
+                 device=None, build_decoder=True, **unused):
         super().__init__()
         nl = len(channel_mult)
         if isinstance(num_res_blocks, int):
@@ -184,6 +184,10 @@ class UNetModel(nn.Module):
                         ResBlock(ch, ted, ch, **kw)]
             self.middle_block = TimestepEmbedSequential(mid)
 
+        self._encoder_channels = list(chans)
+        self._mid_channels = ch
+        if not build_decoder:          # ControlNet: encoder + middle only (models/cldm.py)
+            return
         self.output_blocks = nn.ModuleList([])
         tdo = list(transformer_depth_output)
         for level, mult in list(enumerate(channel_mult))[::-1]:

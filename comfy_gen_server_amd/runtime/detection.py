@@ -155,3 +155,63 @@ def convert_config(unet_config):
         cfg.update(transformer_depth=t_in, transformer_depth_output=t_out, transformer_depth_middle=tdm)
     cfg["num_res_blocks"] = nrb
     return cfg
+
+
+# ------------------------------------------------------------------------------------------------
+# diffusers layout (parity: model_detection.py:240-377 — the reference matches 16 fixed templates;
+# here the same config is derived from the tensors, and heads follow the ldm rule: SD1.x (context
+# 768) uses 8 heads, everything else 64-wide heads)
+# ------------------------------------------------------------------------------------------------
+def unet_config_from_diffusers_unet(sd, dtype=None):
+    keys = set(sd.keys())
+    w_in = sd["conv_in.weight"]
+    model_channels, in_channels = w_in.shape[0], w_in.shape[1]
+    levels = count_blocks(keys, "down_blocks.{}.")
+    num_res_blocks, channel_mult, transformer_depth = [], [], []
+    context_dim, use_linear = None, False
+    for i in range(levels):
+        nrb = count_blocks(keys, f"down_blocks.{i}.resnets." + "{}.")
+        num_res_blocks.append(nrb)
+        channel_mult.append(sd[f"down_blocks.{i}.resnets.0.conv2.weight"].shape[0] // model_channels)
+        for j in range(nrb):
+            d = count_blocks(keys, f"down_blocks.{i}.attentions.{j}.transformer_blocks." + "{}.")
+            transformer_depth.append(d)
+            if d and context_dim is None:
+                context_dim = sd[f"down_blocks.{i}.attentions.{j}.transformer_blocks.0.attn2.to_k.weight"].shape[1]
+                use_linear = sd[f"down_blocks.{i}.attentions.{j}.proj_in.weight"].ndim == 2
+    tdm = count_blocks(keys, "mid_block.attentions.0.transformer_blocks.{}.")
+    if tdm == 0 and "mid_block.resnets.0.conv1.weight" in keys and "mid_block.attentions.0.proj_in.weight" not in keys:
+        tdm = -1
+    if context_dim is None and "mid_block.attentions.0.transformer_blocks.0.attn2.to_k.weight" in keys:
+        context_dim = sd["mid_block.attentions.0.transformer_blocks.0.attn2.to_k.weight"].shape[1]
+    transformer_depth_output = []
+    for i in range(count_blocks(keys, "up_blocks.{}.")):
+        for j in range(count_blocks(keys, f"up_blocks.{i}.resnets." + "{}.")):
+            transformer_depth_output.append(count_blocks(keys, f"up_blocks.{i}.attentions.{j}.transformer_blocks." + "{}."))
+    transformer_depth_output = transformer_depth_output[::-1] if transformer_depth_output else None
+    cfg = {"use_checkpoint": False, "image_size": 32, "use_spatial_transformer": True, "legacy": False,
+           "in_channels": in_channels, "model_channels": model_channels,
+           "out_channels": sd["conv_out.weight"].shape[0] if "conv_out.weight" in keys else 4,
+           "num_res_blocks": num_res_blocks, "channel_mult": channel_mult, "transformer_depth": transformer_depth,
+           "transformer_depth_middle": tdm, "context_dim": context_dim, "use_linear_in_transformer": use_linear,
+           "use_temporal_resblock": False, "use_temporal_attention": False}
+    if transformer_depth_output is not None:
+        cfg["transformer_depth_output"] = transformer_depth_output
+    if "add_embedding.linear_1.weight" in keys:
+        cfg["num_classes"] = "sequential"
+        cfg["adm_in_channels"] = sd["add_embedding.linear_1.weight"].shape[1]
+    elif "class_embedding.linear_1.weight" in keys:
+        cfg["num_classes"] = "sequential"
+        cfg["adm_in_channels"] = sd["class_embedding.linear_1.weight"].shape[1]
+    else:
+        cfg["adm_in_channels"] = None
+    if context_dim == 768:
+        cfg.update(num_heads=8, num_head_channels=-1)
+    else:
+        cfg.update(num_heads=-1, num_head_channels=64)
+    return cfg
+
+
+def model_config_from_diffusers_unet(state_dict):
+    cfg = unet_config_from_diffusers_unet(state_dict)
+    return model_config_from_unet_config(cfg) if cfg is not None else None

@@ -1,5 +1,6 @@
 """CPU unit tests for the extra node modules (reference: comfy_extras/*)."""
 import math
+import os
 
 import pytest
 import torch
@@ -233,3 +234,56 @@ def test_merge_and_save_roundtrip(tiny, tmp_path):
     N("VAESave").save(vae, "vae/v")
     N("CLIPSave").save(clip, "clip/c")
     assert os.listdir(tmp_path / "vae") and os.listdir(tmp_path / "clip")
+
+
+def test_controlnet_roundtrip(tiny, tmp_path):
+    """Random tiny ControlNet: save -> ControlNetLoader -> ControlNetApply(Advanced) -> KSampler;
+    zero convs at zero reproduce the plain model, non-zero changes the result; strength 0 == off."""
+    import copy
+    from safetensors.torch import save_file
+    from comfy_gen_server_amd.models.cldm import ControlNet as CN
+    from comfy_gen_server_amd.models.layers import init_random_
+    from comfy_gen_server_amd.tools.synth import TINY_UNET
+    from comfy_gen_server_amd.utils import folder_paths
+    patcher, clip, vae, pos, neg = tiny
+    cfg = copy.deepcopy(TINY_UNET)
+    cfg.update(num_heads=2, num_head_channels=-1)
+    cn = CN(hint_channels=3, **cfg)
+    init_random_(cn, seed=3)
+    sd = {k: v.contiguous() for k, v in cn.state_dict().items()}
+    os.makedirs(tmp_path / "controlnet", exist_ok=True)
+    save_file(sd, str(tmp_path / "controlnet" / "cn.safetensors"))
+    zero = {k: (torch.zeros_like(v) if ("zero_convs" in k or "middle_block_out" in k) else v) for k, v in sd.items()}
+    save_file(zero, str(tmp_path / "controlnet" / "cn_zero.safetensors"))
+    folder_paths.add_model_folder_path("controlnet", str(tmp_path / "controlnet"))
+    hint = torch.rand(1, 128, 128, 3)
+    base = _sample(patcher, pos, neg)
+    net0 = N("ControlNetLoader").load_controlnet("cn_zero.safetensors")[0]
+    p0 = N("ControlNetApply").apply_controlnet(pos, net0, hint, 1.0)[0]
+    assert torch.allclose(_sample(patcher, p0, neg), base, atol=1e-5)
+    net = N("ControlNetLoader").load_controlnet("cn.safetensors")[0]
+    p1, n1 = N("ControlNetApplyAdvanced").apply_controlnet(pos, neg, net, hint, 1.0, 0.0, 1.0)
+    out = _sample(patcher, p1, n1)
+    assert torch.isfinite(out).all() and not torch.allclose(out, base, atol=1e-4)
+    ps, ns = N("ControlNetApplyAdvanced").apply_controlnet(pos, neg, net, hint, 0.0, 0.0, 1.0)
+    assert torch.allclose(_sample(patcher, ps, ns), base, atol=1e-5)
+    # chained nets + percent window that excludes every step
+    p2, n2 = N("ControlNetApplyAdvanced").apply_controlnet(p1, n1, net, hint, 0.5, 0.0, 1.0)
+    assert torch.isfinite(_sample(patcher, p2, n2)).all()
+    pw, nw = N("ControlNetApplyAdvanced").apply_controlnet(pos, neg, net, hint, 1.0, 0.99, 1.0)
+    d = (_sample(patcher, pw, nw, steps=2) - base).abs().max()   # only batching-order fp32 noise
+    assert d < 1e-4 * base.abs().max()
+
+
+def test_t2i_adapter_shapes():
+    from comfy_gen_server_amd.models.t2i_adapter import Adapter, Adapter_light, StyleAdapter
+    a = Adapter(channels=[32, 64, 128, 128], nums_rb=2, cin=192, ksize=1, sk=True, use_conv=False, xl=False)
+    f = a(torch.rand(1, 3, 128, 128))
+    assert len(f) == 12 and f[2].shape == (1, 32, 16, 16) and f[11].shape == (1, 128, 2, 2)
+    ax = Adapter(channels=[32, 64, 128, 128], nums_rb=2, cin=768, ksize=1, sk=True, use_conv=False, xl=True)
+    fx = ax(torch.rand(1, 3, 128, 128))
+    assert [i for i, t in enumerate(fx) if t is not None] == [3, 5, 8, 10]
+    al = Adapter_light(channels=[32, 64, 128, 128], nums_rb=1, cin=192)
+    assert al(torch.rand(1, 3, 64, 64))[-1].shape == (1, 128, 1, 1)
+    st = StyleAdapter(width=64, context_dim=32, num_head=4, n_layes=2, num_token=3)
+    assert st(torch.rand(2, 5, 64)).shape == (2, 3, 32)
