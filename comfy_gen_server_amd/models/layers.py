@@ -166,7 +166,7 @@ def init_random_(module: nn.Module, seed: int = 0, std_scale: float = 1.0):
         if is_norm and leaf == "weight":
             p.fill_(1.0)
             continue
-        if p.dim() == 1:
+        if p.dim() <= 1:
             t = torch.randn(p.shape, generator=g) * 0.02
         else:
             fan_in = p[0].numel()

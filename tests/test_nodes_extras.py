@@ -287,3 +287,40 @@ def test_t2i_adapter_shapes():
     assert al(torch.rand(1, 3, 64, 64))[-1].shape == (1, 128, 1, 1)
     st = StyleAdapter(width=64, context_dim=32, num_head=4, n_layes=2, num_token=3)
     assert st(torch.rand(2, 5, 64)).shape == (2, 3, 32)
+
+
+def test_taesd_and_gligen(tiny):
+    from comfy_gen_server_amd.models.taesd import TAESD
+    from comfy_gen_server_amd.models.gligen import FourierEmbedder, gligen_from_state_dict, PositionNet, \
+        GatedSelfAttentionDense
+    from comfy_gen_server_amd.models.layers import init_random_
+    t = TAESD()
+    init_random_(t, seed=0)
+    z = t.encode(torch.rand(1, 3, 64, 64) * 2 - 1)
+    assert z.shape == (1, 4, 8, 8)
+    assert t.decode(z).shape == (1, 3, 64, 64)
+    fe = FourierEmbedder(num_freqs=3)
+    x = torch.rand(2, 5, 4)
+    ref = torch.cat([torch.cat([torch.sin(f * x), torch.cos(f * x)], -1) for f in fe.freq_bands], -1)
+    assert torch.allclose(fe(x), ref, atol=1e-6)
+    # GLIGEN on the tiny UNet: one gated block per transformer block (tiny has 4+1 with context 64)
+    patcher, clip, vae, pos, neg = tiny
+    sd = {}
+    blocks = [("input_blocks", 1, 32), ("input_blocks", 3, 64), ("middle_block", 1, 64), ("output_blocks", 0, 64),
+              ("output_blocks", 1, 64), ("output_blocks", 2, 32), ("output_blocks", 3, 32)]
+    for part, b, dim in blocks:
+        g = GatedSelfAttentionDense(dim, 64, 2, dim // 2)
+        init_random_(g, seed=b)
+        for k, v in g.state_dict().items():
+            sd[f"model.diffusion_model.{part}.{b}.1.transformer_blocks.0.fuser.{k}"] = v
+    pn = PositionNet(64, 64)
+    init_random_(pn, seed=9)
+    for k, v in pn.state_dict().items():
+        sd[f"position_net.{k}"] = v
+    gl = gligen_from_state_dict(sd)
+    from comfy_gen_server_amd.runtime.patcher import ModelPatcher
+    gp = ModelPatcher(gl, load_device=torch.device("cpu"), offload_device=torch.device("cpu"))
+    cond = N("GLIGENTextBoxApply").append(pos, clip, gp, "a dog", 32, 32, 0, 0)[0]
+    assert cond[0][1]["gligen"][0] == "position"
+    out = _sample(patcher, cond, neg)
+    assert torch.isfinite(out).all()
