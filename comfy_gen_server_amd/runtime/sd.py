@@ -103,6 +103,9 @@ class VAE:
         self.process_input = lambda image: image * 2.0 - 1.0
         self.process_output = lambda image: torch.clamp((image + 1.0) / 2.0, min=0.0, max=1.0)
         self.kind = "kl"
+        if sd is not None and "decoder.up_blocks.0.resnets.0.norm1.weight" in sd:
+            from .diffusers import convert_vae_state_dict
+            sd = convert_vae_state_dict(sd)
         if config is None:
             if sd is not None and "taesd_decoder.1.weight" in sd:
                 from ..models.taesd import TAESD
