@@ -82,6 +82,7 @@ KERNEL_SIGNATURES = {
     "cgs_gemm_bf16": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
     "cgs_gemm_set_variant": [_I],   # -1 auto, 1 force 128x128 register-staged, 2 force 256-tile glds, 3 mfma32 4-stage
     "cgs_conv_set_variant": [_I],
+    "cgs_attn_set_variant": [_I],     # 0 auto (D=64 fast kernel where legal), 1 generic, 2 fast only
     "cgs_set_tile_group": [_I],       # grouped tile order for GEMM v2/v3 (tile rows per group)
     "cgs_conv_set_tile_group": [_I],   # -1 auto (v3 where legal), 2 force the 8-wave 2-stage kernel
     # out = a * gelu(g) where [a | g] = x rows of width 2*N
@@ -96,6 +97,8 @@ KERNEL_SIGNATURES = {
     "cgs_silu": [_P, _P, _L, _I, _P],
     # NHWC nearest upsample x2
     "cgs_upsample_nearest2x_nhwc": [_P, _P, _I, _I, _I, _I, _I, _P],
+    # depthwise conv NHWC: x, w[k*k, C], bias, y, N, H, W, C, k, replicate, dtype, stream
+    "cgs_dwconv_nhwc": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     # conv implicit GEMM NHWC bf16: x[N,H,W,Cin], w[Cout,kh,kw,Cin], bias, residual, out
     "cgs_conv2d_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cgs_gemm_bf16_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
@@ -105,7 +108,8 @@ KERNEL_SIGNATURES = {
 
 
 _RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_gemm_set_variant": None,
-            "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None}
+            "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
+            "cgs_attn_set_variant": None}
 
 
 def _declare(lib):

@@ -207,6 +207,207 @@ __global__ __launch_bounds__(256, (DP >= 160 ? 1 : 2)) void flash_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fast path: D = 64, no mask / causal (SDXL / SD2 / Cascade self- and cross-attention).
+//  * 8 waves x 32 query rows = 256-row Q block per workgroup (one WG per CU, 2 waves per SIMD);
+//    K/V tiles of 64 keys in a 2-slot LDS ring, ONE barrier per tile.
+//  * software pipeline inside each wave: QK^T of tile t+1 is issued in the same basic block as the
+//    softmax of tile t (independent MFMA and VALU streams interleave), then PV of tile t.
+//    K is staged two tiles ahead, V one tile ahead (register-staged: global loads issued at the
+//    top of the tile, LDS writes after the compute — T14).
+//  * K image: 128-B rows, 16-B chunk c stored at c ^ ((row>>1)&7) -> conflict-free ds_read_b128 of
+//    the 32x32x16 A operand; V image: chunk c ^ (((row>>1)&1)<<2) -> conflict-free
+//    ds_read_b64_tr_b16 of the transposed V^T operand.
+//  * softmax: fma-folded scale (exp2 domain), v_max3 chains, permlane32 max exchange, deferred
+//    rescale (only when a lane's running max grows by > 2^8 — bf16 keeps its relative precision),
+//    only the last tile masks (keys >= Sk).
+#define AF_THR 8.0f
+
+__device__ __forceinline__ float af_xmax(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+template <bool TAIL>
+__device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x16 (&ot)[2], float& m_run,
+                                           float& l_run, float c, int key0, int Sk, int hf) {
+  if (TAIL) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int key = key0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+        s[kt][r] = key < Sk ? s[kt][r] : -INFINITY;
+      }
+  }
+  float mx = fmaxf(s[0][0], s[0][1]);
+#pragma unroll
+  for (int i = 2; i < 32; i += 2) mx = fmaxf(fmaxf(mx, s[i >> 4][i & 15]), s[i >> 4][(i & 15) + 1]);
+  mx = af_xmax(mx) * c;
+  if (__any(mx > m_run + AF_THR)) {
+    float m_new = fmaxf(m_run, mx);
+    float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = m_new;
+    l_run *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ot[dt][r] *= alpha;
+  }
+  const float nm = -m_run;
+  float ps = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][r], c, nm));
+      ps += p;
+      pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p;
+    }
+  l_run += ps;
+}
+
+__global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
+    const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
+    int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
+    long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
+    float c, int nqb) {
+  __shared__ __attribute__((aligned(16))) u16 Ks[2][64 * 64];
+  __shared__ __attribute__((aligned(16))) u16 Vs[2][64 * 64];
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = logical % nqb;
+  const int bh = logical / nqb;
+  const int b = bh / H, h = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hf = lane >> 5;
+
+  const u16* qbase = qp + b * qsb + h * qsh;
+  const u16* kbase = kp + b * ksb + h * ksh;
+  const u16* vbase = vp + b * vsb + h * vsh;
+  u16* obase = op + b * osb + h * osh;
+
+  const int q_row = qb * 256 + wave * 32 + l32;
+  const bool q_ok = q_row < Sq;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    s16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q_ok) t = *reinterpret_cast<const s16x8*>(qbase + (long long)q_row * qss + ks * 16 + 8 * hf);
+    qf[ks] = __builtin_bit_cast(bf16x8, t);
+  }
+
+  // staging: thread -> (key = tid>>3, chunk = tid&7) of a 64x64 tile
+  const int st_key = tid >> 3, st_c = tid & 7;
+  const int k_woff = st_key * 64 + 8 * (st_c ^ ((st_key >> 1) & 7));
+  const int v_woff = st_key * 64 + 8 * (st_c ^ (((st_key >> 1) & 1) << 2));
+  const int n = (Sk + 63) >> 6;
+  auto gload = [&](const u16* base, long long ss, int t) -> s16x8 {
+    int key = t * 64 + st_key;
+    key = key < Sk ? key : Sk - 1;   // clamp: tail rows are masked in the softmax
+    return *reinterpret_cast<const s16x8*>(base + (long long)key * ss + st_c * 8);
+  };
+  // QK^T A-operand read offsets (elements) for kt = 0/1, ks = 0..3
+  auto k_roff = [&](int kt, int ks) {
+    int key = kt * 32 + l32;
+    return key * 64 + 8 * ((2 * ks + hf) ^ ((key >> 1) & 7));
+  };
+  auto qk = [&](const u16* Kt, f32x16 (&s)[2]) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s16x8 a = *reinterpret_cast<const s16x8*>(Kt + k_roff(kt, ks));
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], s[kt], 0, 0, 0);
+      }
+    }
+  };
+  const int i16 = lane & 15;
+  auto pv = [&](const u16* Vt, const bf16x8 (&pf)[4], f32x16 (&ot)[2]) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int row0 = kt * 32 + 16 * st + 4 * hf + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+          const int ch = col >> 3, half = (col >> 2) & 1;
+          const int r1 = row0 + 8;
+          const int o0 = row0 * 64 + 8 * (ch ^ (((row0 >> 1) & 1) << 2)) + 4 * half;
+          const int o1 = r1 * 64 + 8 * (ch ^ (((r1 >> 1) & 1) << 2)) + 4 * half;
+          bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vt + o0));
+          bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vt + o1));
+          bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          ot[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt * 2 + st], ot[dt], 0, 0, 0);
+        }
+      }
+  };
+
+  f32x16 ot[2] = {f32x16{}, f32x16{}};
+  float m_run = -INFINITY, l_run = 0.f;
+  bf16x8 pf[4];
+  f32x16 sA[2], sB[2];
+
+  // prologue: K(0) -> slot 0, K(1) -> slot 1, V(0) -> slot 0; S(0)
+  {
+    s16x8 k0 = gload(kbase, kss, 0);
+    s16x8 k1 = gload(kbase, kss, n > 1 ? 1 : 0);
+    s16x8 v0 = gload(vbase, vss, 0);
+    *reinterpret_cast<s16x8*>(&Ks[0][k_woff]) = k0;
+    *reinterpret_cast<s16x8*>(&Ks[1][k_woff]) = k1;
+    *reinterpret_cast<s16x8*>(&Vs[0][v_woff]) = v0;
+  }
+  __syncthreads();
+  qk(Ks[0], sA);
+
+  // steady state: iteration t consumes S(t) (in sCur), produces S(t+1) (in sNext)
+  auto body = [&](int t, f32x16 (&sCur)[2], f32x16 (&sNext)[2]) {
+    const int slot = t & 1;
+    s16x8 kn = gload(kbase, kss, min(t + 2, n - 1));
+    s16x8 vn = gload(vbase, vss, t + 1);
+    qk(Ks[slot ^ 1], sNext);
+    af_softmax<false>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
+    pv(Vs[slot], pf, ot);
+    *reinterpret_cast<s16x8*>(&Ks[slot][k_woff]) = kn;
+    *reinterpret_cast<s16x8*>(&Vs[slot ^ 1][v_woff]) = vn;
+    __syncthreads();
+  };
+  int t = 0;
+  for (; t + 2 < n; t += 2) {
+    body(t, sA, sB);
+    body(t + 1, sB, sA);
+  }
+  if (t + 1 < n) {   // one full iteration left before the last tile
+    body(t, sA, sB);
+    ++t;
+    af_softmax<true>(sB, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
+  } else {
+    af_softmax<true>(sA, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
+  }
+  pv(Vs[t & 1], pf, ot);
+
+  // epilogue: O[q][d] = O^T[d][q] / l
+  float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (q_ok) {
+    u16* orow = obase + (long long)q_row * oss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        s16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(ot[dt][4 * r4 + j] * inv);
+        *reinterpret_cast<s16x4*>(orow + dt * 32 + 8 * r4 + 4 * hf) = w;
+      }
+  }
+}
+
+static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel
+CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
+
 CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
                                   int D, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
                                   long long ksh, long long vsb, long long vss, long long vsh, long long osb,
@@ -217,6 +418,19 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
   long long nwg = (long long)nqb * B * H;
   if (nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
   float sl2 = scale * 1.4426950408889634f;
+  const bool al16 = ((qss | kss | vss | oss | qsb | ksb | vsb | osb | qsh | ksh | vsh | osh) & 7) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+                      reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) & 15) == 0;
+  if (D == 64 && !key_mask && !causal && al16 && g_attn_variant != 1 && Sk > 0) {
+    int nqb2 = (Sq + 255) / 256;
+    long long nwg2 = (long long)nqb2 * B * H;
+    if (nwg2 > 0x7fffffff) return (int)hipErrorInvalidValue;
+    attn_fwd_d64_kernel<<<dim3((unsigned)nwg2), 512, 0, stream>>>(
+        (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
+        osb, oss, osh, sl2, nqb2);
+    return (int)hipGetLastError();
+  }
+  if (g_attn_variant == 2) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)nwg);
 #define ATT_LAUNCH(DPV)                                                                                         \
   flash_fwd_kernel<DPV><<<grid, 256, 0, stream>>>((const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, B, H, Sq, \

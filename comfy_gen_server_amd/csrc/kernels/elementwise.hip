@@ -134,3 +134,63 @@ CGS_EXPORT int cgs_geglu(const void* x, void* out, int M, int N, int dtype, hipS
   geglu_kernel<<<ew_blocks((long long)M * N / 8), 256, 0, stream>>>((const u16*)x, (u16*)out, M, N);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- depthwise conv, NHWC, stride 1 (K11)
+// y[n,h,w,c] = b[c] + sum_{i,j<k} x[n, h+i-p, w+j-p, c] * wt[(i*k+j)*C + c]; p = k/2.
+// Out-of-range taps are zero ("zeros" padding) or clamped to the border (replicate=1, Stage A).
+// One thread per 8 channels of one output pixel; neighbouring pixels of a wave share the same rows,
+// so the k*k tap re-reads hit L1/L2 — the kernel streams x and y once from HBM.
+template <int DT>
+__global__ __launch_bounds__(256) void dwconv_nhwc_kernel(const s16x8* __restrict__ x, const u16* __restrict__ wt,
+                                                          const u16* __restrict__ b, s16x8* __restrict__ y, int N,
+                                                          int H, int W, int C8, int k, int replicate) {
+  const long long total = (long long)N * H * W * C8;
+  const int p = k >> 1;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    long long pix = i / C8;
+    const int wo = (int)(pix % W);
+    const int ho = (int)((pix / W) % H);
+    const int n = (int)(pix / ((long long)W * H));
+    float acc[8];
+    if (b) {
+      s16x8 bv = reinterpret_cast<const s16x8*>(b)[c8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = cvt_in<DT>((u16)bv[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    }
+    for (int di = 0; di < k; ++di) {
+      int hi = ho + di - p;
+      if (replicate) hi = min(max(hi, 0), H - 1);
+      else if (hi < 0 || hi >= H) continue;
+      for (int dj = 0; dj < k; ++dj) {
+        int wi = wo + dj - p;
+        if (replicate) wi = min(max(wi, 0), W - 1);
+        else if (wi < 0 || wi >= W) continue;
+        s16x8 xv = x[(((long long)n * H + hi) * W + wi) * C8 + c8];
+        s16x8 wv = reinterpret_cast<const s16x8*>(wt + (size_t)(di * k + dj) * C8 * 8)[c8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += cvt_in<DT>((u16)xv[j]) * cvt_in<DT>((u16)wv[j]);
+      }
+    }
+    s16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (short)cvt_out<DT>(acc[j]);
+    y[i] = o;
+  }
+}
+
+CGS_EXPORT int cgs_dwconv_nhwc(const void* x, const void* wt, const void* b, void* y, int N, int H, int W, int C,
+                               int k, int replicate, int dtype, hipStream_t stream) {
+  if (C % 8 || (k & 1) == 0) return (int)hipErrorInvalidValue;
+  long long total = (long long)N * H * W * (C / 8);
+  if (dtype == CGS_BF16)
+    dwconv_nhwc_kernel<CGS_BF16><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b,
+                                                                      (s16x8*)y, N, H, W, C / 8, k, replicate);
+  else
+    dwconv_nhwc_kernel<CGS_F16><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b,
+                                                                     (s16x8*)y, N, H, W, C / 8, k, replicate);
+  return (int)hipGetLastError();
+}

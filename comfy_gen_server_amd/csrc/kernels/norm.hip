@@ -260,13 +260,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ 
   for (int k = 0; k < LN_MAXK; ++k) {
     int ch = lane + 64 * k;
     if (ch < nch) {
-      s16x8 wv = reinterpret_cast<const s16x8*>(w)[ch];
-      s16x8 bv;
+      s16x8 wv, bv;
+      if (w) wv = reinterpret_cast<const s16x8*>(w)[ch];
       if (b) bv = reinterpret_cast<const s16x8*>(b)[ch];
       s16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float f = (v[k][j] - mean) * rstd * cvt_in<DT>((u16)wv[j]) + (b ? cvt_in<DT>((u16)bv[j]) : 0.f);
+        float f = (v[k][j] - mean) * rstd * (w ? cvt_in<DT>((u16)wv[j]) : 1.f) + (b ? cvt_in<DT>((u16)bv[j]) : 0.f);
         o[j] = (short)cvt_out<DT>(f);
       }
       reinterpret_cast<s16x8*>(yr)[ch] = o;
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void layernorm_big_kernel(const u16* __restric
   float rstd = rsqrtf(wave_sum(q) / C + eps);
   u16* yr = y + (size_t)row * C;
   for (int i = lane; i < C; i += 64)
-    yr[i] = cvt_out<DT>((cvt_in<DT>(xr[i]) - mean) * rstd * cvt_in<DT>(w[i]) + (b ? cvt_in<DT>(b[i]) : 0.f));
+    yr[i] = cvt_out<DT>((cvt_in<DT>(xr[i]) - mean) * rstd * (w ? cvt_in<DT>(w[i]) : 1.f) + (b ? cvt_in<DT>(b[i]) : 0.f));
 }
 
 CGS_EXPORT int cgs_layernorm(const void* x, void* y, const void* w, const void* b, int rows, int C, float eps,

@@ -16,5 +16,5 @@ from .dispatch import (  # noqa: F401
 )
 from .core import (  # noqa: F401
     linear, linear_geglu, attention, group_norm, layer_norm, conv2d, silu, gelu,
-    upsample_nearest2x, timestep_embedding, cfg_combine, euler_step,
+    upsample_nearest2x, timestep_embedding, cfg_combine, euler_step, depthwise_conv2d_nhwc,
 )

@@ -316,12 +316,12 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor 
                eps: float = 1e-5) -> torch.Tensor:
     be = backend_for("layernorm", x, "cgs_layernorm")
     C = x.shape[-1]
-    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and weight is not None and C % 8 == 0:
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0:
         count("layernorm", "hip")
         xc = x.contiguous()
         y = torch.empty_like(xc)
         rows = xc.numel() // C
-        _check(_lib().cgs_layernorm(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
+        _check(_lib().cgs_layernorm(xc.data_ptr(), y.data_ptr(), _ptr(weight), _ptr(bias),
                                     rows, C, float(eps), _DT[x.dtype], _stream()), "cgs_layernorm")
         return y
     count("layernorm", "torch" if x.device.type == "cpu" else "lib")
@@ -407,6 +407,30 @@ def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
         return y
     count("upsample", "torch" if x.device.type == "cpu" else "lib")
     return F.interpolate(x, scale_factor=2.0, mode="nearest")
+
+
+def depthwise_conv2d_nhwc(x: torch.Tensor, w_kkc: torch.Tensor, bias: torch.Tensor | None, k: int,
+                          replicate: bool = False) -> torch.Tensor:
+    """Depthwise kxk conv, stride 1, 'same' padding (zeros, or border replicate) on an NHWC tensor
+    [N, H, W, C] (K11: Stable Cascade ResBlocks). ``w_kkc`` = weight [C,1,k,k] laid out [k*k, C]."""
+    N, H, W, C = x.shape
+    be = backend_for("dwconv", x, "cgs_dwconv_nhwc")
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0 and k % 2 == 1:
+        count("dwconv", "hip")
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        _check(_lib().cgs_dwconv_nhwc(xc.data_ptr(), w_kkc.contiguous().data_ptr(), _ptr(bias), y.data_ptr(),
+                                      N, H, W, C, k, int(replicate), _DT[x.dtype], _stream()), "cgs_dwconv")
+        return y
+    count("dwconv", "torch" if x.device.type == "cpu" else "lib")
+    xn = x.permute(0, 3, 1, 2)
+    wt = w_kkc.t().reshape(C, 1, k, k).to(x.dtype)
+    if replicate:
+        xn = F.pad(xn.float(), (k // 2,) * 4, mode="replicate").to(x.dtype)
+        y = F.conv2d(xn, wt, bias, 1, 0, 1, C)
+    else:
+        y = F.conv2d(xn, wt, bias, 1, k // 2, 1, C)
+    return y.permute(0, 2, 3, 1).contiguous()
 
 
 # ----------------------------------------------------------------------------------------------

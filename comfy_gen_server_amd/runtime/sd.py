@@ -125,11 +125,13 @@ class VAE:
                 self.downscale_ratio = 32
                 self.latent_channels = 16
                 self.kind = "effnet"
+                sd = {"encoder." + k: v for k, v in sd.items()}
             elif sd is not None and "blocks.11.num_batches_tracked" in sd:
                 from ..models.cascade import StageC_coder
                 self.first_stage_model = StageC_coder()
                 self.latent_channels = 16
                 self.kind = "previewer"
+                sd = {"previewer." + k: v for k, v in sd.items()}
             else:
                 ddconfig = dict(double_z=True, z_channels=4, resolution=256, in_channels=3, out_ch=3, ch=128,
                                 ch_mult=[1, 2, 4, 4], num_res_blocks=2, attn_resolutions=[], dropout=0.0)

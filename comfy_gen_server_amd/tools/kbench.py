@@ -32,7 +32,7 @@ def _time(fn, iters=20, warm=3):
     return ts[len(ts) // 2]
 
 
-def main(quick=False):
+def main(quick=False, attn_only=False):
     from comfy_gen_server_amd import ops
     from comfy_gen_server_amd.ops import core
     from comfy_gen_server_amd.ops.dispatch import set_backend_override
@@ -44,6 +44,8 @@ def main(quick=False):
                    (B * 4096, 640, 640), (B * 4096, 5120, 640), (B * 4096, 640, 2560), (B * 77, 1280, 2048)]
     if quick:
         gemm_shapes = gemm_shapes[:3]
+    if attn_only:
+        gemm_shapes = []
     for M, N, K in gemm_shapes:
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(torch.bfloat16)
@@ -70,11 +72,27 @@ def main(quick=False):
         k = torch.randn(b, sk, h * d, device=dev).to(torch.bfloat16)
         v = torch.randn(b, sk, h * d, device=dev).to(torch.bfloat16)
         fl = 4.0 * b * h * sq * sk * d
-        t_hip = _time(lambda: ops.attention(q, k, v, h))
+        lib = ops.dispatch._native.load_kernels()
+        ent = dict(B=b, H=h, Sq=sq, Sk=sk, D=d)
+        for var, name in ((1, "generic"), (2, "d64")):
+            lib.cgs_attn_set_variant(var)
+            t_hip = _time(lambda: ops.attention(q, k, v, h))
+            ent[f"{name}_ms"] = t_hip
+            ent[f"{name}_tflops"] = fl / t_hip / 1e9
+        lib.cgs_attn_set_variant(0)
         qh, kh, vh = (t.view(b, -1, h, d).transpose(1, 2) for t in (q, k, v))
         t_sdpa = _time(lambda: F.scaled_dot_product_attention(qh, kh, vh))
-        res["attention"].append(dict(B=b, H=h, Sq=sq, Sk=sk, D=d, hip_ms=t_hip, sdpa_ms=t_sdpa,
-                                     hip_tflops=fl / t_hip / 1e9, sdpa_tflops=fl / t_sdpa / 1e9))
+        ent.update(sdpa_ms=t_sdpa, sdpa_tflops=fl / t_sdpa / 1e9)
+        if sq == sk:   # q/k/v as views of one fused QKV projection (the UNet's layout)
+            qkv = torch.randn(b, sq, 3 * h * d, device=dev).to(torch.bfloat16)
+            qv, kv_, vv = qkv.split(h * d, dim=-1)
+            t_f = _time(lambda: ops.attention(qv, kv_, vv, h))
+            ent.update(fused_qkv_ms=t_f, fused_qkv_tflops=fl / t_f / 1e9)
+        res["attention"].append(ent)
+        if attn_only:
+            print(json.dumps(ent), flush=True)
+    if attn_only:
+        return res
     for N, C, H, W in [(B, 320, 128, 128), (B, 640, 64, 64), (B, 1280, 32, 32)]:
         x = torch.randn(N, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         wt = torch.randn(C, device=dev).to(torch.bfloat16)
@@ -120,4 +138,4 @@ def main(quick=False):
 
 
 if __name__ == "__main__":
-    main(quick="--quick" in sys.argv)
+    main(quick="--quick" in sys.argv, attn_only="--attn" in sys.argv)

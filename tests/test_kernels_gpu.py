@@ -93,6 +93,61 @@ def test_flash_attention_causal_and_spike(cuda):
     assert _rel(o, ref) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,k,rep", [(2, 24, 24, 64, 3, False), (1, 17, 9, 2048, 3, False),
+                                            (1, 32, 31, 192, 3, True), (2, 8, 8, 16, 5, False)])
+def test_depthwise_conv_nhwc(cuda, N, H, W, C, k, rep):
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16)
+    w = torch.randn(C, 1, k, k, device=cuda).to(torch.bfloat16)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16)
+    y = ops.depthwise_conv2d_nhwc(x, w.reshape(C, k * k).t().contiguous(), b, k, replicate=rep)
+    xn = x.float().permute(0, 3, 1, 2)
+    if rep:
+        ref = F.conv2d(F.pad(xn, (k // 2,) * 4, mode="replicate"), w.float(), b.float(), groups=C)
+    else:
+        ref = F.conv2d(xn, w.float(), b.float(), padding=k // 2, groups=C)
+    assert ops.stats().get(("dwconv", "hip"), 0) == 1
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_layernorm_no_affine(cuda):
+    x = torch.randn(300, 2048, device=cuda).to(torch.bfloat16)
+    y = ops.layer_norm(x, None, None, 1e-6)
+    assert ops.stats().get(("layernorm", "hip"), 0) == 1
+    assert _rel(y, F.layer_norm(x.float(), (2048,), eps=1e-6)) < 1e-2
+
+
+@pytest.fixture(params=[1, 2], ids=["generic", "d64fast"])
+def attn_variant(request):
+    lib = _native.load_kernels()
+    lib.cgs_attn_set_variant(request.param)
+    yield request.param
+    lib.cgs_attn_set_variant(0)
+
+
+@pytest.mark.parametrize("B,H,Sq,Sk", [(2, 10, 256, 256), (1, 3, 300, 77), (2, 2, 1000, 1000), (1, 2, 4096, 4096),
+                                       (1, 1, 64, 1), (2, 3, 513, 130)])
+@pytest.mark.parametrize("spike", [False, True])
+def test_attention_d64_variants(cuda, attn_variant, B, H, Sq, Sk, spike):
+    """D=64 fast kernel vs the generic kernel vs fp32 reference: tails in Sq (256-row blocks) and Sk
+    (64-key tiles), and spiked late keys that force running-max rescales mid-sequence."""
+    torch.manual_seed(3)
+    D = 64
+    q = torch.randn(B, Sq, H * D, device=cuda)
+    k = torch.randn(B, Sk, H * D, device=cuda)
+    v = torch.randn(B, Sk, H * D, device=cuda)
+    if spike:
+        q *= 3.0
+        for j in range(Sk // 3, Sk, max(1, Sk // 5)):
+            k[:, j, :] *= 1.0 + 0.5 * (j * 7 % 11)
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    o = ops.attention(q, k, v, H)
+    ref = core.attention_reference(q.float(), k.float(), v.float(), H)
+    assert ops.stats().get(("attention", "hip"), 0) == 1
+    assert torch.isfinite(o).all()
+    assert _rel(o, ref) < 2e-2
+
+
 @pytest.fixture(params=[1, 2, 3, 4, 5], ids=["v1", "v2", "v3w4", "v3w8", "v5pp"])
 def gemm_variant(request):
     lib = _native.load_kernels()
