@@ -17,6 +17,7 @@
 #include "common.h"
 #include "mfma_core.h"
 #include "mfma_pp.h"
+#include "mfma_pp160.h"
 
 #define EPI_BIAS 1
 #define EPI_RESIDUAL 2
@@ -306,6 +307,31 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   conv_nhwc_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
 }
 
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
+  ConvGatherA8 al;
+  al.a = &a;
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  pq::tile(al, a.w, K, M, a.Cout, K, tm * pq::BM, tn * pq::BN, e, smem);
+}
+
+static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = (a.Cout + pq::BN - 1) / pq::BN;
+  const long long nwg = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
+  conv_nhwc_v6_kernel<<<(unsigned)nwg, pq::THREADS, pq::LDS, stream>>>(a);
+}
+
 static int g_conv_group = 8;
 CGS_EXPORT void cgs_conv_set_tile_group(int g) { g_conv_group = g < 1 ? 1 : g; }
 static int g_conv_variant = -1;   // -1 auto (v3/8 waves where legal), 2 = v2 only, 3 = v3/4 waves, 4 = v3/8 waves
@@ -315,6 +341,10 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
   a.group_m = g_conv_group;
   if (variant == 5 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0)) {
     conv_v5_go(a, stream);
+    return (int)hipGetLastError();
+  }
+  if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0)) {
+    conv_v6_go(a, stream);
     return (int)hipGetLastError();
   }
   const int M = a.N * a.Ho * a.Wo;

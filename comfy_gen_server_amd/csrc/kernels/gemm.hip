@@ -13,6 +13,7 @@
 #include "common.h"
 #include "mfma_core.h"
 #include "mfma_pp.h"
+#include "mfma_pp160.h"
 
 #define G_BM 128
 #define G_BN 128
@@ -435,6 +436,38 @@ static int gemm_v5_launch(const void* A, const void* W, void* C, const void* bia
   return (int)hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
+  DenseA8 al{A, lda, M, {}};
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
+  pq::tile(al, W, ldw, M, N, K, tm * pq::BM, tn * pq::BN, e, smem);
+}
+
+static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pq::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + pq::BN - 1) / pq::BN;
+  const long long nwg = (long long)((M + pq::BM - 1) / pq::BM) * tiles_n;
+  gemm_bf16_nt_v6_kernel<<<(unsigned)nwg, pq::THREADS, pq::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+      tiles_n, g_tile_group);
+  return (int)hipGetLastError();
+}
+
 static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 waves), 4 = v3 (8 waves), 5 = v5 ping-pong
 
 CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -453,6 +486,8 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   bool v3_ok = (K % 32 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && (nout % 8 == 0) && (ldc % 8 == 0) &&
                (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
                ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
+  if (v3_ok && K % 64 == 0 && variant == 6 && !(epi & EPI_GEGLU))
+    return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && variant == 5)
     return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && (variant >= 3 || variant == -1)) {
@@ -486,5 +521,6 @@ CGS_EXPORT int cgs_gemm_bf16(const void* A, const void* W, void* C, const void* 
 CGS_EXPORT int cgs_gemm_bf16_v(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                                int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                                int variant, hipStream_t stream) {
+  if (variant == -2) variant = g_gemm_variant;   // -2: the process-wide override (default auto)
   return gemm_dispatch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, variant, stream);
 }

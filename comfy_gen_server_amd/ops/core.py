@@ -90,6 +90,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             cands = []
             if K % 64 == 0 and N % 8 == 0:
                 cands.append(("v5", lambda: run_hip(5)))
+                cands.append(("v6", lambda: run_hip(6)))
             if K % 32 == 0 and N % 8 == 0:
                 cands.append(("v4", lambda: run_hip(4)))
             cands.append(("hip", lambda: run_hip(-1)))
@@ -99,7 +100,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v5": 5, "v4": 4}.get(choice, -1)
+        variant = {"v5": 5, "v4": 4}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N)
     count("gemm", "torch" if be == "torch" else "lib")
     if be == "torch":
@@ -145,7 +146,7 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
             cands.append(("v4", lambda: run_hip(4)))
             cands.append(("hip", lambda: run_hip(-1)))
             choice = autotune.choose(("gemm_geglu", M, N2, K, epi), cands, default="hip")
-        variant = {"v5": 5, "v4": 4}.get(choice, -1)
+        variant = {"v5": 5, "v4": 4}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N2 // 2)
     count("gemm_geglu", be)
     # reference path expects the *interleaved* weight too, undo it
@@ -368,15 +369,15 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
                                             flags, variant, _stream()), "cgs_conv2d_nhwc")
             return out
 
-        variant = -1
+        variant = -2            # process-wide override (cgs_conv_set_variant), default auto
         M = N * Ho * Wo
         if M * Cout * Cin * kh * kw >= (1 << 27):
             cands = [("v4", lambda: run(4))]
             if Cin % 64 == 0:
-                cands += [("v5", lambda: run(5)), ("v2", lambda: run(2))]
+                cands += [("v5", lambda: run(5)), ("v6", lambda: run(6)), ("v2", lambda: run(2))]
             choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None)),
-                                     cands, default="v4")
-            variant = {"v2": 2, "v4": 4, "v5": 5}[choice]
+                                     cands, default="auto")
+            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "auto": -2}[choice]
         return run(variant)
     if upsample2x:
         x = upsample_nearest2x(x)

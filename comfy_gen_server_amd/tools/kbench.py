@@ -32,7 +32,7 @@ def _time(fn, iters=20, warm=3):
     return ts[len(ts) // 2]
 
 
-def main(quick=False, attn_only=False):
+def main(quick=False, attn_only=False, gemm_only=False):
     from comfy_gen_server_amd import ops
     from comfy_gen_server_amd.ops import core
     from comfy_gen_server_amd.ops.dispatch import set_backend_override
@@ -46,6 +46,8 @@ def main(quick=False, attn_only=False):
         gemm_shapes = gemm_shapes[:3]
     if attn_only:
         gemm_shapes = []
+    if gemm_only:
+        gemm_shapes = [(4096, 4096, 4096), (8192, 8192, 8192)] + gemm_shapes[:-1]
     for M, N, K in gemm_shapes:
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(torch.bfloat16)
@@ -53,7 +55,7 @@ def main(quick=False, attn_only=False):
         fl = 2.0 * M * N * K
         lib = ops.dispatch._native.load_kernels()
         ent = dict(M=M, N=N, K=K)
-        for var in (1, 2, 3, 4, 5):
+        for var in (3, 4, 5, 6):
             lib.cgs_gemm_set_variant(var)
             for g in ((1, 8) if var >= 3 else (8,)):
                 lib.cgs_set_tile_group(g)
@@ -64,6 +66,10 @@ def main(quick=False, attn_only=False):
         t_lib = _time(lambda: F.linear(a, w, bias))
         ent["lib_tflops"] = fl / t_lib / 1e9
         res["gemm"].append(ent)
+        if gemm_only:
+            print(json.dumps({k: (round(v) if isinstance(v, float) else v) for k, v in ent.items()}), flush=True)
+    if gemm_only:
+        return res
     att_shapes = [(B, 20, 1024, 1024, 64), (B, 10, 4096, 4096, 64), (B, 20, 1024, 77, 64), (B, 10, 4096, 77, 64)]
     if quick:
         att_shapes = att_shapes[:2]
@@ -123,7 +129,7 @@ def main(quick=False, attn_only=False):
             wn = wt.permute(0, 2, 3, 1).contiguous()
             set_backend_override("conv", "hip")
             lib = ops.dispatch._native.load_kernels()
-            for var in (2, 3, 4, 5):
+            for var in (2, 4, 5, 6):
                 lib.cgs_conv_set_variant(var)
                 for g in (8,):
                     lib.cgs_conv_set_tile_group(g)
@@ -138,4 +144,4 @@ def main(quick=False, attn_only=False):
 
 
 if __name__ == "__main__":
-    main(quick="--quick" in sys.argv, attn_only="--attn" in sys.argv)
+    main(quick="--quick" in sys.argv, attn_only="--attn" in sys.argv, gemm_only="--gemm" in sys.argv)

@@ -148,7 +148,7 @@ def test_attention_d64_variants(cuda, attn_variant, B, H, Sq, Sk, spike):
     assert _rel(o, ref) < 2e-2
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5], ids=["v1", "v2", "v3w4", "v3w8", "v5pp"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160"])
 def gemm_variant(request):
     lib = _native.load_kernels()
     lib.cgs_gemm_set_variant(request.param)
@@ -215,7 +215,7 @@ def test_elementwise(cuda):
     assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
 
 
-@pytest.fixture(params=[2, 3, 4, 5], ids=["cv2", "cv3w4", "cv3w8", "cv5pp"])
+@pytest.fixture(params=[2, 3, 4, 5, 6], ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160"])
 def conv_variant(request):
     lib = _native.load_kernels()
     lib.cgs_conv_set_variant(request.param)
@@ -230,8 +230,8 @@ def conv_variant(request):
                                                   (2, 96, 20, 20, 160, 3, 1, 1), (1, 320, 33, 17, 640, 3, 2, 1)])
 @pytest.mark.parametrize("epi", ["bias", "bias_res", "none"])
 def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi, conv_variant):
-    if conv_variant in (2, 5) and Cin % 64:
-        pytest.skip("v2/v5 need Cin % 64")
+    if conv_variant in (2, 5, 6) and Cin % 64:
+        pytest.skip("v2/v5/v6 need Cin % 64")
     torch.manual_seed(0)
     x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Cout, Cin, k, k, device=cuda) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
