@@ -59,6 +59,17 @@ __device__ __forceinline__ u16 cvt_out(float f) {
   else return f2h(f);
 }
 
+// 4 floats -> 4 bf16 (hardware v_cvt_pk_bf16_f32: round-to-nearest-even, NaN kept) as one 8-B word
+__device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) {
+  bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ float4 unpack4_bf16(uint2 w) {
+  return float4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                __uint_as_float(w.y & 0xffff0000u)};
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 
 __device__ __forceinline__ float gelu_f(float x) {  // exact erf GELU (torch default)

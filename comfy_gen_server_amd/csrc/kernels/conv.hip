@@ -311,13 +311,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  int tm, tn;
-  grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
   ConvGatherA8 al;
   al.a = &a;
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
-  pq::tile(al, a.w, K, M, a.Cout, K, tm * pq::BM, tn * pq::BN, e, smem);
+  pq::run(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n, a.group_m);
+}
+
+static int conv_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
 }
 
 static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
@@ -328,8 +335,9 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   }
   const int M = a.N * a.Ho * a.Wo;
   a.tiles_n = (a.Cout + pq::BN - 1) / pq::BN;
-  const long long nwg = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
-  conv_nhwc_v6_kernel<<<(unsigned)nwg, pq::THREADS, pq::LDS, stream>>>(a);
+  const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
+  const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
+  conv_nhwc_v6_kernel<<<grid, pq::THREADS, pq::LDS, stream>>>(a);
 }
 
 static int g_conv_group = 8;
@@ -343,7 +351,8 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
     conv_v5_go(a, stream);
     return (int)hipGetLastError();
   }
-  if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0)) {
+  if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
+      ((uintptr_t)a.bias % 8) == 0) {
     conv_v6_go(a, stream);
     return (int)hipGetLastError();
   }

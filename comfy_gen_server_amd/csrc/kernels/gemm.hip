@@ -441,14 +441,21 @@ static int gemm_v5_launch(const void* A, const void* W, void* C, const void* bia
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_n, int group_m) {
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  int tm, tn;
-  grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
   DenseA8 al{A, lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
-  pq::tile(al, W, ldw, M, N, K, tm * pq::BM, tn * pq::BN, e, smem);
+  pq::run(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
 }
 
 static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
@@ -461,10 +468,12 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
     attr_set = true;
   }
   const int tiles_n = (N + pq::BN - 1) / pq::BN;
-  const long long nwg = (long long)((M + pq::BM - 1) / pq::BM) * tiles_n;
-  gemm_bf16_nt_v6_kernel<<<(unsigned)nwg, pq::THREADS, pq::LDS, stream>>>(
+  const int tiles_m = (M + pq::BM - 1) / pq::BM;
+  const long long T = (long long)tiles_m * tiles_n;
+  const int grid = (int)(T < num_cus() ? T : num_cus());
+  gemm_bf16_nt_v6_kernel<<<grid, pq::THREADS, pq::LDS, stream>>>(
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
-      tiles_n, g_tile_group);
+      tiles_m, tiles_n, g_tile_group);
   return (int)hipGetLastError();
 }
 
@@ -486,7 +495,7 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   bool v3_ok = (K % 32 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && (nout % 8 == 0) && (ldc % 8 == 0) &&
                (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
                ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
-  if (v3_ok && K % 64 == 0 && variant == 6 && !(epi & EPI_GEGLU))
+  if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && !(epi & EPI_GEGLU) && ((uintptr_t)bias % 8 == 0))
     return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && variant == 5)
     return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);

@@ -32,35 +32,53 @@ constexpr int A_BYTES = BM * 128;
 constexpr int B_BYTES = BN * 128;
 constexpr int STAGE = A_BYTES + B_BYTES;
 constexpr int LDS = 3 * STAGE;     // 156 KiB
-constexpr int EPI_PITCH = 176;     // bytes per staged output row (80 bf16 + pad, 16-B aligned)
 
 // AL: loader with setup(slot, global_row) for slots 0..3 (tile rows slot*64 + (tid >> 3)) and
 // src(slot, k0) -> this lane's 16-B source for K offset k0 (swizzled chunk already applied).
+//
+// Persistent: the grid is one workgroup per CU; workgroup b walks logical tiles b, b + G, ...
+// (G = gridDim.x; XCD-mates take consecutive logical tiles, grouped_tile() orders them). The
+// K-tile stream runs ACROSS tiles: the DMAs of the next tile's first two K-tiles are issued during
+// the current tile's last two, and the epilogue (direct 8-B stores from registers, no LDS) runs
+// while they are in flight -- no per-tile prologue bubble, no LDS-staged epilogue. Needs K >= 128.
 template <class AL>
-__device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K, int m0,
-                                     int n0, const mc::Epi& e, unsigned char* smem) {
+__device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
+                                    const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2;
   const int wm = wave & 3;
   const int nk = K / BK;
+  const int T = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int base_l = xcd_remap(blockIdx.x, G);
+  if (base_l >= T) return;
+
+  auto coords = [&](int l, int& m0, int& n0) {
+    int tm, tn;
+    grouped_tile(l, tiles_m, tiles_n, group_m, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
 
   const int lrow = tid >> 3;
   const int lch = tid & 7;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) al.setup(g, m0 + g * 64 + lrow);
   const u16* bsrc[3];
+  auto setup = [&](int m0, int n0) {
 #pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    const int r = g * 64 + lrow;
-    int n = n0 + (r < BN ? r : BN - 1);
-    n = n < N ? n : N - 1;
-    bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
-  }
-  auto stage = [&](int kt) {
-    const int k0 = (kt < nk ? kt : nk - 1) * BK;   // past the end: reload the last tile into a dead slot
-    unsigned char* base = smem + (kt % 3) * STAGE + wave * 1024;
+    for (int g = 0; g < 4; ++g) al.setup(g, m0 + g * 64 + lrow);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const int r = g * 64 + lrow;
+      int n = n0 + (r < BN ? r : BN - 1);
+      n = n < N ? n : N - 1;
+      bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
+    }
+  };
+  auto stage = [&](int kt, int slot) {
+    const int k0 = kt * BK;
+    unsigned char* base = smem + slot * STAGE + wave * 1024;
 #pragma unroll
     for (int g = 0; g < 4; ++g) mc::lds_dma16(al.src(g, k0), base + g * 8192);
     unsigned char* bb = base + A_BYTES;
@@ -74,11 +92,6 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   };
 
   f32x4 acc[4][5];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const int fr = lane & 15, fq = lane >> 4;
   bf16x8 af[4], bfr[5];
   auto read_frags = [&](const unsigned char* S, int kk) {
@@ -96,72 +109,122 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
       bfr[j] = *reinterpret_cast<const bf16x8*>(SB + r * 128 + 16 * c);
     }
   };
-  auto mma = [&]() {
+  auto mma = [&]() {   // C^T tiles: lane (fr, fq) accumulates C[16i + fr][16j + 4fq + 0..3]
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  // epilogue variants are separate straight-line paths (flags are wave-uniform), so the store-only
+  // path carries no load and hence no vmcnt wait on the next tile's in-flight DMAs
+  auto epilogue_t = [&](int m0, int n0, auto has_bias_c, auto has_res_c) {
+    constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
+    const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
+    float4 bv[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      int col = n_w + 16 * j + 4 * fq;
+      col = col < N ? col : N - 4;
+      bv[j] = HB ? unpack4_bf16(*reinterpret_cast<const uint2*>(e.bias + col)) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    uint2 rw[4][5];   // residual words, all loads issued before the first store (one wait)
+    if (HR) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int row = m_w + 16 * i + fr, col = n_w + 16 * j + 4 * fq;
+          row = row < M ? row : M - 1;
+          col = col < N ? col : N - 4;
+          rw[i][j] = *reinterpret_cast<const uint2*>(e.R + (long long)row * e.ldr + col);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int col = n_w + 16 * j + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m_w + 16 * i + fr;
+        float v0 = acc[i][j][0] * e.alpha + bv[j].x, v1 = acc[i][j][1] * e.alpha + bv[j].y;
+        float v2 = acc[i][j][2] * e.alpha + bv[j].z, v3 = acc[i][j][3] * e.alpha + bv[j].w;
+        if (HR) {
+          const float4 rv = unpack4_bf16(rw[i][j]);
+          v0 += rv.x; v1 += rv.y; v2 += rv.z; v3 += rv.w;
+        }
+        if (row < M && col < N)
+          *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pack4_bf16(v0, v1, v2, v3);
+      }
+    }
+  };
+  using T0 = std::false_type;
+  using T1 = std::true_type;
+  const bool hb = (e.flags & MC_EPI_BIAS) != 0, hr = (e.flags & MC_EPI_RESIDUAL) != 0;
+  auto epilogue = [&](int m0, int n0) {
+    if (hr) {
+      if (hb) epilogue_t(m0, n0, T1{}, T1{});
+      else epilogue_t(m0, n0, T0{}, T1{});
+    } else {
+      if (hb) epilogue_t(m0, n0, T1{}, T0{});
+      else epilogue_t(m0, n0, T0{}, T0{});
+    }
+  };
 
-  stage(0);
-  stage(1);
+  int l = base_l;
+  int m0, n0;
+  coords(l, m0, n0);
+  setup(m0, n0);
+  stage(0, 0);
+  stage(nk > 1 ? 1 : 0, 1);
   wait_tile();
   pp::barrier();
   if (grp == 1) pp::barrier();   // stagger: group 1 runs one segment behind group 0
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* S = smem + (kt % 3) * STAGE;
-    // phase 0: fragments k 0..31; DMA tile kt+2 into the slot tile kt-1 vacated
-    read_frags(S, 0);
-    stage(kt + 2);
-    pp::wait_lgkm0();
-    pp::barrier();
-    mma();
-    pp::barrier();
-    // phase 1: fragments k 32..63; retire this wave's DMAs of tile kt+1
-    read_frags(S, 1);
-    wait_tile();
-    pp::wait_lgkm0();
-    pp::barrier();
-    mma();
-    pp::barrier();
-  }
-  if (grp == 0) pp::barrier();   // balance the stagger
-
-  // ---- epilogue through LDS: 16x16 C layout col = lane & 15, row = 4 * (lane >> 4) + r
-  mc::wait_vmcnt<0>();
-  __syncthreads();
-  unsigned char* region = smem + wave * (64 * EPI_PITCH);
-  const int m_w = wm * 64, n_w = grp * 80;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int oc = 16 * j + fr;
-    const int col = n0 + n_w + oc;
-    const float bv = ((e.flags & MC_EPI_BIAS) && col < N) ? bf2f(e.bias[col]) : 0.f;
+  int slot = 0;                  // ring slot of the K-tile being consumed
+  while (true) {
+    const int ln = l + G;
+    const bool has_next = ln < T;
+    int nm0 = 0, nn0 = 0;
+    if (has_next) coords(ln, nm0, nn0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * i + 4 * fq + r;
-        *reinterpret_cast<u16*>(region + row * EPI_PITCH + 2 * oc) = f2bf(acc[i][j][r] * e.alpha + bv);
+      for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* S = smem + slot * STAGE;
+      const int slot2 = slot >= 1 ? slot - 1 : 2;      // (slot + 2) % 3
+      // phase 0: fragments k 0..31; DMA the K-tile two ahead in the stream into the slot vacated
+      read_frags(S, 0);
+      if (kt + 2 < nk) {
+        stage(kt + 2, slot2);
+      } else if (has_next) {
+        if (kt + 2 == nk) setup(nm0, nn0);             // switch the loaders to the next tile
+        stage(kt + 2 - nk, slot2);
+      } else {
+        stage(nk - 1, slot2);                          // keep the vmcnt pattern: reload into a dead slot
       }
-  }
-  for (int idx = lane; idx < 64 * 10; idx += 64) {
-    const int rr = idx / 10, ch = idx - rr * 10;
-    const int grow = m0 + m_w + rr;
-    const int gcol = n0 + n_w + 8 * ch;
-    s16x8 v = *reinterpret_cast<const s16x8*>(region + rr * EPI_PITCH + 16 * ch);
-    if (grow < M && gcol < N) {
-      if (e.flags & MC_EPI_RESIDUAL) {
-        const s16x8 rv = *reinterpret_cast<const s16x8*>(e.R + (long long)grow * e.ldr + gcol);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((u16)v[t]) + bf2f((u16)rv[t]));
-      }
-      *reinterpret_cast<s16x8*>(e.C + (long long)grow * e.ldc + gcol) = v;
+      pp::wait_lgkm0();
+      pp::barrier();
+      mma();
+      pp::barrier();
+      // phase 1: fragments k 32..63; retire this wave's DMAs of the next K-tile in the stream
+      read_frags(S, 1);
+      wait_tile();
+      pp::wait_lgkm0();
+      pp::barrier();
+      mma();
+      pp::barrier();
+      slot = slot == 2 ? 0 : slot + 1;
     }
+    epilogue(m0, n0);
+    if (!has_next) break;
+    l = ln;
+    m0 = nm0;
+    n0 = nn0;
   }
+  if (grp == 0) pp::barrier();   // balance the stagger
+  mc::wait_vmcnt<0>();           // the trailing dummy DMAs must land before the LDS is released
 }
 
 }  // namespace pq

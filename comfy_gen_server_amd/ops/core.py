@@ -100,7 +100,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v5": 5, "v4": 4}.get(choice, -2)
+        variant = {"v6": 6, "v5": 5, "v4": 4}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N)
     count("gemm", "torch" if be == "torch" else "lib")
     if be == "torch":
