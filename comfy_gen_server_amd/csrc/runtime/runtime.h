@@ -1,0 +1,85 @@
+// Shared declarations for the C++ host runtime (_cgs_runtime).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace cgs {
+
+// ---- BLAKE3 (blake3.cpp)
+std::string blake3_hex(const uint8_t* data, size_t len, size_t out_len = 32);
+std::string blake3_file_hex(const std::string& path);
+
+// ---- safetensors (safetensors.cpp)
+struct TensorInfo {
+  std::string dtype;
+  std::vector<int64_t> shape;
+  uint64_t begin = 0, end = 0;  // byte offsets relative to the data section
+};
+
+class MappedFile {
+ public:
+  explicit MappedFile(const std::string& path);
+  ~MappedFile();
+  MappedFile(const MappedFile&) = delete;
+  MappedFile& operator=(const MappedFile&) = delete;
+  uint8_t* data() const { return base_; }
+  size_t size() const { return size_; }
+
+ private:
+  uint8_t* base_ = nullptr;
+  size_t size_ = 0;
+};
+
+class SafeTensors {
+ public:
+  explicit SafeTensors(const std::string& path);
+  const std::vector<std::string>& keys() const { return order_; }
+  const TensorInfo& info(const std::string& name) const;
+  uint8_t* tensor_ptr(const std::string& name) const;
+  const std::map<std::string, std::string>& metadata() const { return meta_; }
+  std::shared_ptr<MappedFile> file() const { return file_; }
+  // Copy tensors into caller-provided host buffers with a thread pool: page faults of a cold
+  // mmap are the load bottleneck, parallel touch keeps the page cache / NVMe queue full.
+  void copy_many(const std::vector<std::pair<std::string, uint8_t*>>& dst, int threads) const;
+
+ private:
+  std::shared_ptr<MappedFile> file_;
+  uint64_t data_off_ = 0;
+  std::vector<std::string> order_;
+  std::map<std::string, TensorInfo> tensors_;
+  std::map<std::string, std::string> meta_;
+};
+
+struct SaveItem {
+  std::string name, dtype;
+  std::vector<int64_t> shape;
+  std::string bytes;
+};
+void save_safetensors(const std::string& path, const std::vector<SaveItem>& items,
+                      const std::map<std::string, std::string>& metadata);
+std::string json_escape(const std::string& s);
+
+// ---- CLIP byte-level BPE (bpe.cpp)
+class BPE {
+ public:
+  BPE(const std::vector<std::string>& merges, const std::vector<std::string>& vocab);
+  std::vector<int> encode_word(const std::string& utf8_word);
+  size_t vocab_size() const { return encoder_.size(); }
+
+ private:
+  std::vector<int> bpe(const std::string& word) const;
+  std::unordered_map<std::string, int> encoder_;
+  std::unordered_map<std::string, int> ranks_;  // "a b" -> rank
+  std::unordered_map<std::string, std::vector<int>> cache_;
+  std::mutex mu_;
+};
+
+}  // namespace cgs
