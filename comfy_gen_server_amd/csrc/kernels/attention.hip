@@ -405,7 +405,133 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
   }
 }
 
-static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel
+// ------------------------------------------------------------------------------------------------
+// Short-KV path (K03): cross-attention against the text context, D = 64, Sk <= 128 keys
+// (SDXL/SD2 77-token context, Cascade 4..85-token kv_mapper tokens). Every key fits in LDS at once,
+// so there is no key loop and no online softmax: K and V are staged ONCE per workgroup (zero padded
+// to NKT*32 keys, same swizzled images as the D=64 kernel), each wave computes S^T = K Q^T for its
+// 32 queries over all NKT 32-key sub-tiles, takes the exact row max / sum in registers (one
+// permlane32 exchange), and does O^T = V^T P^T. 4 waves x 32 queries = 128 queries per workgroup.
+// The reference runs this shape through the same optimized_attention as self-attention
+// (comfy/ldm/modules/attention.py:352-383); the general flash kernel would pay a full 64-key
+// pipeline for 77 keys.
+template <int NKT>
+__global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
+    const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
+    int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
+    long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
+    float c, int nqb) {
+  constexpr int NK = NKT * 32;
+  __shared__ __attribute__((aligned(16))) u16 Ks[NK * 64];
+  __shared__ __attribute__((aligned(16))) u16 Vs[NK * 64];
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = logical % nqb;
+  const int bh = logical / nqb;
+  const int b = bh / H, h = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hf = lane >> 5;
+
+  const u16* qbase = qp + b * qsb + h * qsh;
+  const u16* kbase = kp + b * ksb + h * ksh;
+  const u16* vbase = vp + b * vsb + h * vsh;
+  u16* obase = op + b * osb + h * osh;
+
+  // stage all keys: thread -> (key, 16-B chunk); keys >= Sk are zero (masked below)
+#pragma unroll
+  for (int it = 0; it < NKT; ++it) {
+    const int idx = it * 256 + tid;
+    const int key = idx >> 3, ch = idx & 7;
+    s16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (key < Sk) {
+      kv = *reinterpret_cast<const s16x8*>(kbase + (long long)key * kss + ch * 8);
+      vv = *reinterpret_cast<const s16x8*>(vbase + (long long)key * vss + ch * 8);
+    }
+    *reinterpret_cast<s16x8*>(&Ks[key * 64 + 8 * (ch ^ ((key >> 1) & 7))]) = kv;
+    *reinterpret_cast<s16x8*>(&Vs[key * 64 + 8 * (ch ^ (((key >> 1) & 1) << 2))]) = vv;
+  }
+
+  const int q_row = qb * 128 + wave * 32 + l32;
+  const bool q_ok = q_row < Sq;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    s16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q_ok) t = *reinterpret_cast<const s16x8*>(qbase + (long long)q_row * qss + ks * 16 + 8 * hf);
+    qf[ks] = __builtin_bit_cast(bf16x8, t);
+  }
+  __syncthreads();
+
+  f32x16 s[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    s[kt] = f32x16{};
+    const int key = kt * 32 + l32;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      s16x8 a = *reinterpret_cast<const s16x8*>(&Ks[key * 64 + 8 * ((2 * ks + hf) ^ ((key >> 1) & 7))]);
+      s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], s[kt], 0, 0, 0);
+    }
+  }
+  // exact softmax over the whole key set (lane = one query, its half of the keys)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+      s[kt][r] = key < Sk ? s[kt][r] : -INFINITY;
+      mx = fmaxf(mx, s[kt][r]);
+    }
+  mx = af_xmax(mx) * c;
+  const float nm = -mx;
+  float ps = 0.f;
+  bf16x8 pf[2 * NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][r], c, nm));
+      ps += p;
+      pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p;
+    }
+  f32x16 ot[2] = {f32x16{}, f32x16{}};
+  const int i16 = lane & 15;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int row0 = kt * 32 + 16 * st + 4 * hf + (i16 >> 2);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+        const int ch = col >> 3, half = (col >> 2) & 1;
+        const int r1 = row0 + 8;
+        const int o0 = row0 * 64 + 8 * (ch ^ (((row0 >> 1) & 1) << 2)) + 4 * half;
+        const int o1 = r1 * 64 + 8 * (ch ^ (((r1 >> 1) & 1) << 2)) + 4 * half;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o0));
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o1));
+        bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ot[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt * 2 + st], ot[dt], 0, 0, 0);
+      }
+    }
+  const float l_tot = ps + __shfl_xor(ps, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (q_ok) {
+    u16* orow = obase + (long long)q_row * oss;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        s16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(ot[dt][4 * r4 + j] * inv);
+        *reinterpret_cast<s16x4*>(orow + dt * 32 + 8 * r4 + 4 * hf) = w;
+      }
+  }
+}
+
+static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel, 3 short-KV kernel
 CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
 
 CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
@@ -421,6 +547,23 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
   const bool al16 = ((qss | kss | vss | oss | qsb | ksb | vsb | osb | qsh | ksh | vsh | osh) & 7) == 0 &&
                     ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
                       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) & 15) == 0;
+  if (D == 64 && !key_mask && !causal && al16 && Sk > 0 && Sk <= 128 &&
+      (g_attn_variant == 0 || g_attn_variant == 3)) {
+    const int nqb3 = (Sq + 127) / 128;
+    const long long nwg3 = (long long)nqb3 * B * H;
+    if (nwg3 > 0x7fffffff) return (int)hipErrorInvalidValue;
+#define SKV_LAUNCH(NKT)                                                                                            \
+  attn_fwd_d64_shortkv_kernel<NKT><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                                     \
+      (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, \
+      osb, oss, osh, sl2, nqb3)
+    if (Sk <= 32) SKV_LAUNCH(1);
+    else if (Sk <= 64) SKV_LAUNCH(2);
+    else if (Sk <= 96) SKV_LAUNCH(3);
+    else SKV_LAUNCH(4);
+#undef SKV_LAUNCH
+    return (int)hipGetLastError();
+  }
+  if (g_attn_variant == 3) return (int)hipErrorInvalidValue;
   if (D == 64 && !key_mask && !causal && al16 && g_attn_variant != 1 && Sk > 0) {
     int nqb2 = (Sq + 255) / 256;
     long long nwg2 = (long long)nqb2 * B * H;

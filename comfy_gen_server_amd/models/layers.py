@@ -30,7 +30,18 @@ class DerivedMixin:
         self.__dict__["_derived"] = {}
 
 
+# Bumped whenever weights may have moved or changed (patch / unpatch / device move): captured
+# hipGraph plans (runtime/graphs.py) hold raw weight pointers and are retired on a new epoch.
+WEIGHTS_EPOCH = 0
+
+
+def bump_weights_epoch():
+    global WEIGHTS_EPOCH
+    WEIGHTS_EPOCH += 1
+
+
 def invalidate_all(module: nn.Module):
+    bump_weights_epoch()
     for m in module.modules():
         if isinstance(m, DerivedMixin):
             m.invalidate_derived()
@@ -84,6 +95,20 @@ class Conv2d(nn.Module, DerivedMixin):
         if w.dtype != x.dtype or w.device != x.device:
             w = w.to(device=x.device, dtype=x.dtype)
             b = None if b is None else b.to(device=x.device, dtype=x.dtype)
+        elif x.is_cuda and self.groups == 1 and self.in_channels % 32 and x.dtype == torch.bfloat16 \
+                and residual is None and not upsample2x:
+            # narrow-input convs (UNet conv_in: 4 or 8 latent channels, 3-channel image stems):
+            # zero-pad Cin to 32 so the MFMA implicit-GEMM kernel runs them too (no library conv
+            # on the hot path, and the forward stays hipGraph-capturable).
+            cp = (self.in_channels + 31) // 32 * 32
+            pad = cp - self.in_channels
+            w = self._derived_get("w_pad", lambda: torch.nn.functional.pad(self.weight, (0, 0, 0, 0, 0, pad)))
+            wn = self._derived_get("w_nhwc_pad", lambda: w.permute(0, 2, 3, 1).contiguous())
+            xp = torch.empty((x.shape[0], cp, x.shape[2], x.shape[3]), device=x.device, dtype=x.dtype,
+                             memory_format=torch.channels_last)
+            xp[:, self.in_channels:].zero_()
+            xp[:, :self.in_channels] = x
+            x = xp
         elif x.is_cuda and self.groups == 1:
             wn = self.weight_nhwc()
         return ops.conv2d(x, w, b, self.stride, self.padding, residual=residual, weight_nhwc=wn,

@@ -9,6 +9,7 @@ Tensor conventions
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -186,6 +187,7 @@ def geglu_deinterleave(w: torch.Tensor) -> torch.Tensor:
 # Attention
 # ----------------------------------------------------------------------------------------------
 _FLASH_HEAD_DIMS = (32, 40, 64, 80, 96, 128, 160)
+_ATTN_ALLOW_LIB = os.environ.get("CGS_ATTN_ALLOW_LIB", "0") == "1"
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
@@ -223,7 +225,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
             return o
 
         choice = "hip"
-        if kp is None and B * heads * Sq * Sk >= (1 << 22):
+        # The vendor SDPA is a tuning candidate only on explicit request: the hot path is the
+        # hand-written kernel (K02/K03), never an SDPA fallback.
+        if kp is None and _ATTN_ALLOW_LIB and B * heads * Sq * Sk >= (1 << 22):
             choice = autotune.choose(("attention", B, heads, Sq, Sk, D, int(causal)),
                                      [("hip", run_hip), ("lib", lambda: _sdpa(q, k, v, heads, causal))],
                                      default="hip")

@@ -74,10 +74,20 @@ class BaseModel(torch.nn.Module):
             if hasattr(v, "dtype") and v.dtype not in (torch.int, torch.long):
                 v = v.to(dtype)
             extra[k] = v
-        out = self.diffusion_model(xc, ts, context=context, control=control,
-                                   transformer_options=transformer_options if transformer_options is not None else {},
-                                   **extra).float()
+        out = self.denoiser_forward()(xc, ts, context=context, control=control,
+                                      transformer_options=transformer_options if transformer_options is not None else {},
+                                      **extra).float()
         return self.model_sampling.calculate_denoised(sigma, out, x)
+
+    def denoiser_forward(self):
+        """The diffusion model's forward, replayed from per-plan hipGraphs on the device
+        (``runtime/graphs.py``); eager on the CPU or whenever hooks make the forward dynamic."""
+        r = self.__dict__.get("_graph_runner")
+        if r is None or r.module is not self.diffusion_model:
+            from .graphs import GraphedForward
+            r = GraphedForward(self.diffusion_model)
+            self.__dict__["_graph_runner"] = r
+        return r
 
     def is_adm(self):
         return self.adm_channels > 0

@@ -328,6 +328,8 @@ class ModelPatcher:
                 self.object_patches_backup[k] = old
         if device_to is not None and not self.is_resident_on(device_to):
             self.model.to(device_to)
+            from ..models.layers import bump_weights_epoch
+            bump_weights_epoch()
         if patch_weights and (force or getattr(self.model, "current_patches_uuid", None) != self.patches_uuid):
             # restore weights that have a backup but are no longer patched
             for k in list(self.backup.keys()):

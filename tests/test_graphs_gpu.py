@@ -1,0 +1,72 @@
+"""hipGraph capture/replay of the denoiser (runtime/graphs.py): replayed forwards must equal the
+eager forward, plans are retired when weights change, hooks keep the forward eager."""
+import pytest
+import torch
+
+from comfy_gen_server_amd.models.layers import init_random_fast_, invalidate_all
+from comfy_gen_server_amd.models.unet import UNetModel
+from comfy_gen_server_amd.runtime.graphs import GraphedForward
+
+CFG = dict(in_channels=4, model_channels=128, out_channels=4, num_res_blocks=[1, 1], channel_mult=[1, 2],
+           transformer_depth=[1, 1], transformer_depth_output=[1, 1, 1, 1], transformer_depth_middle=1,
+           num_heads=2, num_head_channels=-1, use_linear_in_transformer=True, context_dim=128,
+           num_classes="sequential", adm_in_channels=64)
+
+
+def _inputs(dev, B=4, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(B, 4, 32, 32, generator=g).to(dev, torch.bfloat16)
+    t = torch.tensor([999.0, 500.0, 10.0, 1.0][:B]).to(dev)
+    ctx = torch.randn(B, 77, 128, generator=g).to(dev, torch.bfloat16)
+    y = torch.randn(B, 64, generator=g).to(dev, torch.bfloat16)
+    return x, t, ctx, y
+
+
+@pytest.mark.gpu
+def test_graph_replay_matches_eager(cuda, monkeypatch):
+    monkeypatch.setenv("CGS_GRAPHS", "1")
+    with torch.inference_mode():
+        m = UNetModel(**CFG, dtype=torch.bfloat16, device=cuda)
+        init_random_fast_(m, seed=3)
+        runner = GraphedForward(m)
+        x, t, ctx, y = _inputs(cuda)
+        ref = m(x, t, context=ctx, y=y, transformer_options={}).float()
+        outs = [runner(x, t, context=ctx, y=y, transformer_options={}).float() for _ in range(3)]
+        torch.cuda.synchronize()
+        assert runner.stats == {"eager": 1, "capture": 1, "replay": 2}, runner.stats
+        for o in outs:
+            assert (o - ref).abs().max().item() < 2e-2 * (ref.abs().max().item() + 1)
+        # new inputs through the same plan
+        x2, t2, ctx2, y2 = _inputs(cuda, seed=7)
+        ref2 = m(x2, t2, context=ctx2, y=y2, transformer_options={}).float()
+        o2 = runner(x2, t2, context=ctx2, y=y2, transformer_options={}).float()
+        assert runner.stats["replay"] == 3
+        assert (o2 - ref2).abs().max().item() < 2e-2 * (ref2.abs().max().item() + 1)
+        # a weight change (LoRA merge / unpatch path) retires the plan
+        for p in m.parameters():
+            p.data = p.data * 0.5
+        invalidate_all(m)
+        ref3 = m(x2, t2, context=ctx2, y=y2, transformer_options={}).float()
+        o3 = [runner(x2, t2, context=ctx2, y=y2, transformer_options={}).float() for _ in range(3)][-1]
+        assert runner.stats["capture"] == 2
+        assert (o3 - ref3).abs().max().item() < 2e-2 * (ref3.abs().max().item() + 1)
+        # hooks make the forward dynamic: always eager
+        e0 = runner.stats["eager"]
+        runner(x2, t2, context=ctx2, y=y2, transformer_options={"patches": {"middle_patch": [lambda h, o: h]}})
+        assert runner.stats["eager"] == e0 + 1
+
+
+def test_graphs_cpu_is_eager():
+    m = UNetModel(**dict(CFG, model_channels=32, num_heads=2, context_dim=32), dtype=torch.float32)
+    from comfy_gen_server_amd.models.layers import init_random_
+    init_random_(m, seed=0)
+    runner = GraphedForward(m)
+    x = torch.randn(2, 4, 16, 16)
+    t = torch.tensor([10.0, 20.0])
+    ctx = torch.randn(2, 7, 32)
+    y = torch.randn(2, 64)
+    with torch.inference_mode():
+        a = runner(x, t, context=ctx, y=y, transformer_options={})
+        b = runner(x, t, context=ctx, y=y, transformer_options={})
+    assert runner.stats == {"eager": 2, "capture": 0, "replay": 0}
+    assert torch.equal(a, b)
