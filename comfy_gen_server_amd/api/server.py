@@ -540,7 +540,14 @@ class PromptServer:
             await _send_socket_catch_exception(self.sockets[sid].send_json, message)
 
     def send_sync(self, event, data, sid=None):
-        self.loop.call_soon_threadsafe(self.messages.put_nowait, (event, data, sid))
+        """Thread-safe hand-off to the event loop (reference server.py:813-815). After shutdown the
+        loop is closed: late progress ticks from a still-running node are dropped, not raised."""
+        if self.loop.is_closed():
+            return
+        try:
+            self.loop.call_soon_threadsafe(self.messages.put_nowait, (event, data, sid))
+        except RuntimeError:      # closed between the check and the call
+            pass
 
     def queue_updated(self):
         self.send_sync("status", {"status": self.get_queue_info()})

@@ -106,13 +106,14 @@ class GEGLU(nn.Module, DerivedMixin):
         return a * torch.nn.functional.gelu(g)
 
 
-class GELUProj(nn.Module):
+class GELUProj(_Seq):
+    """Non-gated projection ``Sequential(Linear, GELU)`` (keys ``net.0.0.*``, attention.py:71-74)."""
+
     def __init__(self, dim_in, dim_out, dtype=None, device=None):
-        super().__init__()
-        self.proj = Linear(dim_in, dim_out, dtype=dtype, device=device)
+        super().__init__(Linear(dim_in, dim_out, dtype=dtype, device=device))
 
     def forward(self, x):
-        return torch.nn.functional.gelu(self.proj(x))
+        return torch.nn.functional.gelu(self[0](x))
 
 
 class FeedForward(nn.Module):
@@ -129,26 +130,56 @@ class FeedForward(nn.Module):
 
 class BasicTransformerBlock(nn.Module):
     def __init__(self, dim, n_heads, d_head, context_dim=None, gated_ff=True, disable_self_attn=False,
-                 dtype=None, device=None):
+                 dtype=None, device=None, ff_in=False, inner_dim=None, disable_temporal_crossattention=False,
+                 switch_temporal_ca_to_sa=False):
         super().__init__()
+        kw = dict(dtype=dtype, device=device)
+        # video (SVD time-mixing) options of attention.py:419-457: an input FF (dim -> inner_dim), a
+        # residual only when inner_dim == dim, optional temporal cross-attention
+        self.has_ff_in = bool(ff_in or inner_dim is not None)
+        inner_dim = dim if inner_dim is None else inner_dim
+        self.is_res = inner_dim == dim
+        if self.has_ff_in:
+            self.norm_in = LayerNorm(dim, **kw)
+            self.ff_in = FeedForward(dim, dim_out=inner_dim, glu=gated_ff, **kw)
         self.disable_self_attn = disable_self_attn
+        self.switch_temporal_ca_to_sa = switch_temporal_ca_to_sa
         self.n_heads = n_heads
         self.d_head = d_head
-        self.attn1 = CrossAttention(dim, context_dim if disable_self_attn else None, n_heads, d_head,
-                                    dtype=dtype, device=device)
-        self.ff = FeedForward(dim, glu=gated_ff, dtype=dtype, device=device)
-        self.attn2 = CrossAttention(dim, context_dim, n_heads, d_head, dtype=dtype, device=device)
-        self.norm1 = LayerNorm(dim, dtype=dtype, device=device)
-        self.norm2 = LayerNorm(dim, dtype=dtype, device=device)
-        self.norm3 = LayerNorm(dim, dtype=dtype, device=device)
+        self.attn1 = CrossAttention(inner_dim, context_dim if disable_self_attn else None, n_heads, d_head, **kw)
+        self.ff = FeedForward(inner_dim, dim_out=dim, glu=gated_ff, **kw)
+        if disable_temporal_crossattention:
+            if switch_temporal_ca_to_sa:
+                raise ValueError("switch_temporal_ca_to_sa needs the temporal cross-attention")
+            self.attn2 = None
+        else:
+            self.attn2 = CrossAttention(inner_dim, None if switch_temporal_ca_to_sa else context_dim, n_heads, d_head,
+                                        **kw)
+            self.norm2 = LayerNorm(inner_dim, **kw)
+        self.norm1 = LayerNorm(inner_dim, **kw)
+        self.norm3 = LayerNorm(inner_dim, **kw)
+        self._plain = not self.has_ff_in and self.attn2 is not None and self.is_res and not switch_temporal_ca_to_sa
 
     def forward(self, x, context=None, transformer_options=None):
         to = transformer_options or {}
         patches = to.get("patches", {})
         replace = to.get("patches_replace", {})
+        if not self._plain:
+            return self._forward_video(x, context)
         if not patches and not replace:
             return self._forward_fast(x, context, to)
         return self._forward_patched(x, context, to, patches, replace)
+
+    def _forward_video(self, x, context):
+        """Time-mixing block (SVD): ff_in, self-attention, optional temporal cross-attention, FF."""
+        if self.has_ff_in:
+            x = self.ff_in(self.norm_in(x), residual=x if self.is_res else None)
+        ctx1 = context if self.disable_self_attn else None
+        x = self.attn1(self.norm1(x), context=ctx1, residual=x)
+        if self.attn2 is not None:
+            n = self.norm2(x)
+            x = self.attn2(n, context=n if self.switch_temporal_ca_to_sa else context, residual=x)
+        return self.ff(self.norm3(x), residual=x if self.is_res else None)
 
     def _forward_fast(self, x, context, to):
         """Hook-free path: residual adds fused into the out-projection / FF-out GEMM epilogues."""

@@ -115,6 +115,59 @@ class Conv2d(nn.Module, DerivedMixin):
                           groups=self.groups, upsample2x=upsample2x)
 
 
+class Conv3d(nn.Module, DerivedMixin):
+    """3-D convolution for the video blocks (SVD time-mixing ResBlocks, AE3DConv of the temporal VAE).
+
+    Activations stay in the 2-D frame layout ``[(b t), C, H, W]`` (channels_last on the device);
+    ``forward(x, frames)`` convolves over (t, h, w) of the ``b = N / frames`` videos. The video
+    kernels are temporal-only, ``[kt, 1, 1]`` with padding ``[kt // 2, 0, 0]``: on the device that is
+    one implicit-GEMM MFMA conv over the image ``[b, t + 2p, h*w, C]`` with a ``(kt, 1)`` filter (the
+    frames are zero-padded along t once, never an im2col). Other kernel shapes run ``F.conv3d``.
+    """
+
+    def __init__(self, in_channels, out_channels, kernel_size, padding=0, bias=True, dtype=None, device=None):
+        super().__init__()
+        ks = tuple(kernel_size) if isinstance(kernel_size, (list, tuple)) else (kernel_size,) * 3
+        pd = tuple(padding) if isinstance(padding, (list, tuple)) else (padding,) * 3
+        self.in_channels, self.out_channels, self.kernel_size, self.padding = in_channels, out_channels, ks, pd
+        self.weight = nn.Parameter(torch.empty((out_channels, in_channels) + ks, dtype=dtype, device=device),
+                                   requires_grad=False)
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_channels, dtype=dtype, device=device), requires_grad=False)
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, x, frames):
+        n, c, h, w = x.shape
+        b = n // frames
+        kt, kh, kw = self.kernel_size
+        wgt, bias = self.weight, self.bias
+        if wgt.dtype != x.dtype or wgt.device != x.device:
+            wgt = wgt.to(device=x.device, dtype=x.dtype)
+            bias = None if bias is None else bias.to(device=x.device, dtype=x.dtype)
+        temporal = kh == 1 and kw == 1 and self.padding[1] == 0 and self.padding[2] == 0
+        if x.is_cuda and temporal and x.dtype == torch.bfloat16 and c % 32 == 0 and wgt is self.weight:
+            p = self.padding[0]
+            xf = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(b, frames, h * w, c)
+            if p:
+                xp = torch.empty((b, frames + 2 * p, h * w, c), device=x.device, dtype=x.dtype)
+                xp[:, :p].zero_()
+                xp[:, frames + p:].zero_()
+                xp[:, p:frames + p] = xf
+            else:
+                xp = xf
+            img = xp.permute(0, 3, 1, 2)                      # [b, C, t+2p, h*w], channels_last storage
+            w2 = self._derived_get("w2d", lambda: self.weight.reshape(self.out_channels, self.in_channels, kt, 1))
+            wn = self._derived_get("w2d_nhwc", lambda: w2.permute(0, 2, 3, 1).contiguous())
+            y = ops.conv2d(img, w2, bias, 1, 0, weight_nhwc=wn)  # [b, Cout, t, h*w]
+            y = y.permute(0, 2, 3, 1).reshape(n, h, w, self.out_channels)
+            return y.permute(0, 3, 1, 2)
+        x5 = x.reshape(b, frames, c, h, w).permute(0, 2, 1, 3, 4).float()
+        y = torch.nn.functional.conv3d(x5, wgt.float(), None if bias is None else bias.float(), 1, self.padding)
+        y = y.permute(0, 2, 1, 3, 4).reshape(n, self.out_channels, h, w).to(x.dtype)
+        return y.contiguous(memory_format=torch.channels_last) if x.is_cuda else y
+
+
 class GroupNorm(nn.Module):
     def __init__(self, num_groups, num_channels, eps=1e-5, affine=True, dtype=None, device=None):
         super().__init__()

@@ -23,8 +23,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .attention import SpatialTransformer, _Seq
-from .layers import Conv2d, GroupNorm, Linear
+from .attention import BasicTransformerBlock, SpatialTransformer, _Seq
+from .layers import Conv2d, Conv3d, GroupNorm, Linear
 
 
 class ResBlock(nn.Module):
@@ -81,11 +81,93 @@ class Upsample(nn.Module):
         return self.conv(x)
 
 
+# ------------------------------------------------------------------------------------------------
+# Video (SVD / SV3D) blocks: openaimodel.py:267-345 (VideoResBlock), attention.py:642-800
+# (SpatialVideoTransformer), util.py:20-86 (AlphaBlender). Activations keep the 2-D frame layout
+# [(b t), C, H, W]; temporal mixing reshapes NHWC frames, never materialises b c t h w.
+# ------------------------------------------------------------------------------------------------
+class AlphaBlender(nn.Module):
+    def __init__(self, alpha, merge_strategy="learned_with_images"):
+        super().__init__()
+        self.merge_strategy = merge_strategy
+        if merge_strategy == "fixed":
+            self.register_buffer("mix_factor", torch.tensor([float(alpha)]))
+        elif merge_strategy in ("learned", "learned_with_images"):
+            self.mix_factor = nn.Parameter(torch.tensor([float(alpha)]), requires_grad=False)
+        else:
+            raise ValueError(f"unknown merge strategy {merge_strategy}")
+
+    def get_alpha(self, image_only_indicator, device):
+        m = self.mix_factor.to(device=device, dtype=torch.float32)
+        if self.merge_strategy == "fixed":
+            return m
+        a = torch.sigmoid(m)
+        if self.merge_strategy == "learned_with_images" and image_only_indicator is not None:
+            a = torch.where(image_only_indicator.bool().to(device), torch.ones_like(a), a).reshape(-1)
+        return a
+
+    def forward(self, x_spatial, x_temporal, image_only_indicator=None):
+        a = self.get_alpha(image_only_indicator, x_spatial.device)
+        if a.numel() > 1:          # per-frame: frames are the leading dim of both operands
+            a = a.view((-1,) + (1,) * (x_spatial.dim() - 1))
+        a = a.to(x_spatial.dtype)
+        return a * x_spatial + (1.0 - a) * x_temporal
+
+
+def group_norm_frames(gn, x, frames, silu=False):
+    """GroupNorm of a 5-D video tensor (statistics over C/G x t x h x w per video) given as frames."""
+    n, c, h, w = x.shape
+    b = n // frames
+    if x.is_cuda:
+        x4 = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(b, frames * h, w, c)
+        y = gn(x4.permute(0, 3, 1, 2), silu=silu)
+        return y.permute(0, 2, 3, 1).reshape(n, h, w, c).permute(0, 3, 1, 2)
+    x5 = x.reshape(b, frames, c, h, w).transpose(1, 2).float()
+    y = torch.nn.functional.group_norm(x5, gn.num_groups, None if gn.weight is None else gn.weight.float(),
+                                       None if gn.bias is None else gn.bias.float(), gn.eps)
+    if silu:
+        y = torch.nn.functional.silu(y)
+    return y.transpose(1, 2).reshape(n, c, h, w).to(x.dtype)
+
+
+class TimeStackResBlock(nn.Module):
+    """ResBlock(dims=3) of the video blocks: GN over the whole clip, temporal [kt,1,1] convs, optional
+    per-frame timestep embedding (``exchange_temb_dims``), identity skip."""
+
+    def __init__(self, channels, emb_channels, kernel_size=(3, 1, 1), skip_t_emb=False, dtype=None, device=None):
+        super().__init__()
+        ks = list(kernel_size) if isinstance(kernel_size, (list, tuple)) else [kernel_size] * 3
+        pad = [k // 2 for k in ks]
+        kw = dict(dtype=dtype, device=device)
+        self.skip_t_emb = skip_t_emb
+        self.in_layers = _Seq(GroupNorm(32, channels, **kw), nn.SiLU(), Conv3d(channels, channels, ks, pad, **kw))
+        if not skip_t_emb:
+            self.emb_layers = _Seq(nn.SiLU(), Linear(emb_channels, channels, **kw))
+        self.out_layers = _Seq(GroupNorm(32, channels, **kw), nn.SiLU(), nn.Dropout(0.0),
+                               Conv3d(channels, channels, ks, pad, **kw))
+
+    def forward(self, x, emb_silu, frames):
+        h = self.in_layers[2](group_norm_frames(self.in_layers[0], x, frames, silu=True), frames)
+        if not self.skip_t_emb and emb_silu is not None:
+            e = self.emb_layers[1](emb_silu).to(h.dtype)          # [(b t), C]: per-frame embedding
+            h = h + e[:, :, None, None]
+        h = group_norm_frames(self.out_layers[0], h, frames, silu=True)
+        return self.out_layers[3](h, frames) + x
+
+
 class TimestepEmbedSequential(nn.ModuleList):
-    def forward(self, x, emb_silu, context, transformer_options, output_shape=None):
+    def forward(self, x, emb_silu, context, transformer_options, output_shape=None, time_context=None,
+                num_video_frames=None, image_only_indicator=None):
         for layer in self:
-            if isinstance(layer, ResBlock):
+            if isinstance(layer, VideoResBlock):
+                x = layer(x, emb_silu, transformer_options, num_video_frames, image_only_indicator)
+            elif isinstance(layer, ResBlock):
                 x = layer(x, emb_silu, transformer_options)
+            elif isinstance(layer, SpatialVideoTransformer):
+                x = layer(x, context, transformer_options, time_context=time_context, frames=num_video_frames,
+                          image_only_indicator=image_only_indicator)
+                if "transformer_index" in transformer_options:
+                    transformer_options["transformer_index"] += 1
             elif isinstance(layer, SpatialTransformer):
                 x = layer(x, context, transformer_options)
                 if "transformer_index" in transformer_options:
@@ -95,6 +177,82 @@ class TimestepEmbedSequential(nn.ModuleList):
             else:
                 x = layer(x)
         return x
+
+
+class VideoResBlock(ResBlock):
+    def __init__(self, channels, emb_channels, out_channels=None, video_kernel_size=(3, 1, 1),
+                 merge_strategy="fixed", merge_factor=0.5, dtype=None, device=None):
+        super().__init__(channels, emb_channels, out_channels, dtype=dtype, device=device)
+        self.time_stack = TimeStackResBlock(self.out_channels, emb_channels, video_kernel_size, dtype=dtype,
+                                            device=device)
+        self.time_mixer = AlphaBlender(merge_factor, merge_strategy)
+
+    def forward(self, x, emb_silu, transformer_options=None, num_video_frames=None, image_only_indicator=None):
+        x = super().forward(x, emb_silu, transformer_options)
+        xt = self.time_stack(x, emb_silu, num_video_frames)
+        return self.time_mixer(x_spatial=x, x_temporal=xt, image_only_indicator=image_only_indicator)
+
+
+class SpatialVideoTransformer(SpatialTransformer):
+    def __init__(self, in_channels, n_heads, d_head, depth=1, context_dim=None, use_linear=False,
+                 time_context_dim=None, ff_in=False, use_spatial_context=False, merge_strategy="fixed",
+                 merge_factor=0.5, disable_self_attn=False, disable_temporal_crossattention=False,
+                 max_time_embed_period=10000, dtype=None, device=None):
+        super().__init__(in_channels, n_heads, d_head, depth=depth, context_dim=context_dim,
+                         disable_self_attn=disable_self_attn, use_linear=use_linear, dtype=dtype, device=device)
+        inner = n_heads * d_head
+        if use_spatial_context:
+            time_context_dim = context_dim
+        kw = dict(dtype=dtype, device=device)
+        self.time_stack = nn.ModuleList([
+            BasicTransformerBlock(inner, n_heads, d_head, context_dim=time_context_dim, ff_in=ff_in, inner_dim=inner,
+                                  disable_self_attn=disable_self_attn,
+                                  disable_temporal_crossattention=disable_temporal_crossattention, **kw)
+            for _ in range(depth)])
+        self.use_spatial_context = use_spatial_context
+        self.max_time_embed_period = max_time_embed_period
+        self.time_pos_embed = _Seq(Linear(in_channels, in_channels * 4, **kw), nn.SiLU(),
+                                   Linear(in_channels * 4, in_channels, **kw))
+        self.time_mixer = AlphaBlender(merge_factor, merge_strategy)
+
+    def forward(self, x, context=None, transformer_options=None, time_context=None, frames=None,
+                image_only_indicator=None):
+        to = transformer_options if transformer_options is not None else {}
+        b_t, c, h, w = x.shape
+        frames = frames or b_t
+        b = b_t // frames
+        S = h * w
+        if self.use_spatial_context:
+            tc = context if time_context is None else time_context
+            time_context = tc[::frames].repeat_interleave(S, dim=0)
+        elif time_context is not None:
+            time_context = time_context.repeat_interleave(S, dim=0)
+            if time_context.dim() == 2:
+                time_context = time_context[:, None]
+        x_in = x
+        x = self.norm(x)
+        if not self.use_linear:
+            x = self.proj_in(x)
+        x = x.permute(0, 2, 3, 1).reshape(b_t, S, -1)
+        if self.use_linear:
+            x = self.proj_in(x)
+        C = x.shape[-1]
+        fr = torch.arange(frames, device=x.device, dtype=torch.float32).repeat(b)
+        t_emb = ops.timestep_embedding(fr, self.in_channels, max_period=self.max_time_embed_period).to(x.dtype)
+        emb = self.time_pos_embed[2](ops.silu(self.time_pos_embed[0](t_emb)))[:, None, :]
+        for i, (blk, mix) in enumerate(zip(self.transformer_blocks, self.time_stack)):
+            to["block_index"] = i
+            x = blk(x, context=context, transformer_options=to)
+            xm = (x + emb).reshape(b, frames, S, C).transpose(1, 2).reshape(b * S, frames, C)
+            xm = mix(xm, context=time_context)
+            xm = xm.reshape(b, S, frames, C).transpose(1, 2).reshape(b_t, S, C)
+            x = self.time_mixer(x_spatial=x, x_temporal=xm, image_only_indicator=image_only_indicator)
+        if self.use_linear:
+            x = self.proj_out(x)
+        x = x.reshape(b_t, h, w, -1).permute(0, 3, 1, 2)
+        if not self.use_linear:
+            x = self.proj_out(x)
+        return x + x_in
 
 
 def _apply_control(h, control, name):
@@ -113,9 +271,32 @@ class UNetModel(nn.Module):
                  channel_mult=(1, 2, 4, 4), transformer_depth=1, transformer_depth_middle=None,
                  transformer_depth_output=None, context_dim=None, num_heads=-1, num_head_channels=-1,
                  use_linear_in_transformer=False, adm_in_channels=None, num_classes=None,
-                 disable_self_attentions=None, use_temporal_attention=False, dtype=torch.float32,
+                 disable_self_attentions=None, use_temporal_attention=False, use_temporal_resblock=False,
+                 time_context_dim=None, extra_ff_mix_layer=False, use_spatial_context=False, merge_strategy=None,
+                 merge_factor=0.0, video_kernel_size=None, disable_temporal_crossattention=False,
+                 max_ddpm_temb_period=10000, disable_middle_self_attn=False, dtype=torch.float32,
                  device=None, build_decoder=True, **unused):
         super().__init__()
+        self.default_num_video_frames = None
+        vks = video_kernel_size if video_kernel_size is not None else [3, 1, 1]
+
+        def resblock(ch_in, emb_ch, ch_out, **kw2):
+            if use_temporal_resblock:
+                return VideoResBlock(ch_in, emb_ch, ch_out, video_kernel_size=vks, merge_strategy=merge_strategy,
+                                     merge_factor=merge_factor, **kw2)
+            return ResBlock(ch_in, emb_ch, ch_out, **kw2)
+
+        def attn_layer(ch, nh, dh, depth, dsa, **kw2):
+            if use_temporal_attention:
+                return SpatialVideoTransformer(ch, nh, dh, depth=depth, context_dim=context_dim,
+                                               use_linear=use_linear_in_transformer, time_context_dim=time_context_dim,
+                                               ff_in=extra_ff_mix_layer, use_spatial_context=use_spatial_context,
+                                               merge_strategy=merge_strategy, merge_factor=merge_factor,
+                                               disable_self_attn=dsa,
+                                               disable_temporal_crossattention=disable_temporal_crossattention,
+                                               max_time_embed_period=max_ddpm_temb_period, **kw2)
+            return SpatialTransformer(ch, nh, dh, depth=depth, context_dim=context_dim, disable_self_attn=dsa,
+                                      use_linear=use_linear_in_transformer, **kw2)
         nl = len(channel_mult)
         if isinstance(num_res_blocks, int):
             num_res_blocks = [num_res_blocks] * nl
@@ -161,13 +342,12 @@ class UNetModel(nn.Module):
         td = list(transformer_depth)
         for level, mult in enumerate(channel_mult):
             for _ in range(num_res_blocks[level]):
-                layers = [ResBlock(ch, ted, mult * model_channels, **kw)]
+                layers = [resblock(ch, ted, mult * model_channels, **kw)]
                 ch = mult * model_channels
                 nt = td.pop(0) if td else 0
                 if nt > 0:
                     h, dh = heads_for(ch)
-                    layers.append(SpatialTransformer(ch, h, dh, depth=nt, context_dim=context_dim,
-                                                     disable_self_attn=dsa(level), use_linear=use_linear_in_transformer, **kw))
+                    layers.append(attn_layer(ch, h, dh, nt, dsa(level), **kw))
                 self.input_blocks.append(TimestepEmbedSequential(layers))
                 chans.append(ch)
             if level != nl - 1:
@@ -176,12 +356,11 @@ class UNetModel(nn.Module):
 
         self.middle_block = None
         if transformer_depth_middle >= -1:
-            mid = [ResBlock(ch, ted, ch, **kw)]
+            mid = [resblock(ch, ted, ch, **kw)]
             if transformer_depth_middle >= 0:
                 h, dh = heads_for(ch)
-                mid += [SpatialTransformer(ch, h, dh, depth=transformer_depth_middle, context_dim=context_dim,
-                                           disable_self_attn=False, use_linear=use_linear_in_transformer, **kw),
-                        ResBlock(ch, ted, ch, **kw)]
+                mid += [attn_layer(ch, h, dh, transformer_depth_middle, disable_middle_self_attn, **kw),
+                        resblock(ch, ted, ch, **kw)]
             self.middle_block = TimestepEmbedSequential(mid)
 
         self._encoder_channels = list(chans)
@@ -193,13 +372,12 @@ class UNetModel(nn.Module):
         for level, mult in list(enumerate(channel_mult))[::-1]:
             for i in range(num_res_blocks[level] + 1):
                 ich = chans.pop()
-                layers = [ResBlock(ch + ich, ted, model_channels * mult, **kw)]
+                layers = [resblock(ch + ich, ted, model_channels * mult, **kw)]
                 ch = model_channels * mult
                 nt = tdo.pop() if tdo else 0
                 if nt > 0:
                     h, dh = heads_for(ch)
-                    layers.append(SpatialTransformer(ch, h, dh, depth=nt, context_dim=context_dim,
-                                                     disable_self_attn=dsa(level), use_linear=use_linear_in_transformer, **kw))
+                    layers.append(attn_layer(ch, h, dh, nt, dsa(level), **kw))
                 if level and i == num_res_blocks[level]:
                     layers.append(Upsample(ch, ch, **kw))
                 self.output_blocks.append(TimestepEmbedSequential(layers))
@@ -208,6 +386,11 @@ class UNetModel(nn.Module):
     # ------------------------------------------------------------------------------------------
     def forward(self, x, timesteps=None, context=None, y=None, control=None, transformer_options=None, **kwargs):
         to = transformer_options if transformer_options is not None else {}
+        num_video_frames = kwargs.get("num_video_frames", self.default_num_video_frames)
+        image_only_indicator = kwargs.get("image_only_indicator")
+        time_context = kwargs.get("time_context")
+        vk = dict(time_context=time_context, num_video_frames=num_video_frames,
+                  image_only_indicator=image_only_indicator)
         to["original_shape"] = list(x.shape)
         to["transformer_index"] = 0
         patches = to.get("patches", {})
@@ -220,6 +403,8 @@ class UNetModel(nn.Module):
             x = x.to(dt)
         if context is not None:
             context = context.to(dt)
+        if time_context is not None:
+            vk["time_context"] = time_context.to(dt)
         t_emb = ops.timestep_embedding(timesteps, self.model_channels).to(dt)
         emb = self.time_embed[2](ops.silu(self.time_embed[0](t_emb)))
         if self.num_classes is not None:
@@ -232,7 +417,7 @@ class UNetModel(nn.Module):
         h = x
         for i, mod in enumerate(self.input_blocks):
             to["block"] = ("input", i)
-            h = mod(h, emb_silu, context, to)
+            h = mod(h, emb_silu, context, to, **vk)
             h = _apply_control(h, control, "input")
             for p in patches.get("input_block_patch", []):
                 h = p(h, to)
@@ -242,7 +427,7 @@ class UNetModel(nn.Module):
 
         to["block"] = ("middle", 0)
         if self.middle_block is not None:
-            h = self.middle_block(h, emb_silu, context, to)
+            h = self.middle_block(h, emb_silu, context, to, **vk)
         h = _apply_control(h, control, "middle")
 
         for i, mod in enumerate(self.output_blocks):
@@ -255,6 +440,6 @@ class UNetModel(nn.Module):
             if x.is_cuda:
                 h = h.contiguous(memory_format=torch.channels_last)
             out_shape = hs[-1].shape if hs else None
-            h = mod(h, emb_silu, context, to, output_shape=out_shape)
+            h = mod(h, emb_silu, context, to, output_shape=out_shape, **vk)
         h = self.out[0](h, silu=True)
         return self.out[2](h)

@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .layers import Conv2d, GroupNorm, DerivedMixin
+from .layers import Conv2d, Conv3d, GroupNorm, DerivedMixin
 
 
 def _norm(c, dtype=None, device=None):
@@ -146,19 +146,66 @@ class Encoder(nn.Module):
         return self.conv_out(self.norm_out(h, silu=True))
 
 
+class VideoResnetBlock(ResnetBlock):
+    """Temporal-VAE ResnetBlock (temporal_ae.py:25-89): spatial ResnetBlock, then a ResBlock(dims=3)
+    with [3,1,1] time convs over all frames, blended as alpha * temporal + (1 - alpha) * spatial."""
+
+    def __init__(self, in_channels, out_channels=None, dtype=None, device=None, video_kernel_size=(3, 1, 1),
+                 alpha=0.0, merge_strategy="learned"):
+        super().__init__(in_channels, out_channels, dtype=dtype, device=device)
+        from .unet import TimeStackResBlock
+        self.time_stack = TimeStackResBlock(self.out_channels, 0, video_kernel_size, skip_t_emb=True, dtype=dtype,
+                                            device=device)
+        self.merge_strategy = merge_strategy
+        if merge_strategy == "fixed":
+            self.register_buffer("mix_factor", torch.tensor([float(alpha)]))
+        else:
+            self.mix_factor = nn.Parameter(torch.tensor([float(alpha)]), requires_grad=False)
+
+    def forward(self, x, temb=None, frames=None):
+        x = super().forward(x)
+        frames = frames or x.shape[0]
+        xt = self.time_stack(x, None, frames)
+        m = self.mix_factor.float()
+        a = (m if self.merge_strategy == "fixed" else torch.sigmoid(m)).to(x.dtype)
+        return a * xt + (1.0 - a) * x
+
+
+class AE3DConv(Conv2d):
+    """Decoder conv_out of the temporal VAE: 2-D conv, then a [3,1,1] time-mixing Conv3d."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, padding=1, video_kernel_size=(3, 1, 1),
+                 dtype=None, device=None):
+        super().__init__(in_channels, out_channels, kernel_size, padding=padding, dtype=dtype, device=device)
+        vks = list(video_kernel_size) if isinstance(video_kernel_size, (list, tuple)) else [video_kernel_size] * 3
+        self.time_mix_conv = Conv3d(out_channels, out_channels, vks, [k // 2 for k in vks], dtype=dtype,
+                                    device=device)
+
+    def forward(self, x, frames=None):
+        x = super().forward(x)
+        return self.time_mix_conv(x, frames or x.shape[0])
+
+
 class Decoder(nn.Module):
     def __init__(self, ch=128, out_ch=3, ch_mult=(1, 2, 4, 4), num_res_blocks=2, z_channels=4,
-                 dtype=None, device=None, **unused):
+                 dtype=None, device=None, video_kernel_size=None, alpha=0.0, merge_strategy="learned",
+                 **unused):
         super().__init__()
         kw = dict(dtype=dtype, device=device)
+        self.video = video_kernel_size is not None   # temporal_ae.VideoDecoder, time_mode "conv-only"
+        if self.video:
+            vk = dict(video_kernel_size=video_kernel_size, alpha=alpha, merge_strategy=merge_strategy)
+            res = lambda a, b: VideoResnetBlock(a, b, **kw, **vk)  # noqa: E731
+        else:
+            res = lambda a, b: ResnetBlock(a, b, **kw)  # noqa: E731
         self.num_resolutions = len(ch_mult)
         self.num_res_blocks = num_res_blocks
         block_in = ch * ch_mult[-1]
         self.conv_in = Conv2d(z_channels, block_in, 3, padding=1, **kw)
         self.mid = _Level()
-        self.mid.block_1 = ResnetBlock(block_in, block_in, **kw)
+        self.mid.block_1 = res(block_in, block_in)
         self.mid.attn_1 = AttnBlock(block_in, **kw)
-        self.mid.block_2 = ResnetBlock(block_in, block_in, **kw)
+        self.mid.block_2 = res(block_in, block_in)
         ups = []
         for i in reversed(range(self.num_resolutions)):
             lvl = _Level()
@@ -166,26 +213,30 @@ class Decoder(nn.Module):
             lvl.attn = nn.ModuleList()
             block_out = ch * ch_mult[i]
             for _ in range(num_res_blocks + 1):
-                lvl.block.append(ResnetBlock(block_in, block_out, **kw))
+                lvl.block.append(res(block_in, block_out))
                 block_in = block_out
             if i != 0:
                 lvl.upsample = Upsample(block_in, **kw)
             ups.insert(0, lvl)
         self.up = nn.ModuleList(ups)
         self.norm_out = _norm(block_in, **kw)
-        self.conv_out = Conv2d(block_in, out_ch, 3, padding=1, **kw)
+        if self.video:
+            self.conv_out = AE3DConv(block_in, out_ch, 3, padding=1, video_kernel_size=video_kernel_size, **kw)
+        else:
+            self.conv_out = Conv2d(block_in, out_ch, 3, padding=1, **kw)
 
-    def forward(self, z):
+    def forward(self, z, frames=None):
+        vk = {"frames": frames or z.shape[0]} if self.video else {}
         h = self.conv_in(z)
-        h = self.mid.block_1(h)
+        h = self.mid.block_1(h, **vk)
         h = self.mid.attn_1(h)
-        h = self.mid.block_2(h)
+        h = self.mid.block_2(h, **vk)
         for i in reversed(range(self.num_resolutions)):
             for blk in self.up[i].block:
-                h = blk(h)
+                h = blk(h, **vk)
             if i != 0:
                 h = self.up[i].upsample(h)
-        return self.conv_out(self.norm_out(h, silu=True))
+        return self.conv_out(self.norm_out(h, silu=True), **vk)
 
 
 class AutoencoderKL(nn.Module):
@@ -194,7 +245,8 @@ class AutoencoderKL(nn.Module):
         ddconfig = dict(ddconfig or {})
         ddconfig.setdefault("z_channels", embed_dim)
         kw = dict(dtype=dtype, device=device)
-        self.encoder = Encoder(**ddconfig, **kw)
+        self.encoder = Encoder(**{k: v for k, v in ddconfig.items()
+                                  if k not in ("video_kernel_size", "alpha", "merge_strategy")}, **kw)
         self.decoder = Decoder(**ddconfig, **kw)
         zc = ddconfig["z_channels"]
         self.quant_conv = Conv2d(2 * zc, 2 * embed_dim, 1, **kw)

@@ -284,6 +284,43 @@ class Stable_Zero123(BASE):
     clip_vision_prefix = "cond_stage_model.model.visual."
     latent_format = latent_formats.SD15
 
+    def get_model(self, sd, prefix="", device=None):
+        w = sd.get("cc_projection.weight") if sd else None
+        shape = tuple(w.shape) if w is not None else (768, 772)
+        return model_base.Stable_Zero123(self, device=device, cc_in=shape[1], cc_out=shape[0])
+
+
+class SVD_img2vid(BASE):
+    """Stable Video Diffusion img2vid (supported_models.py:267-290)."""
+    unet_config = {"model_channels": 320, "in_channels": 8, "use_linear_in_transformer": True,
+                   "transformer_depth": [1, 1, 1, 1, 1, 1, 0, 0], "context_dim": 1024, "adm_in_channels": 768,
+                   "use_temporal_attention": True, "use_temporal_resblock": True}
+    unet_extra_config = {"num_heads": -1, "num_head_channels": 64}
+    clip_vision_prefix = "conditioner.embedders.0.open_clip.model.visual."
+    latent_format = latent_formats.SD15
+    sampling_settings = {"sigma_max": 700.0, "sigma_min": 0.002}
+
+    def model_type(self, sd, prefix=""):
+        return model_base.ModelType.V_PREDICTION_EDM
+
+    def get_model(self, sd, prefix="", device=None):
+        return model_base.SVD_img2vid(self, device=device)
+
+
+class SV3D_u(SVD_img2vid):
+    unet_config = dict(SVD_img2vid.unet_config, adm_in_channels=256)
+    vae_key_prefix = ["conditioner.embedders.1.encoder."]
+
+    def get_model(self, sd, prefix="", device=None):
+        return model_base.SV3D_u(self, device=device)
+
+
+class SV3D_p(SV3D_u):
+    unet_config = dict(SVD_img2vid.unet_config, adm_in_channels=1280)
+
+    def get_model(self, sd, prefix="", device=None):
+        return model_base.SV3D_p(self, device=device)
+
 
 class Stable_Cascade_C(BASE):
     unet_config = {"stable_cascade_stage": "c"}
@@ -336,4 +373,4 @@ class Stable_Cascade_B(Stable_Cascade_C):
 
 MODELS = [Stable_Zero123, SD15_instructpix2pix, SD15, SD20, SD21UnclipL, SD21UnclipH, SDXL_instructpix2pix,
           SDXLRefiner, SDXL, SSD1B, KOALA_700M, KOALA_1B, Segmind_Vega, SD_X4Upscaler, Stable_Cascade_C,
-          Stable_Cascade_B]
+          Stable_Cascade_B, SV3D_u, SV3D_p, SVD_img2vid]

@@ -313,3 +313,96 @@ class SD_X4Upscaler(BaseModel):
         if ca is not None:
             out["c_crossattn"] = C.CONDCrossAttn(ca)
         return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Video / novel-view families (model_base.py:336-442): SVD img2vid, SV3D (u / p), Stable Zero123
+# ------------------------------------------------------------------------------------------------
+def _concat_latent(kwargs, noise):
+    from ..utils.image import resize_to_batch_size
+    latent_image = kwargs.get("concat_latent_image")
+    if latent_image is None:
+        latent_image = torch.zeros_like(noise)
+    if latent_image.shape[1:] != noise.shape[1:]:
+        latent_image = common_upscale(latent_image, noise.shape[-1], noise.shape[-2], "bilinear", "center")
+    return resize_to_batch_size(latent_image, noise.shape[0])
+
+
+class SVD_img2vid(BaseModel):
+    """Video UNet (VideoResBlock / SpatialVideoTransformer) conditioned on the CLIP-vision embedding
+    (c_crossattn), the start-frame latent (c_concat) and fps / motion bucket / augmentation ADM."""
+
+    def __init__(self, model_config, model_type=ModelType.V_PREDICTION_EDM, device=None):
+        super().__init__(model_config, model_type, device=device)
+
+    def encode_adm(self, **kwargs):
+        vals = [kwargs.get("fps", 6) - 1, kwargs.get("motion_bucket_id", 127), kwargs.get("augmentation_level", 0)]
+        return timestep_embed_256(vals).flatten().unsqueeze(0)
+
+    def extra_conds(self, **kwargs):
+        out = {}
+        adm = self.encode_adm(**kwargs)
+        if adm is not None:
+            out["y"] = C.CONDRegular(adm)
+        noise = kwargs.get("noise")
+        out["c_concat"] = C.CONDNoiseShape(_concat_latent(kwargs, noise))
+        ca = kwargs.get("cross_attn")
+        if ca is not None:
+            out["c_crossattn"] = C.CONDCrossAttn(ca)
+        if "time_conditioning" in kwargs:
+            out["time_context"] = C.CONDCrossAttn(kwargs["time_conditioning"])
+        out["num_video_frames"] = C.CONDConstant(noise.shape[0])
+        return out
+
+
+class SV3D_u(SVD_img2vid):
+    def encode_adm(self, **kwargs):
+        return timestep_embed_256([kwargs.get("augmentation_level", 0)]).flatten().unsqueeze(0)
+
+
+class SV3D_p(SVD_img2vid):
+    def encode_adm(self, **kwargs):
+        from ..utils.image import resize_to_batch_size
+        noise = kwargs.get("noise")
+        aug = timestep_embed_256([kwargs.get("augmentation_level", 0)])
+        elev = torch.deg2rad(torch.fmod(torch.tensor([90.0 - float(v) for v in _as_list(kwargs.get("elevation", 0))]),
+                                        360.0))
+        azim = torch.deg2rad(torch.fmod(torch.tensor([float(v) for v in _as_list(kwargs.get("azimuth", 0))]), 360.0))
+        parts = [aug, ops.core.timestep_embedding(elev, 512), ops.core.timestep_embedding(azim, 512)]
+        parts = [resize_to_batch_size(p, noise.shape[0]) for p in parts]
+        return torch.cat(parts, dim=1)
+
+
+def _as_list(v):
+    if isinstance(v, torch.Tensor):
+        return v.flatten().tolist()
+    return list(v) if isinstance(v, (list, tuple)) else [v]
+
+
+class Stable_Zero123(BaseModel):
+    """SD1.5-shaped UNet with 8 input channels: noise ‖ start-image latent, and a ``cc_projection``
+    (768+4 -> 768) applied to the CLIP-vision + camera embedding (model_base.py:414-442)."""
+
+    def __init__(self, model_config, model_type=ModelType.EPS, device=None, cc_in=772, cc_out=768):
+        super().__init__(model_config, model_type, device=device)
+        from ..models.layers import Linear
+        self.cc_projection = Linear(cc_in, cc_out, dtype=self.get_dtype(), device=device)
+
+    def load_model_weights(self, sd, unet_prefix=""):
+        for name in ("weight", "bias"):
+            k = f"cc_projection.{name}"
+            if k in sd:
+                getattr(self.cc_projection, name).data = sd.pop(k).to(self.get_dtype())
+        return super().load_model_weights(sd, unet_prefix)
+
+    def extra_conds(self, **kwargs):
+        out = {}
+        noise = kwargs.get("noise")
+        out["c_concat"] = C.CONDNoiseShape(_concat_latent(kwargs, noise))
+        ca = kwargs.get("cross_attn")
+        if ca is not None:
+            if ca.shape[-1] != 768:
+                w = self.cc_projection.weight
+                ca = self.cc_projection(ca.to(device=w.device, dtype=w.dtype))
+            out["c_crossattn"] = C.CONDCrossAttn(ca)
+        return out

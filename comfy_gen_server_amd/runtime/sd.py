@@ -166,6 +166,10 @@ class VAE:
                     if "decoder.conv_in.weight" in sd:
                         ddconfig["z_channels"] = sd["decoder.conv_in.weight"].shape[1]
                         self.latent_channels = ddconfig["z_channels"]
+                    if "decoder.mid.block_1.mix_factor" in sd:
+                        # SVD temporal decoder (sd.py:175-182): time-mixing ResBlocks + AE3DConv out
+                        ddconfig.update(video_kernel_size=[3, 1, 1], alpha=0.0)
+                        self.kind = "video"
                 self.first_stage_model = V.AutoencoderKL(embed_dim=ddconfig["z_channels"], ddconfig=ddconfig,
                                                          device=torch.device("meta"))
                 self.first_stage_model.to_empty(device="cpu")
@@ -193,9 +197,11 @@ class VAE:
     def decode(self, samples_in):
         dm.load_model_gpu(self.patcher)
         out = []
+        # the temporal decoder mixes across the frames of a decode call: decode a clip in one call
+        step = samples_in.shape[0] if self.kind == "video" else self.batch
         with torch.inference_mode():
-            for i in range(0, samples_in.shape[0], self.batch):
-                s = self._mf(samples_in[i:i + self.batch])
+            for i in range(0, samples_in.shape[0], max(1, step)):
+                s = self._mf(samples_in[i:i + max(1, step)])
                 img = self.first_stage_model.decode(s)
                 out.append(self.process_output(img.float()).to(self.output_device))
         pixels = torch.cat(out, 0)

@@ -1,0 +1,107 @@
+"""Numerical parity against the reference implementation itself (its Python sources under
+/root/reference, imported read-only in a subprocess with a CPU-only argv, SURVEY Appendix B recipe).
+
+Same random weights are loaded into both implementations (fp32, CPU) and the outputs compared:
+SDXL-style UNet, SVD video UNet (VideoResBlock / SpatialVideoTransformer / AlphaBlender incl. the
+image-only indicator), KL-VAE decoder and the SVD temporal VAE decoder. Skipped where the reference
+tree is not mounted (e.g. the GPU box)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "comfy")), reason="reference tree not mounted")
+
+_SCRIPT = r'''
+import sys, types
+sys.path.insert(0, REF); sys.argv = ["x", "--cpu"]
+import comfy.options; comfy.options.enable_args_parsing()
+sys.modules.setdefault("torchsde", types.ModuleType("torchsde"))
+import torch, comfy.ops
+sys.path.insert(0, ROOT)
+from comfy_gen_server_amd.models.layers import init_random_
+torch.manual_seed(0)
+
+def close(a, b, tol=2e-4):
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * max(1.0, scale), (err, scale)
+    return err
+
+def load(ref, ours):
+    sd = ours.state_dict()
+    m, u = ref.load_state_dict(sd, strict=False)
+    assert not m and not u, (m[:5], u[:5])
+
+which = sys.argv_which
+if which == "unet":
+    from comfy.ldm.modules.diffusionmodules.openaimodel import UNetModel as R
+    from comfy_gen_server_amd.models.unet import UNetModel
+    cfg = dict(in_channels=4, model_channels=64, out_channels=4, num_res_blocks=[1, 1, 1], channel_mult=[1, 2, 2],
+               transformer_depth=[0, 1, 2], transformer_depth_output=[0, 0, 1, 1, 2, 2], transformer_depth_middle=1,
+               num_heads=-1, num_head_channels=32, use_linear_in_transformer=True, context_dim=48,
+               num_classes="sequential", adm_in_channels=40)
+    m = UNetModel(**cfg); init_random_(m, seed=1)
+    r = R(use_spatial_transformer=True, image_size=32, legacy=False, operations=comfy.ops.disable_weight_init, **cfg)
+    load(r, m)
+    x = torch.randn(2, 4, 16, 16); t = torch.tensor([900., 10.]); c = torch.randn(2, 9, 48); y = torch.randn(2, 40)
+    with torch.no_grad():
+        print("unet", close(m(x, t, context=c, y=y), r(x, t, context=c, y=y, transformer_options={})))
+elif which == "svd":
+    from comfy.ldm.modules.diffusionmodules.openaimodel import UNetModel as R
+    from comfy_gen_server_amd.models.unet import UNetModel
+    cfg = dict(in_channels=8, model_channels=32, out_channels=4, num_res_blocks=[1, 1], channel_mult=[1, 2],
+               transformer_depth=[1, 1], transformer_depth_output=[1, 1, 1, 1], transformer_depth_middle=1,
+               num_heads=-1, num_head_channels=16, use_linear_in_transformer=True, context_dim=64,
+               num_classes="sequential", adm_in_channels=24, use_temporal_resblock=True, use_temporal_attention=True,
+               extra_ff_mix_layer=True, use_spatial_context=True, merge_strategy="learned_with_images",
+               merge_factor=0.0, video_kernel_size=[3, 1, 1])
+    m = UNetModel(**cfg); init_random_(m, seed=5)
+    for k, v in m.state_dict().items():
+        if k.endswith("mix_factor"):
+            v.fill_(0.3)
+    r = R(use_spatial_transformer=True, image_size=32, legacy=False, operations=comfy.ops.disable_weight_init, **cfg)
+    load(r, m)
+    x = torch.randn(10, 8, 16, 16); t = torch.rand(10) * 900; c = torch.randn(10, 1, 64); y = torch.randn(10, 24)
+    ind = torch.zeros(2, 5); ind[:, 0] = 1
+    with torch.no_grad():
+        a = close(m(x, t, context=c, y=y, num_video_frames=5),
+                  r(x, t, context=c, y=y, num_video_frames=5, transformer_options={}))
+        b = close(m(x, t, context=c, y=y, num_video_frames=5, image_only_indicator=ind),
+                  r(x, t, context=c, y=y, num_video_frames=5, image_only_indicator=ind, transformer_options={}))
+    print("svd", a, b)
+elif which in ("vae", "vae_video"):
+    from comfy_gen_server_amd.models.vae import Decoder
+    video = which == "vae_video"
+    kw = dict(ch=32, out_ch=3, ch_mult=[1, 2], num_res_blocks=1, z_channels=4)
+    if video:
+        from comfy.ldm.modules.temporal_ae import VideoDecoder as R
+        r = R(attn_resolutions=[], in_channels=3, resolution=64, video_kernel_size=[3, 1, 1], alpha=0.0, **kw)
+        m = Decoder(video_kernel_size=[3, 1, 1], alpha=0.0, **kw)
+    else:
+        from comfy.ldm.modules.diffusionmodules.model import Decoder as R
+        r = R(attn_resolutions=[], in_channels=3, resolution=64, **kw)
+        m = Decoder(**kw)
+    init_random_(m, seed=2)
+    for k, v in m.state_dict().items():
+        if k.endswith("mix_factor"):
+            v.fill_(-0.4)
+    load(r, m)
+    z = torch.randn(6, 4, 8, 8)
+    with torch.no_grad():
+        print(which, close(m(z), r(z)))
+'''
+
+
+@pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video"])
+def test_matches_reference(which):
+    code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
+    env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd="/tmp", env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert which in r.stdout
