@@ -166,7 +166,7 @@ class VideoResnetBlock(ResnetBlock):
         x = super().forward(x)
         frames = frames or x.shape[0]
         xt = self.time_stack(x, None, frames)
-        m = self.mix_factor.float()
+        m = self.mix_factor.to(device=x.device, dtype=torch.float32)
         a = (m if self.merge_strategy == "fixed" else torch.sigmoid(m)).to(x.dtype)
         return a * xt + (1.0 - a) * x
 
