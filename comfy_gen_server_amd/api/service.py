@@ -14,10 +14,12 @@ mapping):
   POST /api/v1/comfy/SyncLocalFiles    -> LocalFiles (added/updated/removed since last call, blake3)
   GET  /api/v1/health/Check, /api/v1/health/Watch (stream)
 
-JobSnapshot.status: QUEUED=1 EXECUTING=2 COMPLETED=3 ERROR=4 ABORTED=5; outputs carry
+JobSnapshot.status uses the proto enum values (QUEUED=0 EXECUTING=1 COMPLETED=2 ERROR=3 ABORTED=4;
+-1 = unknown job in the JSON form, NOT_FOUND over gRPC); outputs carry
 WorkflowFile{blake3_hash, mime_type, reference{url, is_temp}}; metrics{queue_seconds,
 execution_seconds} are filled (the reference never produces them). ``output_config.webhook_url``
-gets a POST of the final snapshot.
+gets a POST of the final snapshot. The same contract over real gRPC (protobuf wire format) is
+``grpc_service.py``; both share the job model and the helpers below.
 """
 from __future__ import annotations
 
@@ -36,7 +38,7 @@ from ..graph.validation import validate_prompt
 from ..utils import folder_paths
 from ..utils.hashing import file_digest
 
-STATUS = {"UNSPECIFIED": 0, "QUEUED": 1, "EXECUTING": 2, "COMPLETED": 3, "ERROR": 4, "ABORTED": 5}
+STATUS = {"UNSPECIFIED": -1, "QUEUED": 0, "EXECUTING": 1, "COMPLETED": 2, "ERROR": 3, "ABORTED": 4}
 
 
 class JobTracker:
@@ -84,30 +86,107 @@ class JobTracker:
         return snap
 
 
+def _norm_input(v):
+    # google.protobuf.Struct carries every number as a double: restore integral link slots
+    # ([node_id, 0.0] -> [node_id, 0]); INT widget values are coerced by the validator.
+    if isinstance(v, list) and len(v) == 2 and isinstance(v[0], str) and isinstance(v[1], float) and v[1].is_integer():
+        return [v[0], int(v[1])]
+    return v
+
+
 def _workflow_to_prompt(req):
     wf = req.get("workflow") or {}
-    prompt = {nid: {"class_type": step["class_type"], "inputs": step.get("inputs", {})} for nid, step in wf.items()}
+    prompt = {nid: {"class_type": step["class_type"],
+                    "inputs": {k: _norm_input(v) for k, v in (step.get("inputs") or {}).items()}}
+              for nid, step in wf.items()}
     return prompt
 
 
+def submit_request(server, tracker, req):
+    """Validate + enqueue a ComfyRequest (dict form). Returns (job_id, None) or (None, error dict)."""
+    prompt = _workflow_to_prompt(req)
+    valid = validate_prompt(prompt)
+    if not valid[0]:
+        return None, {"error": valid[1], "node_errors": valid[3]}
+    job_id = str(uuid.uuid4())
+    number = server.number
+    server.number += 1
+    oc = req.get("output_config") or {}
+    tracker.jobs[job_id] = {"request_id": req.get("request_id"), "submitted": time.time(),
+                            "webhook_url": oc.get("webhook_url"), "write_to_graph_id": oc.get("write_to_graph_id")}
+    server.prompt_queue.put((number, job_id, prompt, {}, valid[2]))
+    return job_id, None
+
+
+def node_definitions(extension_ids=None):
+    """NodeDefs.defs: every registered node (or those of the listed extension modules)."""
+    defs = {}
+    for name in registry.NODE_CLASS_MAPPINGS:
+        cls = registry.NODE_CLASS_MAPPINGS[name]
+        if extension_ids and getattr(cls, "RELATIVE_PYTHON_MODULE", cls.__module__) not in extension_ids:
+            continue
+        try:
+            info = registry.node_info(name)
+        except Exception:
+            continue
+        inputs = []
+        for sect in ("required", "optional"):
+            for label, spec in info["input"].get(sect, {}).items():
+                et = spec[0] if isinstance(spec[0], str) else "COMBO"
+                sp = dict(spec[1]) if len(spec) > 1 and isinstance(spec[1], dict) else {}
+                if et == "COMBO":
+                    sp["options"] = list(spec[0])
+                sp["optional"] = sect == "optional"
+                inputs.append({"label": label, "edge_type": et, "spec": json.loads(json.dumps(sp, default=str))})
+        outputs = [{"label": n, "edge_type": t} for n, t in zip(info["output_name"], info["output"])]
+        defs[name] = {"display_name": info["display_name"], "description": info["description"],
+                      "category": info["category"], "inputs": inputs, "outputs": outputs,
+                      "output_node": info["output_node"]}
+    return defs
+
+
+def model_catalog(base_family=None):
+    models = {}
+    for kind in folder_paths.folder_names_and_paths:
+        if kind in ("custom_nodes", "configs") or (base_family and kind not in base_family):
+            continue
+        try:
+            files = folder_paths.get_filename_list(kind)
+        except Exception:
+            files = []
+        models[kind] = {"info": [{"display_name": f} for f in files]}
+    return models
+
+
+def local_files_delta(tracker):
+    cur = {}
+    for kind in ("input", "output", "temp"):
+        d = folder_paths.get_directory_by_type(kind)
+        if not d or not os.path.isdir(d):
+            continue
+        for root, _, files in os.walk(d):
+            for f in files:
+                p = os.path.join(root, f)
+                st = os.stat(p)
+                cur[p] = (st.st_mtime, st.st_size, kind)
+    prev = tracker._local_files
+
+    def entry(p, meta):
+        return {"name": os.path.basename(p), "path": p, "size": meta[1],
+                "mime_type": mimetypes.guess_type(p)[0] or "application/octet-stream"}
+    added = [entry(p, m) for p, m in cur.items() if p not in prev]
+    updated = [entry(p, m) for p, m in cur.items() if p in prev and prev[p][:2] != m[:2]]
+    removed = [entry(p, m) for p, m in prev.items() if p not in cur]
+    tracker._local_files = cur
+    return {"added": added, "updated": updated, "removed": removed}
+
+
 def add_service_routes(routes, server):
-    tracker = JobTracker(server)
+    tracker = getattr(server, "job_tracker", None) or JobTracker(server)
     server.job_tracker = tracker
 
     def submit(req):
-        prompt = _workflow_to_prompt(req)
-        valid = validate_prompt(prompt)
-        if not valid[0]:
-            return None, {"error": valid[1], "node_errors": valid[3]}
-        job_id = str(uuid.uuid4())
-        number = server.number
-        server.number += 1
-        extra = {}
-        oc = req.get("output_config") or {}
-        tracker.jobs[job_id] = {"request_id": req.get("request_id"), "submitted": time.time(),
-                                "webhook_url": oc.get("webhook_url"), "write_to_graph_id": oc.get("write_to_graph_id")}
-        server.prompt_queue.put((number, job_id, prompt, extra, valid[2]))
-        return job_id, None
+        return submit_request(server, tracker, req)
 
     @routes.post("/api/v1/comfy/Run")
     async def run(request):
@@ -145,62 +224,23 @@ def add_service_routes(routes, server):
 
     @routes.post("/api/v1/comfy/GetNodeDefinitions")
     async def get_node_defs(request):
-        defs = {}
-        for name in registry.NODE_CLASS_MAPPINGS:
-            try:
-                info = registry.node_info(name)
-            except Exception:
-                continue
-            inputs = []
-            for sect in ("required", "optional"):
-                for label, spec in info["input"].get(sect, {}).items():
-                    et = spec[0] if isinstance(spec[0], str) else "COMBO"
-                    sp = dict(spec[1]) if len(spec) > 1 and isinstance(spec[1], dict) else {}
-                    if et == "COMBO":
-                        sp["options"] = list(spec[0])
-                    sp["optional"] = sect == "optional"
-                    inputs.append({"label": label, "edge_type": et, "spec": sp})
-            outputs = [{"label": n, "edge_type": t} for n, t in zip(info["output_name"], info["output"])]
-            defs[name] = {"display_name": info["display_name"], "description": info["description"],
-                          "category": info["category"], "inputs": inputs, "outputs": outputs,
-                          "output_node": info["output_node"]}
-        return web.json_response({"defs": defs})
+        try:
+            req = await request.json()
+        except Exception:
+            req = {}
+        return web.json_response({"defs": node_definitions(req.get("extension_ids"))})
 
     @routes.post("/api/v1/comfy/GetModelCatalog")
     async def get_model_catalog(request):
-        models = {}
-        for kind in folder_paths.folder_names_and_paths:
-            if kind in ("custom_nodes", "configs"):
-                continue
-            try:
-                files = folder_paths.get_filename_list(kind)
-            except Exception:
-                files = []
-            models[kind] = {"info": [{"display_name": f} for f in files]}
-        return web.json_response({"models": models})
+        try:
+            req = await request.json()
+        except Exception:
+            req = {}
+        return web.json_response({"models": model_catalog(req.get("base_family"))})
 
     @routes.post("/api/v1/comfy/SyncLocalFiles")
     async def sync_local_files(request):
-        cur = {}
-        for kind in ("input", "output", "temp"):
-            d = folder_paths.get_directory_by_type(kind)
-            if not d or not os.path.isdir(d):
-                continue
-            for root, _, files in os.walk(d):
-                for f in files:
-                    p = os.path.join(root, f)
-                    st = os.stat(p)
-                    cur[p] = (st.st_mtime, st.st_size, kind)
-        prev = tracker._local_files
-
-        def entry(p, meta):
-            return {"name": os.path.basename(p), "path": p, "size": meta[1],
-                    "mime_type": mimetypes.guess_type(p)[0] or "application/octet-stream"}
-        added = [entry(p, m) for p, m in cur.items() if p not in prev]
-        updated = [entry(p, m) for p, m in cur.items() if p in prev and prev[p][:2] != m[:2]]
-        removed = [entry(p, m) for p, m in prev.items() if p not in cur]
-        tracker._local_files = cur
-        return web.json_response({"added": added, "updated": updated, "removed": removed})
+        return web.json_response(local_files_delta(tracker))
 
     @routes.get("/api/v1/health/Check")
     async def health_check(request):

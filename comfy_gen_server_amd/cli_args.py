@@ -44,6 +44,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--port", type=int, default=8188)
     p.add_argument("--enable-cors-header", type=str, default=None, metavar="ORIGIN", nargs="?", const="*")
     p.add_argument("--max-upload-size", type=float, default=100)
+    p.add_argument("--grpc-port", type=int, default=None,
+                   help="also serve comfy_request.v1.Comfy + grpc.health.v1.Health over gRPC on this port")
     # paths
     p.add_argument("--extra-model-paths-config", type=str, default=None, metavar="PATH", nargs="+", action="append")
     p.add_argument("--output-directory", type=str, default=None)

@@ -181,6 +181,10 @@ def main(argv=None):
     asyncio.set_event_loop(loop)
     server, q = build_server(args, loop)
     threading.Thread(target=prompt_worker, daemon=True, args=(q, server)).start()
+    grpc_srv = None
+    if args.grpc_port is not None:
+        from .api.grpc_service import start_grpc_server
+        grpc_srv, _ = start_grpc_server(server, args.grpc_port, host=args.listen or "0.0.0.0")
     if args.quick_test_for_ci:
         return 0
     call_on_start = None
@@ -193,6 +197,8 @@ def main(argv=None):
                                     verbose=not args.dont_print_server, call_on_start=call_on_start))
     except KeyboardInterrupt:
         logging.info("Stopped server")
+    if grpc_srv is not None:
+        grpc_srv.stop(grace=1.0)
     cleanup_temp()
     return 0
 
