@@ -531,6 +531,170 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wide-head path (K22): the KL-VAE mid-block attention, ONE head of D = 512 over H*W tokens
+// (16 k tokens at 1024², comfy/ldm/modules/diffusionmodules/model.py:227-292). A 32-query O^T
+// accumulator for D = 512 does not fit one wave (256 accumulator registers), so the head dim is
+// split over the 4 waves of a workgroup: wave w owns d in [128w, 128w+128) of Q, of the output
+// and of the V^T operand. Per 32-key tile each wave computes a PARTIAL S^T = K Q^T over its d
+// slice (8 MFMA 32x32x16), the 4 partials are summed through LDS (every wave ends up with the
+// full, identical scores), the online softmax runs redundantly in the 4 waves, and each wave does
+// O^T[its 128 d] += V^T P^T (8 MFMA). K/V tiles (32 keys x 512 d) are register-prefetched one tile
+// ahead into a single LDS buffer; K rows use a chunk ^ (key & 15) swizzle (conflict-free
+// ds_read_b128 A fragments), V rows chunk ^ ((key & 3) << 2) (conflict-free ds_read_b64_tr_b16).
+constexpr int WD_D = 512;
+constexpr int WD_KT = 32;                      // keys per tile
+constexpr int WD_CH = WD_D / 8;                // 16-B chunks per row
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_wide_kernel(
+    const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
+    int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
+    long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
+    float c, int nqb) {
+  __shared__ __attribute__((aligned(16))) u16 Ks[WD_KT * WD_D];
+  __shared__ __attribute__((aligned(16))) u16 Vs[WD_KT * WD_D];
+  __shared__ __attribute__((aligned(16))) float Sx[4][64][16];
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = logical % nqb;
+  const int bh = logical / nqb;
+  const int b = bh / H, h = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hf = lane >> 5, i16 = lane & 15;
+  const int d0 = wave * 128;
+
+  const u16* qbase = qp + b * qsb + h * qsh;
+  const u16* kbase = kp + b * ksb + h * ksh;
+  const u16* vbase = vp + b * vsb + h * vsh;
+  u16* obase = op + b * osb + h * osh;
+
+  const int q_row = qb * 32 + l32;
+  const bool q_ok = q_row < Sq;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    s16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q_ok) t = *reinterpret_cast<const s16x8*>(qbase + (long long)q_row * qss + d0 + ks * 16 + 8 * hf);
+    qf[ks] = __builtin_bit_cast(bf16x8, t);
+  }
+
+  const int ntiles = (Sk + WD_KT - 1) / WD_KT;
+  s16x8 kr[8], vr[8];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int idx = it * 256 + tid;
+      const int key = idx >> 6, ch = idx & 63;
+      const int gk = t * WD_KT + key;
+      s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      kr[it] = gk < Sk ? *reinterpret_cast<const s16x8*>(kbase + (long long)gk * kss + ch * 8) : z;
+      vr[it] = gk < Sk ? *reinterpret_cast<const s16x8*>(vbase + (long long)gk * vss + ch * 8) : z;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int idx = it * 256 + tid;
+      const int key = idx >> 6, ch = idx & 63;
+      *reinterpret_cast<s16x8*>(&Ks[key * WD_D + 8 * (ch ^ (key & 15))]) = kr[it];
+      *reinterpret_cast<s16x8*>(&Vs[key * WD_D + 8 * (ch ^ ((key & 3) << 2))]) = vr[it];
+    }
+  };
+
+  f32x16 ot[4] = {f32x16{}, f32x16{}, f32x16{}, f32x16{}};
+  float m_run = -INFINITY, l_run = 0.f;
+  gload(0);
+  lstore();
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    // partial S^T over this wave's 128-d slice
+    f32x16 sp = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int ch = 16 * wave + 2 * ks + hf;
+      s16x8 a = *reinterpret_cast<const s16x8*>(&Ks[l32 * WD_D + 8 * (ch ^ (l32 & 15))]);
+      sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], sp, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4)
+      *reinterpret_cast<float4_t*>(&Sx[wave][lane][4 * r4]) = float4_t{sp[4 * r4], sp[4 * r4 + 1], sp[4 * r4 + 2],
+                                                                      sp[4 * r4 + 3]};
+    __syncthreads();
+    f32x16 s = f32x16{};
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        float4_t v = *reinterpret_cast<const float4_t*>(&Sx[w][lane][4 * r4]);
+        s[4 * r4] += v[0]; s[4 * r4 + 1] += v[1]; s[4 * r4 + 2] += v[2]; s[4 * r4 + 3] += v[3];
+      }
+    // online softmax (identical in the 4 waves)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = t * WD_KT + (r & 3) + 8 * (r >> 2) + 4 * hf;
+      s[r] = key < Sk ? s[r] : -INFINITY;
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = af_xmax(mx) * c;
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+    m_run = m_new;
+    float ps = 0.f;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], c, -m_use));
+      ps += p;
+      pf[r >> 3][r & 7] = (__bf16)p;
+    }
+    l_run = l_run * alpha + ps;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ot[dt][r] *= alpha;
+    // O^T[d slice] += V^T P^T
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int row0 = 16 * st + 4 * hf + (i16 >> 2);
+      const int r1 = row0 + 8;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = d0 + dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+        const int ch = col >> 3, half = (col >> 2) & 1;
+        const int o0 = row0 * WD_D + 8 * (ch ^ ((row0 & 3) << 2)) + 4 * half;
+        const int o1 = r1 * WD_D + 8 * (ch ^ ((r1 & 3) << 2)) + 4 * half;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o0));
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o1));
+        bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ot[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st], ot[dt], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // every wave is done with Ks / Vs / Sx of tile t
+    if (t + 1 < ntiles) {
+      lstore();
+      __syncthreads();
+    }
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (q_ok) {
+    u16* orow = obase + (long long)q_row * oss + d0;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        s16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(ot[dt][4 * r4 + j] * inv);
+        *reinterpret_cast<s16x4*>(orow + dt * 32 + 8 * r4 + 4 * hf) = w;
+      }
+  }
+}
+
 static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel, 3 short-KV kernel
 CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
 
@@ -564,6 +728,16 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
     return (int)hipGetLastError();
   }
   if (g_attn_variant == 3) return (int)hipErrorInvalidValue;
+  if (D == WD_D) {
+    if (key_mask || causal || !al16 || Sk <= 0) return (int)hipErrorInvalidValue;
+    const int nqb4 = (Sq + 31) / 32;
+    const long long nwg4 = (long long)nqb4 * B * H;
+    if (nwg4 > 0x7fffffff) return (int)hipErrorInvalidValue;
+    attn_fwd_wide_kernel<<<dim3((unsigned)nwg4), 256, 0, stream>>>(
+        (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
+        osb, oss, osh, sl2, nqb4);
+    return (int)hipGetLastError();
+  }
   if (D == 64 && !key_mask && !causal && al16 && g_attn_variant != 1 && Sk > 0) {
     int nqb2 = (Sq + 255) / 256;
     long long nwg2 = (long long)nqb2 * B * H;

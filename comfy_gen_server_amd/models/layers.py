@@ -100,7 +100,8 @@ class Conv2d(nn.Module, DerivedMixin):
             # narrow-input convs (UNet conv_in: 4 or 8 latent channels, 3-channel image stems):
             # zero-pad Cin to 32 so the MFMA implicit-GEMM kernel runs them too (no library conv
             # on the hot path, and the forward stays hipGraph-capturable).
-            cp = (self.in_channels + 31) // 32 * 32
+            q = 32 if self.out_channels % 8 == 0 else 64      # kernel legality: Cout % 8 or Cin % 64
+            cp = (self.in_channels + q - 1) // q * q
             pad = cp - self.in_channels
             w = self._derived_get("w_pad", lambda: torch.nn.functional.pad(self.weight, (0, 0, 0, 0, 0, pad)))
             wn = self._derived_get("w_nhwc_pad", lambda: w.permute(0, 2, 3, 1).contiguous())

@@ -208,7 +208,8 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     Sk = k.shape[1]
     D = HD // heads
     be = backend_for("attention", q, "cgs_flash_attn_fwd")
-    if (be == "hip" and mask is None and D in _FLASH_HEAD_DIMS and q.dtype == torch.bfloat16
+    wide_ok = D == 512 and not causal and key_padding is None
+    if (be == "hip" and mask is None and (D in _FLASH_HEAD_DIMS or wide_ok) and q.dtype == torch.bfloat16
             and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1):
         kp = None
         if key_padding is not None:

@@ -33,6 +33,8 @@ def _time(fn, iters=20, warm=3):
 
 
 def main(quick=False, attn_only=False, gemm_only=False):
+    import os
+    os.environ["CGS_AUTOTUNE"] = "0"      # explicit variants below; the per-shape tuner would override them
     from comfy_gen_server_amd import ops
     from comfy_gen_server_amd.ops import core
     from comfy_gen_server_amd.ops.dispatch import set_backend_override
@@ -117,7 +119,8 @@ def main(quick=False, attn_only=False, gemm_only=False):
         t_lib = _time(lambda: F.layer_norm(x, (C,), wt, bt))
         res["layernorm"].append(dict(rows=rows, C=C, hip_ms=t_hip, lib_ms=t_lib, hip_GBps=nbytes / t_hip / 1e6,
                                      lib_GBps=nbytes / t_lib / 1e6))
-    for N, Ci, H, W, Co in [(B, 320, 128, 128, 320), (B, 640, 64, 64, 640), (B, 1280, 32, 32, 1280),
+    for N, Ci, H, W, Co in [(B, 320, 128, 128, 320), (B, 640, 128, 128, 320), (B, 960, 128, 128, 320),
+                            (B, 640, 64, 64, 640), (B, 1280, 32, 32, 1280),
                             (B, 1920, 32, 32, 1280), (1, 256, 512, 512, 256), (1, 128, 1024, 1024, 128)]:
         x = torch.randn(N, Ci, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         wt = (torch.randn(Co, Ci, 3, 3, device=dev) / math.sqrt(Ci * 9)).to(torch.bfloat16)
@@ -129,7 +132,7 @@ def main(quick=False, attn_only=False, gemm_only=False):
             wn = wt.permute(0, 2, 3, 1).contiguous()
             set_backend_override("conv", "hip")
             lib = ops.dispatch._native.load_kernels()
-            for var in (2, 4, 5, 6):
+            for var in (2, 3, 4, 5, 6):
                 lib.cgs_conv_set_variant(var)
                 for g in (8,):
                     lib.cgs_conv_set_tile_group(g)
