@@ -2,11 +2,11 @@
 model_loading.py:24-99`` dispatch, ``architecture/RRDB.py`` and ``architecture/SRVGG.py``).
 
 Supported here: ESRGAN / Real-ESRGAN (RRDBNet, old and new key layouts, x1/x2 pixel-unshuffle
-variants, scale 1-8) and Real-ESRGAN compact (SRVGGNetCompact). Every 3x3 conv is a
+variants, scale 1-8), Real-ESRGAN compact (SRVGGNetCompact), SPSR and Swift-SRGAN. Every 3x3 conv is a
 ``layers.Conv2d`` so on the device it runs as the NHWC implicit-GEMM MFMA kernel (bias fused);
 the state dict is re-keyed to the old-arch ``model.N`` layout the reference uses, so any file
 that loads there loads here. Other chaiNNer architectures (SwinIR/Swin2SR/HAT/DAT, OmniSR, SCUNet,
-SPSR, Swift-SRGAN, LaMa, GFPGAN/CodeFormer/RestoreFormer) are detected by the same key probes and
+LaMa, GFPGAN/CodeFormer/RestoreFormer) are detected by the same key probes and
 rejected with ``UnsupportedModel`` naming the architecture.
 """
 from __future__ import annotations
@@ -201,8 +201,169 @@ class SRVGGNetCompact(nn.Module):
         return out + F.interpolate(x, scale_factor=self.scale, mode="nearest")
 
 
+class _GradMag(nn.Module):
+    """Per-channel gradient magnitude with [0,-1,0;0,0,0;0,1,0] / [0,0,0;-1,0,1;0,0,0] kernels
+    (SPSR's gradient branch input; keys ``get_g_nopadding.weight_{h,v}``)."""
+
+    def __init__(self):
+        super().__init__()
+        self.weight_h = nn.Parameter(torch.tensor([[[[0., 0., 0.], [-1., 0., 1.], [0., 0., 0.]]]]), requires_grad=False)
+        self.weight_v = nn.Parameter(torch.tensor([[[[0., -1., 0.], [0., 0., 0.], [0., 1., 0.]]]]), requires_grad=False)
+
+    def forward(self, x):
+        c = x.shape[1]
+        xf = x.float()
+        gv = F.conv2d(xf, self.weight_v.float().expand(c, 1, 3, 3), padding=1, groups=c)
+        gh = F.conv2d(xf, self.weight_h.float().expand(c, 1, 3, 3), padding=1, groups=c)
+        return torch.sqrt(gv * gv + gh * gh + 1e-6).to(x.dtype)
+
+
+def _seq_conv(cin, cout, k=3):
+    return nn.Sequential(Conv2d(cin, cout, k, padding=k // 2))
+
+
+class SPSRNet(nn.Module):
+    """SPSR (structure-preserving SR): an ESRGAN trunk whose RRDB features at blocks 5/10/15/20 feed
+    a gradient-map branch; both branches are fused at HR resolution (chaiNNer SPSR.py key layout:
+    ``model.*``, ``b_*``, ``f_*``, ``HR_conv*_new``)."""
+
+    def __init__(self, state_dict):
+        super().__init__()
+        sd = state_dict
+        self.model_arch = "SPSR"
+        self.in_nc = sd["model.0.weight"].shape[1]
+        self.out_nc = sd["f_HR_conv1.0.bias"].shape[0]
+        nf = self.num_filters = sd["model.0.weight"].shape[0]
+        self.num_blocks = 1 + max(int(k.split(".")[3]) for k in sd if k.startswith("model.1.sub.") and "RDB" in k)
+        ups = sorted({int(k.split(".")[1]) for k in sd if re.match(r"^model\.\d+\.weight$", k) and int(k.split(".")[1]) > 1})
+        hr0 = ups[-1]                      # HR_conv0_new is the last model.N conv
+        ups = ups[:-1]
+        self.scale = 2 ** len(ups)
+        mods = {"0": Conv2d(self.in_nc, nf, 3, padding=1), "1": _Trunk(nf, self.num_blocks)}
+        for n in ups:
+            mods[str(n)] = Conv2d(nf, nf, 3, padding=1)
+        self.model = nn.ModuleDict(mods)
+        self._ups = [str(n) for n in ups]
+        self.HR_conv0_new = _seq_conv(nf, nf)
+        self.HR_conv1_new = _seq_conv(nf, nf)
+        self.get_g_nopadding = _GradMag()
+        self.b_fea_conv = _seq_conv(self.in_nc, nf)
+        for i in range(1, 5):
+            setattr(self, f"b_concat_{i}", _seq_conv(2 * nf, nf))
+            setattr(self, f"b_block_{i}", RRDB(2 * nf))
+        self.b_LR_conv = _seq_conv(nf, nf)
+        b_mods = []
+        for _ in ups:
+            b_mods += [nn.Upsample(scale_factor=2, mode="nearest"), Conv2d(nf, nf, 3, padding=1), nn.LeakyReLU(0.2)]
+        b_mods += [Conv2d(nf, nf, 3, padding=1), nn.LeakyReLU(0.2), Conv2d(nf, nf, 3, padding=1)]
+        self.b_module = nn.Sequential(*b_mods)
+        self.conv_w = nn.Sequential(Conv2d(nf, self.out_nc, 1))
+        self.f_concat = _seq_conv(2 * nf, nf)
+        self.f_block = RRDB(2 * nf)
+        self.f_HR_conv0 = _seq_conv(nf, nf)
+        self.f_HR_conv1 = _seq_conv(nf, self.out_nc)
+        sd = dict(sd)
+        for t in ("weight", "bias"):        # HR_conv0_new is registered twice (model.N and by name)
+            sd.setdefault(f"HR_conv0_new.0.{t}", sd.pop(f"model.{hr0}.{t}", None))
+            sd.pop(f"model.{hr0}.{t}", None)
+        missing, _ = self.load_state_dict(sd, strict=False)
+        missing = [m for m in missing if not m.startswith("get_g_nopadding")]
+        if missing:
+            raise UnsupportedModel(f"SPSR: missing keys {missing[:4]}")
+
+    def forward(self, x):
+        if x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
+        g = self.get_g_nopadding(x)
+        m = self.model
+        h = m["0"](x)
+        trunk = m["1"].sub
+        feats, y = [], h
+        for i, blk in enumerate(trunk[:-1]):
+            y = blk(y)
+            if (i + 1) % 5 == 0 and len(feats) < 4:
+                feats.append(y)
+        while len(feats) < 4:
+            feats.append(y)
+        y = trunk[-1](y, residual=h)               # LR conv + long skip
+        for name in self._ups:
+            y = _lrelu(m[name](y, upsample2x=True))
+        y = _lrelu(self.HR_conv0_new[0](y))
+        y = self.HR_conv1_new[0](y)
+        b_fea = self.b_fea_conv[0](g)
+        xb = b_fea
+        for i in range(1, 5):
+            xb = getattr(self, f"b_concat_{i}")[0](getattr(self, f"b_block_{i}")(torch.cat([xb, feats[i - 1]], 1)))
+        xb = self.b_LR_conv[0](xb, residual=b_fea)
+        xb = self.b_module(xb)
+        f = self.f_concat[0](self.f_block(torch.cat([xb, y], 1)))
+        return self.f_HR_conv1[0](_lrelu(self.f_HR_conv0[0](f)))
+
+
+class _SepConv(nn.Module):
+    def __init__(self, cin, cout, k, padding, bias=True):
+        super().__init__()
+        self.depthwise = nn.Conv2d(cin, cin, k, padding=padding, groups=cin, bias=bias)
+        self.pointwise = Conv2d(cin, cout, 1, bias=bias)
+
+    def forward(self, x):
+        return self.pointwise(self.depthwise(x))
+
+
+class _SwiftConvBlock(nn.Module):
+    def __init__(self, cin, cout, use_act=True, use_bn=True, k=3, padding=1):
+        super().__init__()
+        self.use_act = use_act
+        self.cnn = _SepConv(cin, cout, k, padding, bias=not use_bn)
+        self.bn = nn.BatchNorm2d(cout) if use_bn else nn.Identity()
+        self.act = nn.PReLU(num_parameters=cout)
+
+    def forward(self, x):
+        y = self.bn(self.cnn(x))
+        return self.act(y) if self.use_act else y
+
+
+class SwiftSRGAN(nn.Module):
+    """Swift-SRGAN generator (depthwise-separable convs, BN, PReLU, pixel-shuffle x2 stages;
+    chaiNNer SwiftSRGAN.py, state dict under ``model``)."""
+
+    def __init__(self, state_dict):
+        super().__init__()
+        sd = state_dict["model"] if "model" in state_dict else state_dict
+        self.model_arch = "Swift-SRGAN"
+        self.in_nc = sd["initial.cnn.depthwise.weight"].shape[0]
+        self.out_nc = sd["final_conv.pointwise.weight"].shape[0]
+        nf = self.num_filters = sd["initial.cnn.pointwise.weight"].shape[0]
+        self.num_blocks = len({k.split(".")[1] for k in sd if k.startswith("residual.")})
+        n_up = len({k.split(".")[1] for k in sd if k.startswith("upsampler.")})
+        self.scale = 2 ** n_up
+        self.initial = _SwiftConvBlock(self.in_nc, nf, use_bn=False, k=9, padding=4)
+        self.residual = nn.Sequential(*[nn.Module() for _ in range(self.num_blocks)])
+        for i in range(self.num_blocks):
+            self.residual[i].block1 = _SwiftConvBlock(nf, nf)
+            self.residual[i].block2 = _SwiftConvBlock(nf, nf, use_act=False)
+        self.convblock = _SwiftConvBlock(nf, nf, use_act=False)
+        self.upsampler = nn.Sequential(*[nn.Module() for _ in range(n_up)])
+        for i in range(n_up):
+            self.upsampler[i].conv = _SepConv(nf, nf * 4, 3, 1)
+            self.upsampler[i].ps = nn.PixelShuffle(2)
+            self.upsampler[i].act = nn.PReLU(num_parameters=nf)
+        self.final_conv = _SepConv(nf, self.in_nc, 9, 4)
+        self.load_state_dict(sd, strict=False)
+        self.eval()
+
+    def forward(self, x):
+        init = self.initial(x)
+        h = init
+        for r in self.residual:
+            h = r.block2(r.block1(h)) + h
+        h = self.convblock(h) + init
+        for u in self.upsampler:
+            h = u.act(u.ps(u.conv(h)))
+        return (torch.tanh(self.final_conv(h)) + 1) / 2
+
+
 _UNSUPPORTED_PROBES = [
-    ("SPSR", lambda k: "f_HR_conv1.0.weight" in k),
     ("HAT", lambda k: "layers.0.residual_group.blocks.0.conv_block.cab.0.weight" in k),
     ("Swin2SR", lambda k: "layers.0.residual_group.blocks.0.norm1.weight" in k and "patch_embed.proj.weight" in k),
     ("SwinIR", lambda k: "layers.0.residual_group.blocks.0.norm1.weight" in k),
@@ -225,8 +386,10 @@ def load_state_dict(state_dict) -> nn.Module:
     keys = set(state_dict.keys())
     if "body.0.weight" in keys and "body.1.weight" in keys:
         return SRVGGNetCompact(state_dict)
+    if "f_HR_conv1.0.weight" in keys:
+        return SPSRNet(state_dict)
     if "model" in keys and isinstance(state_dict["model"], dict) and "initial.cnn.depthwise.weight" in state_dict["model"]:
-        raise UnsupportedModel("Swift-SRGAN upscale models are not supported")
+        return SwiftSRGAN(state_dict)
     for name, probe in _UNSUPPORTED_PROBES:
         if probe(keys):
             raise UnsupportedModel(f"{name} upscale models are not supported")

@@ -3,7 +3,7 @@
 
 Same random weights are loaded into both implementations (fp32, CPU) and the outputs compared:
 SDXL-style UNet, SVD video UNet (VideoResBlock / SpatialVideoTransformer / AlphaBlender incl. the
-image-only indicator), KL-VAE decoder and the SVD temporal VAE decoder. Skipped where the reference
+image-only indicator), KL-VAE decoder, the SVD temporal VAE decoder and the chaiNNer upscalers (SPSR, Swift-SRGAN). Skipped where the reference
 tree is not mounted (e.g. the GPU box)."""
 import os
 import subprocess
@@ -94,10 +94,44 @@ elif which in ("vae", "vae_video"):
     z = torch.randn(6, 4, 8, 8)
     with torch.no_grad():
         print(which, close(m(z), r(z)))
+elif which in ("spsr", "swift"):
+    # the reference architectures size themselves from a state dict: seed one with the shape-defining
+    # keys, let the reference random-init the rest, then load its full state dict into ours
+    from comfy_gen_server_amd.models import upscalers as U
+    if which == "spsr":
+        from comfy_extras.chainner_models.architecture.SPSR import SPSRNet as R
+        seed = {"model.0.weight": torch.zeros(16, 3, 3, 3), "f_HR_conv1.0.bias": torch.zeros(3),
+                "model.1.sub.20.weight": torch.zeros(16, 16, 3, 3), "model.6.weight": torch.zeros(16, 16, 3, 3),
+                "model.8.weight": torch.zeros(16, 16, 3, 3)}
+        x = torch.rand(1, 3, 12, 10)
+    else:
+        from comfy_extras.chainner_models.architecture.SwiftSRGAN import Generator as R
+        seed = {"initial.cnn.depthwise.weight": torch.zeros(3, 1, 9, 9),
+                "initial.cnn.pointwise.weight": torch.zeros(16, 3, 1, 1),
+                "final_conv.pointwise.weight": torch.zeros(3, 16, 1, 1),
+                "residual.0.block1.cnn.depthwise.weight": torch.zeros(16, 1, 3, 3),
+                "residual.1.block1.cnn.depthwise.weight": torch.zeros(16, 1, 3, 3),
+                "upsampler.0.conv.depthwise.weight": torch.zeros(16, 1, 3, 3),
+                "upsampler.1.conv.depthwise.weight": torch.zeros(16, 1, 3, 3)}
+        x = torch.rand(1, 3, 12, 10)
+    torch.manual_seed(3)
+    r = R(seed).eval()
+    with torch.no_grad():
+        for k, v in r.state_dict().items():   # randomise BN stats / PReLU too
+            if not v.is_floating_point() or k.endswith(("weight_h", "weight_v")):
+                continue
+            v.copy_(torch.randn_like(v) * (0.1 if v.dim() > 1 else 0.5))
+            if "running_var" in k:
+                v.abs_().add_(0.5)
+    sd = r.state_dict()
+    m = U.load_state_dict({"model": sd} if which == "swift" else sd)
+    assert m.scale == r.scale == 4 and type(m).__name__ != "RRDBNet"
+    with torch.no_grad():
+        print(which, close(m(x), r(x), tol=1e-3))
 '''
 
 
-@pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video"])
+@pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")
