@@ -2,10 +2,11 @@
 model_loading.py:24-99`` dispatch, ``architecture/RRDB.py`` and ``architecture/SRVGG.py``).
 
 Supported here: ESRGAN / Real-ESRGAN (RRDBNet, old and new key layouts, x1/x2 pixel-unshuffle
-variants, scale 1-8), Real-ESRGAN compact (SRVGGNetCompact), SPSR and Swift-SRGAN. Every 3x3 conv is a
+variants, scale 1-8), Real-ESRGAN compact (SRVGGNetCompact), SPSR, Swift-SRGAN, and the
+Swin-transformer family (SwinIR / Swin2SR / HAT, ``swin_sr.py``). Every 3x3 conv is a
 ``layers.Conv2d`` so on the device it runs as the NHWC implicit-GEMM MFMA kernel (bias fused);
 the state dict is re-keyed to the old-arch ``model.N`` layout the reference uses, so any file
-that loads there loads here. Other chaiNNer architectures (SwinIR/Swin2SR/HAT/DAT, OmniSR, SCUNet,
+that loads there loads here. Other chaiNNer architectures (DAT, OmniSR, SCUNet,
 LaMa, GFPGAN/CodeFormer/RestoreFormer) are detected by the same key probes and
 rejected with ``UnsupportedModel`` naming the architecture.
 """
@@ -364,9 +365,6 @@ class SwiftSRGAN(nn.Module):
 
 
 _UNSUPPORTED_PROBES = [
-    ("HAT", lambda k: "layers.0.residual_group.blocks.0.conv_block.cab.0.weight" in k),
-    ("Swin2SR", lambda k: "layers.0.residual_group.blocks.0.norm1.weight" in k and "patch_embed.proj.weight" in k),
-    ("SwinIR", lambda k: "layers.0.residual_group.blocks.0.norm1.weight" in k),
     ("GFPGAN", lambda k: "toRGB.0.weight" in k and "stylegan_decoder.style_mlp.1.weight" in k),
     ("RestoreFormer", lambda k: "encoder.conv_in.weight" in k and "encoder.down.0.block.0.norm1.weight" in k),
     ("CodeFormer", lambda k: "encoder.blocks.0.weight" in k and "quantize.embedding.weight" in k),
@@ -390,6 +388,14 @@ def load_state_dict(state_dict) -> nn.Module:
         return SPSRNet(state_dict)
     if "model" in keys and isinstance(state_dict["model"], dict) and "initial.cnn.depthwise.weight" in state_dict["model"]:
         return SwiftSRGAN(state_dict)
+    if "layers.0.residual_group.blocks.0.norm1.weight" in keys:
+        from . import swin_sr
+        try:
+            if "layers.0.residual_group.blocks.0.conv_block.cab.0.weight" in keys:
+                return swin_sr.HAT(state_dict)
+            return swin_sr.SwinIR(state_dict, v2="patch_embed.proj.weight" in keys)
+        except (KeyError, ValueError, RuntimeError) as e:
+            raise UnsupportedModel(f"malformed Swin-family upscale model: {e!r}") from e
     for name, probe in _UNSUPPORTED_PROBES:
         if probe(keys):
             raise UnsupportedModel(f"{name} upscale models are not supported")

@@ -37,6 +37,23 @@ def load(ref, ours):
     m, u = ref.load_state_dict(sd, strict=False)
     assert not m and not u, (m[:5], u[:5])
 
+def check_upscaler(r, seed, x, which):
+    from comfy_gen_server_amd.models import upscalers as U
+    bufs = {n for n, _ in r.named_buffers()}
+    with torch.no_grad():
+        for k, v in r.state_dict().items():   # randomise BN stats / PReLU too
+            if not v.is_floating_point() or k in bufs or k.endswith(("weight_h", "weight_v")):
+                continue
+            v.copy_(torch.randn_like(v) * (0.1 if v.dim() > 1 else 0.5))
+            if "running_var" in k:
+                v.abs_().add_(0.5)
+    sd = r.state_dict()
+    m = U.load_state_dict({"model": sd} if which == "swift" else sd)
+    assert m.scale == r.scale and type(m).__name__ != "RRDBNet", (m.scale, r.scale)
+    with torch.no_grad():
+        print(which, close(m(x), r(x), tol=1e-3))
+
+
 which = sys.argv_which
 if which == "unet":
     from comfy.ldm.modules.diffusionmodules.openaimodel import UNetModel as R
@@ -116,22 +133,70 @@ elif which in ("spsr", "swift"):
         x = torch.rand(1, 3, 12, 10)
     torch.manual_seed(3)
     r = R(seed).eval()
-    with torch.no_grad():
-        for k, v in r.state_dict().items():   # randomise BN stats / PReLU too
-            if not v.is_floating_point() or k.endswith(("weight_h", "weight_v")):
-                continue
-            v.copy_(torch.randn_like(v) * (0.1 if v.dim() > 1 else 0.5))
-            if "running_var" in k:
-                v.abs_().add_(0.5)
-    sd = r.state_dict()
-    m = U.load_state_dict({"model": sd} if which == "swift" else sd)
-    assert m.scale == r.scale == 4 and type(m).__name__ != "RRDBNet"
-    with torch.no_grad():
-        print(which, close(m(x), r(x), tol=1e-3))
+    check_upscaler(r, seed, x, which)
+elif which.startswith(("swinir", "swin2sr", "hat")):
+    from comfy_gen_server_amd.models import upscalers as U
+    Z = torch.zeros
+    dim, ws, nf = 24, 8, 64
+    def blocks(n_layers, depth, extra=()):
+        d = {}
+        for i in range(n_layers):
+            for j in range(depth):
+                d[f"layers.{i}.residual_group.blocks.{j}.norm1.weight"] = Z(dim)
+                for e in extra:
+                    d[f"layers.{i}.residual_group.blocks.{j}.{e[0]}"] = Z(*e[1])
+        return d
+    b0 = "layers.0.residual_group.blocks.0."
+    x = torch.rand(1, 3, 13, 11)
+    if which.startswith("swinir"):
+        from comfy_extras.chainner_models.architecture.SwinIR import SwinIR as R
+        kind = which.split("_")[1]
+        if kind == "denoise":
+            ws = 7
+        seed = {"conv_first.weight": Z(dim, 3, 3, 3), b0 + "mlp.fc1.bias": Z(dim * 2),
+                b0 + "attn.relative_position_bias_table": Z((2 * ws - 1) ** 2, 3),
+                b0 + "attn.relative_position_index": Z(ws * ws, ws * ws, dtype=torch.long)}
+        seed.update(blocks(2, 2))
+        if kind == "classic":
+            seed.update({"conv_before_upsample.0.weight": Z(nf, dim, 3, 3), "upsample.0.weight": Z(4 * nf, nf, 3, 3),
+                         "upsample.2.weight": Z(4 * nf, nf, 3, 3), "conv_last.weight": Z(3, nf, 3, 3)})
+        elif kind == "light":
+            seed.update({"upsample.0.weight": Z(12, dim, 3, 3), "upsample.0.bias": Z(12)})
+        elif kind == "real":
+            seed.update({"conv_before_upsample.0.weight": Z(nf, dim, 3, 3), "conv_up1.weight": Z(nf, nf, 3, 3),
+                         "conv_up2.weight": Z(nf, nf, 3, 3), "conv_last.weight": Z(3, nf, 3, 3),
+                         "layers.0.conv.4.weight": Z(dim, dim // 4, 3, 3)})
+        else:
+            seed.update({"conv_last.weight": Z(3, dim, 3, 3), "layers.0.residual_group.blocks.1.attn_mask": Z(4, 49, 49)})
+    elif which.startswith("swin2sr"):
+        from comfy_extras.chainner_models.architecture.Swin2SR import Swin2SR as R
+        R.load_state_dict = lambda self, sd, strict=True: torch.nn.Module.load_state_dict(self, sd, strict=False)
+        seed = {"conv_first.weight": Z(dim, 3, 3, 3), "patch_embed.proj.weight": Z(dim, dim, 1, 1),
+                b0 + "mlp.fc1.bias": Z(dim * 2), b0 + "attn.relative_position_index": Z(ws * ws, ws * ws, dtype=torch.long),
+                "conv_before_upsample.0.weight": Z(nf, dim, 3, 3), "upsample.0.weight": Z(4 * nf, nf, 3, 3),
+                "conv_last.weight": Z(3, nf, 3, 3)}
+        seed.update(blocks(2, 2))
+        if which.endswith("aux"):
+            seed["conv_aux.weight"] = Z(3, nf, 3, 3)
+    else:
+        from comfy_extras.chainner_models.architecture.HAT import HAT as R
+        dim, nf = 60, 16
+        seed = {"conv_first.weight": Z(dim, 3, 3, 3), "conv_last.weight": Z(3, nf, 3, 3),
+                "conv_before_upsample.0.weight": Z(nf, dim, 3, 3), "upsample.0.weight": Z(4 * nf, nf, 3, 3),
+                "upsample.2.weight": Z(4 * nf, nf, 3, 3), b0 + "mlp.fc1.bias": Z(dim * 2),
+                b0 + "attn.relative_position_bias_table": Z((2 * ws - 1) ** 2, 3),
+                "relative_position_index_SA": Z(ws * ws, ws * ws, dtype=torch.long)}
+        seed.update(blocks(2, 2, [("conv_block.cab.0.weight", (dim // 3, dim, 3, 3))]))
+        x = torch.rand(1, 3, 19, 16)
+    torch.manual_seed(3)
+    r = R(seed).eval()
+    check_upscaler(r, seed, x, which)
 '''
 
 
-@pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift"])
+@pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
+                                   "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
+                                   "hat"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

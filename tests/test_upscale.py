@@ -105,8 +105,10 @@ def test_esrgan_pixel_unshuffle_variant_and_srvgg():
     ref = F.pixel_shuffle(h, s) + F.interpolate(x, scale_factor=s, mode="nearest")
     with torch.no_grad():
         assert torch.allclose(v(x), ref, atol=1e-5)
-    with pytest.raises(upscalers.UnsupportedModel):
+    with pytest.raises(upscalers.UnsupportedModel):     # recognised family, malformed file
         upscalers.load_state_dict({"layers.0.residual_group.blocks.0.norm1.weight": torch.zeros(1)})
+    with pytest.raises(upscalers.UnsupportedModel, match="DAT"):
+        upscalers.load_state_dict({"layers.0.blocks.2.attn.attn_mask_0": torch.zeros(1)})
 
 
 def test_upscale_nodes_tiled(tmp_path):
@@ -140,4 +142,67 @@ def test_upscale_esrgan_gpu(cuda):
         y = m(x.to(cuda, torch.bfloat16)).float().cpu()
         ref = _esrgan_ref(sd, x, 1)
     assert ops.stats().get(("conv", "hip"), 0) > 10
+    assert ((y - ref).norm() / ref.norm()).item() < 3e-2
+
+
+def _swin_seed(kind, dim=48, ws=8, nf=32):
+    """Shape-defining keys for the Swin family; the rest is random-initialised by the test."""
+    Z = torch.zeros
+    b0 = "layers.0.residual_group.blocks.0."
+    sd = {"conv_first.weight": Z(dim, 3, 3, 3), b0 + "mlp.fc1.bias": Z(dim * 2),
+          "conv_before_upsample.0.weight": Z(nf, dim, 3, 3), "upsample.0.weight": Z(4 * nf, nf, 3, 3),
+          "conv_last.weight": Z(3, nf, 3, 3), b0 + "attn.relative_position_index": Z(ws * ws, ws * ws)}
+    for i in range(2):
+        for j in range(2):
+            sd[f"layers.{i}.residual_group.blocks.{j}.norm1.weight"] = Z(dim)
+            if kind == "hat":
+                sd[f"layers.{i}.residual_group.blocks.{j}.conv_block.cab.0.weight"] = Z(dim // 3, dim, 3, 3)
+                sd[f"layers.{i}.residual_group.blocks.{j}.conv_block.cab.3.attention.1.weight"] = Z(dim // 16, dim, 1, 1)
+    if kind == "swin2sr":
+        sd["patch_embed.proj.weight"] = Z(dim, dim, 1, 1)
+        sd[b0 + "attn.logit_scale"] = Z(3, 1, 1)
+    else:
+        sd[b0 + "attn.relative_position_bias_table"] = Z((2 * ws - 1) ** 2, 3)
+    if kind == "hat":
+        sd["relative_position_index_SA"] = Z(ws * ws, ws * ws)
+        sd["layers.0.residual_group.overlap_attn.relative_position_bias_table"] = Z((ws + 12 - 1) ** 2, 3)
+        sd["layers.0.conv.weight"] = Z(dim, dim, 3, 3)
+    return sd
+
+
+def _random_swin(kind):
+    from comfy_gen_server_amd.models import swin_sr
+    from comfy_gen_server_amd.models.layers import init_random_
+    seed = _swin_seed(kind)
+    m = swin_sr.HAT(seed, strict=False) if kind == "hat" else swin_sr.SwinIR(seed, v2=kind == "swin2sr", strict=False)
+    init_random_(m, seed=4)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd.update({k: v for k, v in seed.items() if "position_index" in k})   # file-only index buffers
+    return sd
+
+
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat"])
+def test_swin_family_dispatch_and_forward(kind):
+    sd = _random_swin(kind)
+    m = upscalers.load_state_dict(sd)
+    assert m.model_arch == {"swinir": "SwinIR", "swin2sr": "Swin2SR", "hat": "HAT"}[kind] and m.scale == 2
+    with torch.no_grad():
+        y = m(torch.rand(1, 3, 13, 10))
+    assert y.shape == (1, 3, 26, 20) and torch.isfinite(y).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat"])
+def test_swin_family_gpu(cuda, kind):
+    """Swin-family upscalers in bf16 on the device (HIP GEMMs for qkv/proj/MLP, MFMA convs) vs fp32 CPU."""
+    from comfy_gen_server_amd import ops
+    sd = _random_swin(kind)
+    m = upscalers.load_state_dict(sd)
+    x = torch.rand(1, 3, 40, 32)
+    with torch.no_grad():
+        ref = m(x)
+        g = m.to(device=cuda, dtype=torch.bfloat16)
+        ops.reset_stats()
+        y = g(x.to(cuda, torch.bfloat16)).float().cpu()
+    assert ops.stats().get(("gemm", "hip"), 0) + ops.stats().get(("gemm", "lib"), 0) > 0
     assert ((y - ref).norm() / ref.norm()).item() < 3e-2
