@@ -558,3 +558,133 @@ class HAT(nn.Module):
         x = self.conv_last(self.upsample(self.conv_before_upsample(x)))
         x = x / self.img_range + mean
         return x[:, :, :H * self.upscale, :W * self.upscale]
+
+
+# ----------------------------------------------------------------------------------------------
+# SCUNet (swin-conv UNet blind denoiser; reference SCUNet.py:274-446): 4-level UNet whose blocks
+# split channels between a residual conv path and a (shifted-)window transformer path.
+# ----------------------------------------------------------------------------------------------
+
+
+def _scunet_mask(nh: int, nw: int, p: int, device) -> torch.Tensor:
+    """[nh*nw, p*p, p*p] bool, True = blocked: after the cyclic shift only the last window row /
+    column mixes pixels from opposite image borders."""
+    s = p - p // 2
+    m = torch.zeros(nh, nw, p, p, p, p, dtype=torch.bool)
+    m[-1, :, :s, :, s:, :] = True
+    m[-1, :, s:, :, :s, :] = True
+    m[:, -1, :, :s, :, s:] = True
+    m[:, -1, :, s:, :, :s] = True
+    return m.reshape(nh * nw, p * p, p * p).to(device)
+
+
+class _WMSA(nn.Module):
+    def __init__(self, dim: int, head_dim: int, ws: int, shifted: bool):
+        super().__init__()
+        self.heads, self.hd, self.ws, self.shifted = dim // head_dim, head_dim, ws, shifted
+        self.embedding_layer = Linear(dim, 3 * dim)
+        self.relative_position_params = nn.Parameter(torch.zeros(self.heads, 2 * ws - 1, 2 * ws - 1),
+                                                     requires_grad=False)
+        self.linear = Linear(dim, dim)
+        c = torch.stack(torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing="ij"), -1).reshape(-1, 2)
+        rel = c[:, None, :] - c[None, :, :] + ws - 1
+        self.register_buffer("rel", rel, persistent=False)
+
+    def forward(self, x):                       # x [B, H, W, C]
+        B, H, W, C = x.shape
+        p, h = self.ws, self.heads
+        if self.shifted:
+            x = torch.roll(x, (-(p // 2), -(p // 2)), (1, 2))
+        win = _partition(x, p)                                          # [B*nW, N, C]
+        q, k, v = self.embedding_layer(win).view(win.shape[0], p * p, 3, h, self.hd).permute(2, 0, 3, 1, 4).unbind(0)
+        s = ((q * self.hd ** -0.5) @ k.transpose(-2, -1)).float()
+        s = s + self.relative_position_params.float()[:, self.rel[..., 0], self.rel[..., 1]]
+        if self.shifted:
+            nW = (H // p) * (W // p)
+            m = _scunet_mask(H // p, W // p, p, x.device)
+            s = s.view(B, nW, h, p * p, p * p).masked_fill(m[None, :, None], float("-inf")).view_as(s)
+        o = (torch.softmax(s, -1).to(v.dtype) @ v).transpose(1, 2).reshape(-1, p * p, C)
+        y = _reverse(self.linear(o), p, B, H, W)
+        if self.shifted:
+            y = torch.roll(y, (p // 2, p // 2), (1, 2))
+        return y
+
+
+class _SCUTransBlock(nn.Module):
+    def __init__(self, dim, head_dim, ws, shifted):
+        super().__init__()
+        self.ln1 = LayerNorm(dim)
+        self.msa = _WMSA(dim, head_dim, ws, shifted)
+        self.ln2 = LayerNorm(dim)
+        self.mlp = nn.Sequential(Linear(dim, 4 * dim), nn.GELU(), Linear(4 * dim, dim))
+
+    def forward(self, x):
+        x = x + self.msa(self.ln1(x))
+        return x + self.mlp(self.ln2(x))
+
+
+class ConvTransBlock(nn.Module):
+    def __init__(self, conv_dim, trans_dim, head_dim, ws, shifted):
+        super().__init__()
+        self.conv_dim = conv_dim
+        c = conv_dim + trans_dim
+        self.trans_block = _SCUTransBlock(trans_dim, head_dim, ws, shifted)
+        self.conv1_1 = Conv2d(c, c, 1)
+        self.conv1_2 = Conv2d(c, c, 1)
+        self.conv_block = nn.Sequential(Conv2d(conv_dim, conv_dim, 3, padding=1, bias=False), nn.ReLU(),
+                                        Conv2d(conv_dim, conv_dim, 3, padding=1, bias=False))
+
+    def forward(self, x):
+        y = self.conv1_1(x)
+        cx, tx = y[:, :self.conv_dim], y[:, self.conv_dim:]
+        cx = self.conv_block(cx) + cx
+        tx = self.trans_block(tx.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        return x + self.conv1_2(torch.cat([cx, tx], 1))
+
+
+class SCUNet(nn.Module):
+    """SCUNet (dim 64, 4 blocks per stage, 32-wide heads, 8x8 windows — the released config)."""
+
+    def __init__(self, state_dict, strict: bool = True):
+        super().__init__()
+        self.model_arch = "SCUNet"
+        self.scale = 1
+        dim = self.dim = state_dict["m_head.0.weight"].shape[0] if "m_head.0.weight" in state_dict else 64
+        in_nc = self.in_nc = self.out_nc = state_dict["m_head.0.weight"].shape[1] if "m_head.0.weight" in state_dict else 3
+        ws, hd = 8, 32
+        cfg = [4] * 7
+        res = 256                               # training resolution: stage-wise shift eligibility
+
+        def stage(c, n, r):
+            return [ConvTransBlock(c, c, hd, ws, bool(i % 2) and r > ws) for i in range(n)]
+
+        self.m_head = nn.Sequential(Conv2d(in_nc, dim, 3, padding=1, bias=False))
+        self.m_down1 = nn.Sequential(*stage(dim // 2, cfg[0], res), Conv2d(dim, 2 * dim, 2, stride=2, bias=False))
+        self.m_down2 = nn.Sequential(*stage(dim, cfg[1], res // 2), Conv2d(2 * dim, 4 * dim, 2, stride=2, bias=False))
+        self.m_down3 = nn.Sequential(*stage(2 * dim, cfg[2], res // 4),
+                                     Conv2d(4 * dim, 8 * dim, 2, stride=2, bias=False))
+        self.m_body = nn.Sequential(*stage(4 * dim, cfg[3], res // 8))
+        self.m_up3 = nn.Sequential(nn.ConvTranspose2d(8 * dim, 4 * dim, 2, 2, bias=False), *stage(2 * dim, cfg[4], res // 4))
+        self.m_up2 = nn.Sequential(nn.ConvTranspose2d(4 * dim, 2 * dim, 2, 2, bias=False), *stage(dim, cfg[5], res // 2))
+        self.m_up1 = nn.Sequential(nn.ConvTranspose2d(2 * dim, dim, 2, 2, bias=False), *stage(dim // 2, cfg[6], res))
+        self.m_tail = nn.Sequential(Conv2d(dim, in_nc, 3, padding=1, bias=False))
+        for m in self.modules():
+            if isinstance(m, nn.ConvTranspose2d):
+                m.weight.requires_grad_(False)
+        missing, _ = self.load_state_dict(state_dict, strict=False)
+        if missing and strict:
+            raise ValueError(f"SCUNet: missing keys {missing[:4]}")
+        self.eval()
+
+    def forward(self, x0):
+        h, w = x0.shape[-2:]
+        x0 = F.pad(x0, (0, (64 - w % 64) % 64, 0, (64 - h % 64) % 64), "reflect")
+        x1 = self.m_head(x0)
+        x2 = self.m_down1(x1)
+        x3 = self.m_down2(x2)
+        x4 = self.m_down3(x3)
+        x = self.m_body(x4)
+        x = self.m_up3(x + x4)
+        x = self.m_up2(x + x3)
+        x = self.m_up1(x + x2)
+        return self.m_tail(x + x1)[:, :, :h, :w]

@@ -57,11 +57,12 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     Device path: the HIP GEMM family (v5 ping-pong 256x256x64, v3 8-wave 32x32 MFMA, v1 128x128),
     the kernel picked per shape by ``ops.autotune`` among those and hipBLASLt (through ATen)."""
     be = backend_for("gemm", x, "cgs_gemm_bf16")
-    if be == "hip" and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
+    # K % 8: the kernels' 16-byte row loads (a K=2 coordinate MLP is not GEMM-shaped work anyway)
+    if be == "hip" and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
         K = x.shape[-1]
         N = weight.shape[0]
         a = x.reshape(-1, K)
-        if a.stride(-1) != 1 or (a.shape[0] > 1 and a.stride(0) < K):
+        if a.stride(-1) != 1 or (a.shape[0] > 1 and a.stride(0) < K) or a.stride(0) % 8:
             a = a.contiguous()
         M = a.shape[0]
         epi = 0

@@ -134,6 +134,17 @@ elif which in ("spsr", "swift"):
     torch.manual_seed(3)
     r = R(seed).eval()
     check_upscaler(r, seed, x, which)
+elif which == "scunet":
+    from comfy_extras.chainner_models.architecture.SCUNet import SCUNet as R
+    from comfy_gen_server_amd.models import swin_sr, upscalers as U
+    m = swin_sr.SCUNet({}, strict=False); init_random_(m, seed=6)
+    sd = m.state_dict()
+    r = R(sd).eval()                       # the reference loads strict: key sets must match exactly
+    m = U.load_state_dict(sd)
+    assert type(m).__name__ == "SCUNet"
+    x = torch.rand(1, 3, 40, 72)
+    with torch.no_grad():
+        print(which, close(m(x), r(x), tol=1e-3))
 elif which.startswith(("swinir", "swin2sr", "hat")):
     from comfy_gen_server_amd.models import upscalers as U
     Z = torch.zeros
@@ -196,7 +207,7 @@ elif which.startswith(("swinir", "swin2sr", "hat")):
 
 @pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
                                    "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
-                                   "hat"])
+                                   "hat", "scunet"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

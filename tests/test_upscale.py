@@ -173,6 +173,10 @@ def _swin_seed(kind, dim=48, ws=8, nf=32):
 def _random_swin(kind):
     from comfy_gen_server_amd.models import swin_sr
     from comfy_gen_server_amd.models.layers import init_random_
+    if kind == "scunet":
+        m = swin_sr.SCUNet({}, strict=False)
+        init_random_(m, seed=4)
+        return {k: v.clone() for k, v in m.state_dict().items()}
     seed = _swin_seed(kind)
     m = swin_sr.HAT(seed, strict=False) if kind == "hat" else swin_sr.SwinIR(seed, v2=kind == "swin2sr", strict=False)
     init_random_(m, seed=4)
@@ -181,18 +185,20 @@ def _random_swin(kind):
     return sd
 
 
-@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat"])
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet"])
 def test_swin_family_dispatch_and_forward(kind):
     sd = _random_swin(kind)
     m = upscalers.load_state_dict(sd)
-    assert m.model_arch == {"swinir": "SwinIR", "swin2sr": "Swin2SR", "hat": "HAT"}[kind] and m.scale == 2
+    s = 1 if kind == "scunet" else 2
+    assert m.model_arch == {"swinir": "SwinIR", "swin2sr": "Swin2SR", "hat": "HAT", "scunet": "SCUNet"}[kind]
+    assert m.scale == s
     with torch.no_grad():
         y = m(torch.rand(1, 3, 13, 10))
-    assert y.shape == (1, 3, 26, 20) and torch.isfinite(y).all()
+    assert y.shape == (1, 3, 13 * s, 10 * s) and torch.isfinite(y).all()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat"])
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet"])
 def test_swin_family_gpu(cuda, kind):
     """Swin-family upscalers in bf16 on the device (HIP GEMMs for qkv/proj/MLP, MFMA convs) vs fp32 CPU."""
     from comfy_gen_server_amd import ops
