@@ -52,6 +52,16 @@ def shift_mask(H: int, W: int, ws: int, shift: int, device) -> torch.Tensor:
     return m
 
 
+def pad_to_multiple(x: torch.Tensor, m: int) -> torch.Tensor:
+    """Reflect-pad H/W up to a multiple of ``m`` (reference ``check_image_size``); inputs smaller
+    than the pad, where reflection is undefined, are edge-replicated instead."""
+    H, W = x.shape[-2:]
+    ph, pw = (m - H % m) % m, (m - W % m) % m
+    if not ph and not pw:
+        return x
+    return F.pad(x, (0, pw, 0, ph), "reflect" if ph < H and pw < W else "replicate")
+
+
 def _partition(x: torch.Tensor, ws: int) -> torch.Tensor:
     B, H, W, C = x.shape
     return x.view(B, H // ws, ws, W // ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, C)
@@ -335,7 +345,7 @@ class SwinIR(nn.Module):
     def forward(self, x):
         H, W = x.shape[-2:]
         m = self.window_size * self.start_unshuffle
-        x = F.pad(x, (0, (m - W % m) % m, 0, (m - H % m) % m), "reflect")
+        x = pad_to_multiple(x, m)
         mean = self.mean.to(x.dtype)
         x = (x - mean) * self.img_range
         if self.start_unshuffle > 1:
@@ -547,7 +557,7 @@ class HAT(nn.Module):
         mean = self.mean.to(x.dtype)
         x = (x - mean) * self.img_range
         ws = self.window_size
-        x = F.pad(x, (0, (ws - W % ws) % ws, 0, (ws - H % ws) % ws), "reflect")
+        x = pad_to_multiple(x, ws)
         f = self.conv_first(x)
         hw = f.shape[-2:]
         mask = shift_mask(hw[0], hw[1], ws, ws // 2, x.device)
@@ -678,7 +688,7 @@ class SCUNet(nn.Module):
 
     def forward(self, x0):
         h, w = x0.shape[-2:]
-        x0 = F.pad(x0, (0, (64 - w % 64) % 64, 0, (64 - h % 64) % 64), "reflect")
+        x0 = pad_to_multiple(x0, 64)
         x1 = self.m_head(x0)
         x2 = self.m_down1(x1)
         x3 = self.m_down2(x2)
