@@ -134,6 +134,15 @@ elif which in ("spsr", "swift"):
     torch.manual_seed(3)
     r = R(seed).eval()
     check_upscaler(r, seed, x, which)
+elif which == "omnisr":
+    from comfy_extras.chainner_models.architecture.OmniSR.OmniSR import OmniSR as R
+    Z = torch.zeros
+    seed = {"input.weight": Z(32, 3, 3, 3), "up.0.weight": Z(3 * 4, 32, 3, 3),
+            "residual_layer.1.residual_layer.0.layer.0.fn.0.weight": Z(32, 32, 1, 1),
+            "residual_layer.0.residual_layer.0.layer.2.fn.rel_pos_bias.weight": Z(15 * 15, 4)}
+    torch.manual_seed(3)
+    r = R(seed).eval()
+    check_upscaler(r, seed, torch.rand(1, 3, 21, 18), which)
 elif which == "scunet":
     from comfy_extras.chainner_models.architecture.SCUNet import SCUNet as R
     from comfy_gen_server_amd.models import swin_sr, upscalers as U
@@ -207,7 +216,7 @@ elif which.startswith(("swinir", "swin2sr", "hat")):
 
 @pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
                                    "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
-                                   "hat", "scunet"])
+                                   "hat", "scunet", "omnisr"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

@@ -173,8 +173,14 @@ def _swin_seed(kind, dim=48, ws=8, nf=32):
 def _random_swin(kind):
     from comfy_gen_server_amd.models import swin_sr
     from comfy_gen_server_amd.models.layers import init_random_
-    if kind == "scunet":
-        m = swin_sr.SCUNet({}, strict=False)
+    if kind in ("scunet", "omnisr"):
+        if kind == "scunet":
+            m = swin_sr.SCUNet({}, strict=False)
+        else:
+            from comfy_gen_server_amd.models.omnisr import OmniSR
+            m = OmniSR({"input.weight": torch.zeros(64, 3, 3, 3), "up.0.weight": torch.zeros(12, 64, 3, 3),
+                        "residual_layer.1.residual_layer.0.layer.0.fn.0.weight": torch.zeros(64, 64, 1, 1)},
+                       strict=False)
         init_random_(m, seed=4)
         return {k: v.clone() for k, v in m.state_dict().items()}
     seed = _swin_seed(kind)
@@ -185,20 +191,21 @@ def _random_swin(kind):
     return sd
 
 
-@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet"])
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet", "omnisr"])
 def test_swin_family_dispatch_and_forward(kind):
     sd = _random_swin(kind)
     m = upscalers.load_state_dict(sd)
     s = 1 if kind == "scunet" else 2
-    assert m.model_arch == {"swinir": "SwinIR", "swin2sr": "Swin2SR", "hat": "HAT", "scunet": "SCUNet"}[kind]
+    assert m.model_arch == {"swinir": "SwinIR", "swin2sr": "Swin2SR", "hat": "HAT", "scunet": "SCUNet",
+                            "omnisr": "OmniSR"}[kind]
     assert m.scale == s
     with torch.no_grad():
-        y = m(torch.rand(1, 3, 13, 10))
-    assert y.shape == (1, 3, 13 * s, 10 * s) and torch.isfinite(y).all()
+        y = m(torch.rand(1, 3, 17, 16))
+    assert y.shape == (1, 3, 17 * s, 16 * s) and torch.isfinite(y).all()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet"])
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet", "omnisr"])
 def test_swin_family_gpu(cuda, kind):
     """Swin-family upscalers in bf16 on the device (HIP GEMMs for qkv/proj/MLP, MFMA convs) vs fp32 CPU."""
     from comfy_gen_server_amd import ops
