@@ -143,6 +143,24 @@ elif which == "omnisr":
     torch.manual_seed(3)
     r = R(seed).eval()
     check_upscaler(r, seed, torch.rand(1, 3, 21, 18), which)
+elif which == "dat":
+    from comfy_extras.chainner_models.architecture.DAT import DAT as R
+    R.load_state_dict = lambda self, sd, strict=True: torch.nn.Module.load_state_dict(self, sd, strict=False)
+    Z = torch.zeros
+    dim = 64
+    seed = {"conv_first.weight": Z(dim, 3, 3, 3), "conv_before_upsample.0.weight": Z(64, dim, 3, 3),
+            "upsample.0.weight": Z(256, 64, 3, 3), "conv_last.weight": Z(3, 64, 3, 3),
+            "layers.0.blocks.1.attn.temperature": Z(4, 1, 1), "layers.0.blocks.0.ffn.fc1.weight": Z(dim * 2, dim),
+            "layers.0.blocks.2.attn.attn_mask_0": Z(32, 32, 32)}
+    rpe = torch.stack(torch.meshgrid(torch.arange(-3, 4), torch.arange(-7, 8), indexing="ij")).flatten(1).t().float()
+    seed["layers.0.blocks.0.attn.attns.0.rpe_biases"] = rpe
+    for i in range(2):
+        for j in range(4):
+            seed[f"layers.{i}.blocks.{j}.norm1.weight"] = Z(dim)
+    torch.manual_seed(3)
+    r = R(seed).eval()
+    assert r.split_size == [4, 8]
+    check_upscaler(r, seed, torch.rand(1, 3, 20, 28), which)
 elif which == "scunet":
     from comfy_extras.chainner_models.architecture.SCUNet import SCUNet as R
     from comfy_gen_server_amd.models import swin_sr, upscalers as U
@@ -216,7 +234,7 @@ elif which.startswith(("swinir", "swin2sr", "hat")):
 
 @pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
                                    "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
-                                   "hat", "scunet", "omnisr"])
+                                   "hat", "scunet", "omnisr", "dat"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

@@ -173,6 +173,19 @@ def _swin_seed(kind, dim=48, ws=8, nf=32):
 def _random_swin(kind):
     from comfy_gen_server_amd.models import swin_sr
     from comfy_gen_server_amd.models.layers import init_random_
+    if kind == "dat":
+        from comfy_gen_server_amd.models.dat import DAT
+        Z = torch.zeros
+        seed = {"conv_first.weight": Z(64, 3, 3, 3), "conv_before_upsample.0.weight": Z(64, 64, 3, 3),
+                "upsample.0.weight": Z(256, 64, 3, 3), "conv_last.weight": Z(3, 64, 3, 3),
+                "layers.0.blocks.1.attn.temperature": Z(4, 1, 1), "layers.0.blocks.0.ffn.fc1.weight": Z(128, 64),
+                "layers.0.blocks.2.attn.attn_mask_0": Z(1)}
+        seed.update({f"layers.{i}.blocks.{j}.norm1.weight": Z(64) for i in range(2) for j in range(4)})
+        m = DAT(seed, strict=False)
+        init_random_(m, seed=4)
+        sd = {k: v.clone() for k, v in m.state_dict().items()}
+        sd["layers.0.blocks.2.attn.attn_mask_0"] = Z(1)        # file-only buffer the loader sniffs
+        return sd
     if kind in ("scunet", "omnisr"):
         if kind == "scunet":
             m = swin_sr.SCUNet({}, strict=False)
@@ -191,13 +204,13 @@ def _random_swin(kind):
     return sd
 
 
-@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet", "omnisr"])
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet", "omnisr", "dat"])
 def test_swin_family_dispatch_and_forward(kind):
     sd = _random_swin(kind)
     m = upscalers.load_state_dict(sd)
     s = 1 if kind == "scunet" else 2
     assert m.model_arch == {"swinir": "SwinIR", "swin2sr": "Swin2SR", "hat": "HAT", "scunet": "SCUNet",
-                            "omnisr": "OmniSR"}[kind]
+                            "omnisr": "OmniSR", "dat": "DAT"}[kind]
     assert m.scale == s
     with torch.no_grad():
         y = m(torch.rand(1, 3, 17, 16))
@@ -205,7 +218,7 @@ def test_swin_family_dispatch_and_forward(kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet", "omnisr"])
+@pytest.mark.parametrize("kind", ["swinir", "swin2sr", "hat", "scunet", "omnisr", "dat"])
 def test_swin_family_gpu(cuda, kind):
     """Swin-family upscalers in bf16 on the device (HIP GEMMs for qkv/proj/MLP, MFMA convs) vs fp32 CPU."""
     from comfy_gen_server_amd import ops
