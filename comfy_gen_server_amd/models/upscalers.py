@@ -4,10 +4,10 @@ model_loading.py:24-99`` dispatch, ``architecture/RRDB.py`` and ``architecture/S
 Supported here: ESRGAN / Real-ESRGAN (RRDBNet, old and new key layouts, x1/x2 pixel-unshuffle
 variants, scale 1-8), Real-ESRGAN compact (SRVGGNetCompact), SPSR, Swift-SRGAN, and the
 Swin-transformer family (SwinIR / Swin2SR / HAT / SCUNet, ``swin_sr.py``), Omni-SR
-(``omnisr.py``) and DAT (``dat.py``). Every 3x3 conv is a
+(``omnisr.py``), DAT (``dat.py``) and the LaMa inpainter (``lama.py``). Every 3x3 conv is a
 ``layers.Conv2d`` so on the device it runs as the NHWC implicit-GEMM MFMA kernel (bias fused);
 the state dict is re-keyed to the old-arch ``model.N`` layout the reference uses, so any file
-that loads there loads here. Other chaiNNer architectures (LaMa, GFPGAN/CodeFormer/RestoreFormer) are detected by the same key probes and
+that loads there loads here. Other chaiNNer architectures (GFPGAN/CodeFormer/RestoreFormer) are detected by the same key probes and
 rejected with ``UnsupportedModel`` naming the architecture.
 """
 from __future__ import annotations
@@ -368,7 +368,6 @@ _UNSUPPORTED_PROBES = [
     ("GFPGAN", lambda k: "toRGB.0.weight" in k and "stylegan_decoder.style_mlp.1.weight" in k),
     ("RestoreFormer", lambda k: "encoder.conv_in.weight" in k and "encoder.down.0.block.0.norm1.weight" in k),
     ("CodeFormer", lambda k: "encoder.blocks.0.weight" in k and "quantize.embedding.weight" in k),
-    ("LaMa", lambda k: "model.model.1.bn_l.running_mean" in k or "generator.model.1.bn_l.running_mean" in k),
 ]
 
 
@@ -394,20 +393,23 @@ def load_state_dict(state_dict) -> nn.Module:
         except (KeyError, ValueError, RuntimeError) as e:
             raise UnsupportedModel(f"malformed Swin-family upscale model: {e!r}") from e
     if "layers.0.blocks.2.attn.attn_mask_0" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer", "LaMa")):
+            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer")):
         from .dat import DAT
         try:
             return DAT(state_dict)
         except (KeyError, ValueError) as e:
             raise UnsupportedModel(f"malformed DAT upscale model: {e!r}") from e
     if "residual_layer.0.residual_layer.0.layer.0.fn.0.weight" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer", "LaMa")):
+            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer")):
         from .omnisr import OmniSR
         return OmniSR(state_dict)
     if "m_head.0.weight" in keys and "m_tail.0.weight" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer", "LaMa")):
+            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer")):
         from . import swin_sr
         return swin_sr.SCUNet(state_dict)
+    if "model.model.1.bn_l.running_mean" in keys or "generator.model.1.bn_l.running_mean" in keys:
+        from .lama import LaMa
+        return LaMa(state_dict)
     for name, probe in _UNSUPPORTED_PROBES:
         if probe(keys):
             raise UnsupportedModel(f"{name} upscale models are not supported")

@@ -161,6 +161,28 @@ elif which == "dat":
     r = R(seed).eval()
     assert r.split_size == [4, 8]
     check_upscaler(r, seed, torch.rand(1, 3, 20, 28), which)
+elif which == "lama":
+    # torchvision is not installed: the reference only needs it for a rotation wrapper that the
+    # released config never instantiates, so a stub module satisfies the import
+    tv = types.ModuleType("torchvision"); tvt = types.ModuleType("torchvision.transforms")
+    tvf = types.ModuleType("torchvision.transforms.functional")
+    tvf.InterpolationMode = types.SimpleNamespace(BILINEAR=2); tvf.rotate = None
+    sys.modules.update({"torchvision": tv, "torchvision.transforms": tvt, "torchvision.transforms.functional": tvf})
+    from comfy_extras.chainner_models.architecture.LaMa import LaMa as R
+    from comfy_gen_server_amd.models import upscalers as U
+    from comfy_gen_server_amd.models.lama import LaMa
+    m = LaMa({}, strict=False); init_random_(m, seed=7)
+    with torch.no_grad():
+        for k, v in m.state_dict().items():
+            if "running_var" in k:
+                v.abs_().add_(0.5)
+    sd = {k.replace("model.model", "generator.model"): v for k, v in m.state_dict().items()}
+    r = R(sd).eval()
+    m = U.load_state_dict(sd)
+    assert type(m).__name__ == "LaMa"
+    img = torch.rand(1, 3, 64, 48); mask = (torch.rand(1, 1, 64, 48) > 0.5).float()
+    with torch.no_grad():
+        print(which, close(m(img, mask), r(img, mask), tol=1e-3))
 elif which == "scunet":
     from comfy_extras.chainner_models.architecture.SCUNet import SCUNet as R
     from comfy_gen_server_amd.models import swin_sr, upscalers as U
@@ -234,7 +256,7 @@ elif which.startswith(("swinir", "swin2sr", "hat")):
 
 @pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
                                    "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
-                                   "hat", "scunet", "omnisr", "dat"])
+                                   "hat", "scunet", "omnisr", "dat", "lama"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

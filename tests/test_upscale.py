@@ -232,3 +232,40 @@ def test_swin_family_gpu(cuda, kind):
         y = g(x.to(cuda, torch.bfloat16)).float().cpu()
     assert ops.stats().get(("gemm", "hip"), 0) + ops.stats().get(("gemm", "lib"), 0) > 0
     assert ((y - ref).norm() / ref.norm()).item() < 3e-2
+
+
+def _random_lama():
+    from comfy_gen_server_amd.models.lama import LaMa
+    from comfy_gen_server_amd.models.layers import init_random_
+    m = LaMa({}, strict=False)
+    init_random_(m, seed=2)
+    with torch.no_grad():
+        for k, v in m.state_dict().items():
+            if "running_var" in k:
+                v.abs_().add_(0.5)
+    return {k.replace("model.model", "generator.model"): v.clone() for k, v in m.state_dict().items()}
+
+
+def test_lama_dispatch_keeps_unmasked_pixels():
+    m = upscalers.load_state_dict(_random_lama())
+    assert m.model_arch == "LaMa" and m.scale == 1
+    img = torch.rand(1, 3, 32, 40)
+    mask = torch.zeros(1, 1, 32, 40)
+    mask[..., 8:20, 10:30] = 1
+    with torch.no_grad():
+        y = m(img, mask)
+    assert y.shape == img.shape
+    assert torch.equal(y[..., :8, :], img[..., :8, :])          # outside the hole: untouched
+
+
+@pytest.mark.gpu
+def test_lama_gpu(cuda):
+    """FFC generator in bf16 on the device (spectral path in fp32 via rocFFT) vs fp32 CPU."""
+    m = upscalers.load_state_dict(_random_lama())
+    img = torch.rand(1, 3, 64, 64)
+    mask = (torch.rand(1, 1, 64, 64) > 0.5).float()
+    with torch.no_grad():
+        ref = m(img, mask)
+        g = m.to(device=cuda, dtype=torch.bfloat16)
+        y = g(img.to(cuda, torch.bfloat16), mask.to(cuda, torch.bfloat16)).float().cpu()
+    assert ((y - ref).norm() / ref.norm()).item() < 3e-2
