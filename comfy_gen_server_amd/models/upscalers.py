@@ -365,7 +365,6 @@ class SwiftSRGAN(nn.Module):
 
 
 _UNSUPPORTED_PROBES = [
-    ("GFPGAN", lambda k: "toRGB.0.weight" in k and "stylegan_decoder.style_mlp.1.weight" in k),
     ("RestoreFormer", lambda k: "encoder.conv_in.weight" in k and "encoder.down.0.block.0.norm1.weight" in k),
     ("CodeFormer", lambda k: "encoder.blocks.0.weight" in k and "quantize.embedding.weight" in k),
 ]
@@ -384,6 +383,9 @@ def load_state_dict(state_dict) -> nn.Module:
         return SPSRNet(state_dict)
     if "model" in keys and isinstance(state_dict["model"], dict) and "initial.cnn.depthwise.weight" in state_dict["model"]:
         return SwiftSRGAN(state_dict)
+    if "toRGB.0.weight" in keys and "stylegan_decoder.style_mlp.1.weight" in keys:
+        from .face import GFPGANv1Clean
+        return GFPGANv1Clean(state_dict)
     if "layers.0.residual_group.blocks.0.norm1.weight" in keys:
         from . import swin_sr
         try:
@@ -393,18 +395,18 @@ def load_state_dict(state_dict) -> nn.Module:
         except (KeyError, ValueError, RuntimeError) as e:
             raise UnsupportedModel(f"malformed Swin-family upscale model: {e!r}") from e
     if "layers.0.blocks.2.attn.attn_mask_0" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer")):
+            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("RestoreFormer", "CodeFormer")):
         from .dat import DAT
         try:
             return DAT(state_dict)
         except (KeyError, ValueError) as e:
             raise UnsupportedModel(f"malformed DAT upscale model: {e!r}") from e
     if "residual_layer.0.residual_layer.0.layer.0.fn.0.weight" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer")):
+            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("RestoreFormer", "CodeFormer")):
         from .omnisr import OmniSR
         return OmniSR(state_dict)
     if "m_head.0.weight" in keys and "m_tail.0.weight" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("GFPGAN", "RestoreFormer", "CodeFormer")):
+            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("RestoreFormer", "CodeFormer")):
         from . import swin_sr
         return swin_sr.SCUNet(state_dict)
     if "model.model.1.bn_l.running_mean" in keys or "generator.model.1.bn_l.running_mean" in keys:

@@ -32,6 +32,11 @@ class UpscaleModelLoader:
         return (upscalers.load_state_dict(sd).eval(),)
 
 
+def _first(out):
+    """Face-restoration nets return (image, aux...) like the reference architectures."""
+    return out[0] if isinstance(out, (tuple, list)) else out
+
+
 class ImageUpscaleWithModel:
     RETURN_TYPES = ("IMAGE",)
     FUNCTION = "upscale"
@@ -52,7 +57,7 @@ class ImageUpscaleWithModel:
                 steps = x.shape[0] * U.get_tiled_scale_steps(x.shape[3], x.shape[2], tile, tile, overlap)
                 pbar = ProgressBar(steps)
                 with torch.inference_mode():
-                    s = U.tiled_scale(x, lambda a: upscale_model(a).float(), tile_x=tile, tile_y=tile,
+                    s = U.tiled_scale(x, lambda a: _first(upscale_model(a)).float(), tile_x=tile, tile_y=tile,
                                       overlap=overlap, upscale_amount=upscale_model.scale, pbar=pbar,
                                       output_device=dm.intermediate_device())
                 break

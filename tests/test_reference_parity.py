@@ -183,6 +183,20 @@ elif which == "lama":
     img = torch.rand(1, 3, 64, 48); mask = (torch.rand(1, 1, 64, 48) > 0.5).float()
     with torch.no_grad():
         print(which, close(m(img, mask), r(img, mask), tol=1e-3))
+elif which == "gfpgan":
+    from comfy_extras.chainner_models.architecture.face.gfpganv1_clean_arch import GFPGANv1Clean as R
+    from comfy_gen_server_amd.models import upscalers as U
+    from comfy_gen_server_amd.models.face import GFPGANv1Clean
+    m = GFPGANv1Clean({}, strict=False); init_random_(m, seed=8, std_scale=0.5)
+    sd = m.state_dict()
+    r = R(sd).eval()                       # strict load on the reference side
+    m = U.load_state_dict(sd)
+    x = torch.rand(1, 3, 512, 512) * 2 - 1
+    with torch.no_grad():
+        a, rgbs_a = m(x, randomize_noise=False)
+        b, rgbs_b = r(x, randomize_noise=False)
+    assert len(rgbs_a) == len(rgbs_b) == 7
+    print(which, close(a, b, tol=2e-3), close(rgbs_a[-1], rgbs_b[-1], tol=2e-3))
 elif which == "scunet":
     from comfy_extras.chainner_models.architecture.SCUNet import SCUNet as R
     from comfy_gen_server_amd.models import swin_sr, upscalers as U
@@ -256,7 +270,7 @@ elif which.startswith(("swinir", "swin2sr", "hat")):
 
 @pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
                                    "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
-                                   "hat", "scunet", "omnisr", "dat", "lama"])
+                                   "hat", "scunet", "omnisr", "dat", "lama", "gfpgan"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

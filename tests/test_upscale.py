@@ -269,3 +269,41 @@ def test_lama_gpu(cuda):
         g = m.to(device=cuda, dtype=torch.bfloat16)
         y = g(img.to(cuda, torch.bfloat16), mask.to(cuda, torch.bfloat16)).float().cpu()
     assert ((y - ref).norm() / ref.norm()).item() < 3e-2
+
+
+def _random_gfpgan():
+    from comfy_gen_server_amd.models.face import GFPGANv1Clean
+    from comfy_gen_server_amd.models.layers import init_random_
+    m = GFPGANv1Clean({}, strict=False)
+    init_random_(m, seed=3, std_scale=0.5)
+    return {k: v.clone() for k, v in m.state_dict().items()}
+
+
+def test_gfpgan_dispatch_and_activation_modulation():
+    """Activation-side modulation == the per-sample modulated-weight grouped conv (batch of 2)."""
+    from comfy_gen_server_amd.models.face import ModulatedConv2d
+    m = upscalers.load_state_dict(_random_gfpgan())
+    assert m.model_arch == "GFPGAN" and m.scale == 8
+    mc = ModulatedConv2d(16, 8, 3, 12, demodulate=True, sample_mode="upsample")
+    torch.nn.init.normal_(mc.modulation.weight)
+    torch.nn.init.normal_(mc.modulation.bias)
+    x, st = torch.randn(2, 16, 5, 6), torch.randn(2, 12)
+    s = F.linear(st, mc.modulation.weight, mc.modulation.bias).view(2, 1, 16, 1, 1)
+    w = mc.weight * s
+    w = w * torch.rsqrt(w.pow(2).sum([2, 3, 4]) + 1e-8).view(2, 8, 1, 1, 1)
+    xu = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+    ref = F.conv2d(xu.reshape(1, 32, 10, 12), w.view(16, 16, 3, 3), padding=1, groups=2).view(2, 8, 10, 12)
+    with torch.no_grad():
+        assert torch.allclose(mc(x, st), ref, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_gfpgan_gpu(cuda):
+    m = upscalers.load_state_dict(_random_gfpgan())
+    x = torch.rand(1, 3, 512, 512) * 2 - 1
+    with torch.no_grad():
+        ref, _ = m(x, randomize_noise=False)
+        g = m.to(device=cuda, dtype=torch.bfloat16)
+        y, _ = g(x.to(cuda, torch.bfloat16), randomize_noise=False)
+    y = y.float().cpu()
+    assert ((y - ref).norm() / ref.norm()).item() < 3e-2
