@@ -220,3 +220,325 @@ class GFPGANv1Clean(nn.Module):
                 rgbs.append(self.toRGB[i](feat))
         image = self.stylegan_decoder(latent, conditions, randomize_noise=randomize_noise)
         return image, rgbs
+
+
+# ----------------------------------------------------------------------------------------------
+# RestoreFormer (restoreformer_arch.py): VQGAN-style encoder -> 1024-entry codebook -> decoder
+# whose 16x16 attention layers cross-attend from the encoder's features (multi-head, d=64).
+# ----------------------------------------------------------------------------------------------
+
+from . import vae as _vae  # noqa: E402  (ResnetBlock / Downsample / Upsample share the ldm key layout)
+from .layers import GroupNorm, LayerNorm  # noqa: E402
+
+
+def _gn(c):
+    return GroupNorm(32, c, eps=1e-6)
+
+
+def _tokens(x):
+    return x.flatten(2).transpose(1, 2)
+
+
+def _image(t, like):
+    B, C, H, W = like.shape
+    return t.transpose(1, 2).reshape(B, C, H, W)
+
+
+class _MHAttnBlock(nn.Module):
+    """Multi-head (cross-)attention over the spatial positions: q from ``y`` (or ``x``), k/v from
+    ``x``; the device runs it on the HIP flash-attention kernel."""
+
+    def __init__(self, c, heads):
+        super().__init__()
+        self.heads = heads
+        self.norm1, self.norm2 = _gn(c), _gn(c)
+        self.q, self.k, self.v, self.proj_out = (Conv2d(c, c, 1) for _ in range(4))
+
+    def forward(self, x, y=None):
+        h = self.norm1(x)
+        yq = h if y is None else self.norm2(y)
+        o = ops.attention(_tokens(self.q(yq)), _tokens(self.k(h)), _tokens(self.v(h)), self.heads)
+        return self.proj_out(_image(o, x), residual=x)
+
+
+def _quantize(z, codebook):
+    """Nearest codebook entry per position (z [B, C, H, W], codebook [n, C])."""
+    B, C, H, W = z.shape
+    zf = z.permute(0, 2, 3, 1).reshape(-1, C).float()
+    cb = codebook.float()
+    d = zf.pow(2).sum(1, keepdim=True) + cb.pow(2).sum(1) - 2 * zf @ cb.t()
+    idx = d.argmin(1)
+    return codebook[idx].view(B, H, W, C).permute(0, 3, 1, 2).to(z.dtype)
+
+
+class RestoreFormer(nn.Module):
+    def __init__(self, state_dict, strict: bool = True):
+        super().__init__()
+        self.model_arch = "RestoreFormer"
+        self.sub_type = "Face SR"
+        self.scale, self.in_nc, self.out_nc = 8, 3, 3
+        ch, mult, nrb, heads, z = 64, (1, 2, 2, 4, 4, 8), 2, 8, 256
+        self.nrb = nrb
+        enc = nn.Module()
+        enc.conv_in = Conv2d(3, ch, 3, padding=1)
+        enc.down = nn.ModuleList()
+        res, cin = 512, ch
+        for i, m in enumerate(mult):
+            lvl = nn.Module()
+            lvl.block, lvl.attn = nn.ModuleList(), nn.ModuleList()
+            for _ in range(nrb):
+                lvl.block.append(_vae.ResnetBlock(cin, ch * m))
+                cin = ch * m
+                if res == 16:
+                    lvl.attn.append(_MHAttnBlock(cin, heads))
+            if i != len(mult) - 1:
+                lvl.downsample = _vae.Downsample(cin)
+                res //= 2
+            enc.down.append(lvl)
+        enc.mid = nn.Module()
+        enc.mid.block_1, enc.mid.attn_1, enc.mid.block_2 = (_vae.ResnetBlock(cin), _MHAttnBlock(cin, heads),
+                                                            _vae.ResnetBlock(cin))
+        enc.norm_out = _gn(cin)
+        enc.conv_out = Conv2d(cin, z, 3, padding=1)
+        self.encoder = enc
+        dec = nn.Module()
+        dec.conv_in = Conv2d(z, cin, 3, padding=1)
+        dec.mid = nn.Module()
+        dec.mid.block_1, dec.mid.attn_1, dec.mid.block_2 = (_vae.ResnetBlock(cin), _MHAttnBlock(cin, heads),
+                                                            _vae.ResnetBlock(cin))
+        ups = []
+        res = 16
+        for i in reversed(range(len(mult))):
+            lvl = nn.Module()
+            lvl.block, lvl.attn = nn.ModuleList(), nn.ModuleList()
+            for _ in range(nrb + 1):
+                lvl.block.append(_vae.ResnetBlock(cin, ch * mult[i]))
+                cin = ch * mult[i]
+                if res == 16:
+                    lvl.attn.append(_MHAttnBlock(cin, heads))
+            if i != 0:
+                lvl.upsample = _vae.Upsample(cin)
+                res *= 2
+            ups.insert(0, lvl)
+        dec.up = nn.ModuleList(ups)
+        dec.norm_out = _gn(cin)
+        dec.conv_out = Conv2d(cin, 3, 3, padding=1)
+        self.decoder = dec
+        self.quantize = nn.Module()
+        self.quantize.embedding = nn.Embedding(1024, 256)
+        self.quant_conv = Conv2d(z, 256, 1)
+        self.post_quant_conv = Conv2d(256, z, 1)
+        for p in self.parameters():
+            p.requires_grad_(False)
+        missing, _ = self.load_state_dict(state_dict, strict=False)
+        if missing and strict:
+            raise ValueError(f"RestoreFormer: missing keys {missing[:4]}")
+        self.eval()
+
+    def forward(self, x, **_):
+        e, hs = self.encoder, {}
+        h = e.conv_in(x)
+        last = len(e.down) - 1
+        for i, lvl in enumerate(e.down):
+            for j in range(self.nrb):
+                h = lvl.block[j](h)
+                if len(lvl.attn):
+                    h = lvl.attn[j](h)
+            if i != last:
+                h = lvl.downsample(h)
+        h = e.mid.block_1(h)
+        hs_block = h                                   # "block_{last}_atten"
+        h = e.mid.block_2(e.mid.attn_1(h))
+        hs_mid = h                                     # "mid_atten"
+        h = e.conv_out(e.norm_out(h, silu=True))
+        q = _quantize(self.quant_conv(h), self.quantize.embedding.weight)
+        d = self.decoder
+        h = d.conv_in(self.post_quant_conv(q))
+        h = d.mid.block_2(d.mid.attn_1(d.mid.block_1(h), hs_mid))
+        for i in reversed(range(len(d.up))):
+            lvl = d.up[i]
+            for j in range(self.nrb + 1):
+                h = lvl.block[j](h)
+                if len(lvl.attn):
+                    h = lvl.attn[j](h, hs_block)
+            if i != 0:
+                h = lvl.upsample(h)
+        return d.conv_out(d.norm_out(h, silu=True)), None
+
+
+# ----------------------------------------------------------------------------------------------
+# CodeFormer (codeformer.py): VQGAN encoder -> 9-layer transformer predicting codebook indices
+# from the low-quality latent -> AdaIN-matched codebook features -> generator with
+# controllable-fidelity SFT fusion of encoder features at 32..256 px.
+# ----------------------------------------------------------------------------------------------
+
+
+class _CFResBlock(nn.Module):
+    def __init__(self, cin, cout=None):
+        super().__init__()
+        cout = cout or cin
+        self.norm1, self.conv1 = _gn(cin), Conv2d(cin, cout, 3, padding=1)
+        self.norm2, self.conv2 = _gn(cout), Conv2d(cout, cout, 3, padding=1)
+        self.conv_out = Conv2d(cin, cout, 1) if cin != cout else None
+
+    def forward(self, x):
+        h = self.conv1(self.norm1(x, silu=True))
+        skip = x if self.conv_out is None else self.conv_out(x)
+        return self.conv2(self.norm2(h, silu=True), residual=skip)
+
+
+class _CFAttn(nn.Module):
+    """Single-head spatial self-attention (d = C = 512 at 16x16: the wide-head HIP kernel)."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.norm = _gn(c)
+        self.q, self.k, self.v, self.proj_out = (Conv2d(c, c, 1) for _ in range(4))
+
+    def forward(self, x):
+        h = self.norm(x)
+        o = ops.attention(_tokens(self.q(h)), _tokens(self.k(h)), _tokens(self.v(h)), 1)
+        return self.proj_out(_image(o, x), residual=x)
+
+
+def _vq_blocks(nf, mult, nrb, emb_dim, encoder: bool):
+    blocks: list = []
+    if encoder:
+        res, cin = 512, nf
+        blocks.append(Conv2d(3, nf, 3, padding=1))
+        for i, m in enumerate(mult):
+            for _ in range(nrb):
+                blocks.append(_CFResBlock(cin, nf * m))
+                cin = nf * m
+                if res == 16:
+                    blocks.append(_CFAttn(cin))
+            if i != len(mult) - 1:
+                blocks.append(_vae.Downsample(cin))
+                res //= 2
+        blocks += [_CFResBlock(cin), _CFAttn(cin), _CFResBlock(cin), _gn(cin), Conv2d(cin, emb_dim, 3, padding=1)]
+    else:
+        cin, res = nf * mult[-1], 512 // 2 ** (len(mult) - 1)
+        blocks += [Conv2d(emb_dim, cin, 3, padding=1), _CFResBlock(cin), _CFAttn(cin), _CFResBlock(cin)]
+        for i in reversed(range(len(mult))):
+            for _ in range(nrb):
+                blocks.append(_CFResBlock(cin, nf * mult[i]))
+                cin = nf * mult[i]
+                if res == 16:
+                    blocks.append(_CFAttn(cin))
+            if i != 0:
+                blocks.append(_vae.Upsample(cin))
+                res *= 2
+        blocks += [_gn(cin), Conv2d(cin, 3, 3, padding=1)]
+    m = nn.Module()
+    m.blocks = nn.ModuleList(blocks)
+    return m
+
+
+class _SALayer(nn.Module):
+    """Pre-norm transformer layer; the attention keeps ``nn.MultiheadAttention``'s packed
+    ``in_proj`` weights (keys ``self_attn.in_proj_weight`` / ``out_proj``)."""
+
+    def __init__(self, dim, heads, mlp):
+        super().__init__()
+        self.heads = heads
+        self.self_attn = nn.Module()
+        self.self_attn.in_proj_weight = nn.Parameter(torch.empty(3 * dim, dim), requires_grad=False)
+        self.self_attn.in_proj_bias = nn.Parameter(torch.empty(3 * dim), requires_grad=False)
+        self.self_attn.out_proj = Linear(dim, dim)
+        self.linear1, self.linear2 = Linear(dim, mlp), Linear(mlp, dim)
+        self.norm1, self.norm2 = LayerNorm(dim), LayerNorm(dim)
+
+    def forward(self, t, pos):                           # t [B, S, D] (batch-first)
+        D = t.shape[-1]
+        w, b = self.self_attn.in_proj_weight.to(t.dtype), self.self_attn.in_proj_bias.to(t.dtype)
+        h = self.norm1(t)
+        qk = ops.linear(h + pos, w[:2 * D], b[:2 * D])       # q and k share their input: one GEMM
+        v = ops.linear(h, w[2 * D:], b[2 * D:])
+        a = ops.attention(qk[..., :D], qk[..., D:], v, self.heads)
+        t = self.self_attn.out_proj(a, residual=t)
+        return self.linear2(F.gelu(self.linear1(self.norm2(t))), residual=t)
+
+
+def _mean_std(f, eps=1e-5):
+    b, c = f.shape[:2]
+    v = f.float().reshape(b, c, -1)
+    return v.mean(2).view(b, c, 1, 1), (v.var(2) + eps).sqrt().view(b, c, 1, 1)
+
+
+def _adain(content, style):
+    cm, cs = _mean_std(content)
+    sm, ss = _mean_std(style)
+    return ((content.float() - cm) / cs * ss + sm).to(content.dtype)
+
+
+class _FuseSFT(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.encode_enc = _CFResBlock(2 * c, c)
+        self.scale = nn.Sequential(Conv2d(c, c, 3, padding=1), nn.LeakyReLU(0.2), Conv2d(c, c, 3, padding=1))
+        self.shift = nn.Sequential(Conv2d(c, c, 3, padding=1), nn.LeakyReLU(0.2), Conv2d(c, c, 3, padding=1))
+
+    def forward(self, enc, dec, w):
+        e = self.encode_enc(torch.cat([enc, dec], 1))
+        return dec + w * (dec * self.scale(e) + self.shift(e))
+
+
+class CodeFormer(nn.Module):
+    _ENC_TAP = {"512": 2, "256": 5, "128": 8, "64": 11, "32": 14, "16": 18}
+    _GEN_TAP = {"16": 6, "32": 9, "64": 12, "128": 15, "256": 18, "512": 21}
+    _CONNECT = ("32", "64", "128", "256")
+    _CH = {"16": 512, "32": 256, "64": 256, "128": 128, "256": 128, "512": 64}
+
+    def __init__(self, state_dict, strict: bool = True):
+        super().__init__()
+        sd = state_dict
+        self.model_arch = "CodeFormer"
+        self.sub_type = "Face SR"
+        self.scale = 8
+        dim = sd["position_emb"].shape[1] if "position_emb" in sd else 512
+        latent = sd["position_emb"].shape[0] if "position_emb" in sd else 256
+        n_layers = len({k.split(".")[1] for k in sd if k.startswith("ft_layers.")}) or 9
+        n_code = sd["quantize.embedding.weight"].shape[0] if "quantize.embedding.weight" in sd else 1024
+        self.in_nc = self.out_nc = sd["encoder.blocks.0.weight"].shape[1] if "encoder.blocks.0.weight" in sd else 3
+        mult = (1, 2, 2, 4, 4, 8)
+        self.encoder = _vq_blocks(64, mult, 2, 256, encoder=True)
+        self.quantize = nn.Module()
+        self.quantize.embedding = nn.Embedding(n_code, 256)
+        self.generator = _vq_blocks(64, mult, 2, 256, encoder=False)
+        self.position_emb = nn.Parameter(torch.zeros(latent, dim), requires_grad=False)
+        self.feat_emb = Linear(256, dim)
+        self.ft_layers = nn.Sequential(*[_SALayer(dim, 8, dim * 2) for _ in range(n_layers)])
+        self.idx_pred_layer = nn.Sequential(LayerNorm(dim), Linear(dim, n_code, bias=False))
+        self.fuse_convs_dict = nn.ModuleDict({s: _FuseSFT(self._CH[s]) for s in self._CONNECT})
+        for p in self.parameters():
+            p.requires_grad_(False)
+        missing, _ = self.load_state_dict(sd, strict=False)
+        if missing and strict:
+            raise ValueError(f"CodeFormer: missing keys {missing[:4]}")
+        self.eval()
+
+    def forward(self, x, weight=0.5, **_):
+        taps = {self._ENC_TAP[s] for s in self._CONNECT}
+        enc = {}
+        for i, blk in enumerate(self.encoder.blocks):
+            x = blk(x)
+            if i in taps:
+                enc[str(x.shape[-1])] = x
+        lq = x
+        B = x.shape[0]
+        t = self.feat_emb(_tokens(lq))
+        pos = self.position_emb.to(t.dtype)[None]
+        for layer in self.ft_layers:
+            t = layer(t, pos)
+        logits = self.idx_pred_layer(t)                               # [B, hw, n_code]
+        idx = logits.float().argmax(-1)                               # top-1 of the softmax
+        side = int(math.isqrt(t.shape[1]))
+        q = self.quantize.embedding.weight[idx].to(lq.dtype).view(B, side, side, -1).permute(0, 3, 1, 2)
+        x = _adain(q, lq)
+        fuse_at = {self._GEN_TAP[s] for s in self._CONNECT}
+        for i, blk in enumerate(self.generator.blocks):
+            x = blk(x)
+            if i in fuse_at and weight > 0:
+                s = str(x.shape[-1])
+                x = self.fuse_convs_dict[s](enc[s], x, weight)
+        return x, logits

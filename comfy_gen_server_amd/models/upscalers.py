@@ -1,14 +1,14 @@
 """Image super-resolution networks for ``UpscaleModelLoader`` (parity: ``comfy_extras/chainner_models/
 model_loading.py:24-99`` dispatch, ``architecture/RRDB.py`` and ``architecture/SRVGG.py``).
 
-Supported here: ESRGAN / Real-ESRGAN (RRDBNet, old and new key layouts, x1/x2 pixel-unshuffle
-variants, scale 1-8), Real-ESRGAN compact (SRVGGNetCompact), SPSR, Swift-SRGAN, and the
-Swin-transformer family (SwinIR / Swin2SR / HAT / SCUNet, ``swin_sr.py``), Omni-SR
-(``omnisr.py``), DAT (``dat.py``) and the LaMa inpainter (``lama.py``). Every 3x3 conv is a
+Every architecture the reference dispatches is implemented: ESRGAN / Real-ESRGAN (RRDBNet, old and
+new key layouts, x1/x2 pixel-unshuffle variants, scale 1-8), Real-ESRGAN compact
+(SRVGGNetCompact), SPSR and Swift-SRGAN (here); SwinIR / Swin2SR / HAT / SCUNet (``swin_sr.py``),
+Omni-SR (``omnisr.py``), DAT (``dat.py``), the LaMa inpainter (``lama.py``) and the face
+restorers GFPGAN / RestoreFormer / CodeFormer (``face.py``). Every 3x3 conv is a
 ``layers.Conv2d`` so on the device it runs as the NHWC implicit-GEMM MFMA kernel (bias fused);
 the state dict is re-keyed to the old-arch ``model.N`` layout the reference uses, so any file
-that loads there loads here. Other chaiNNer architectures (GFPGAN/CodeFormer/RestoreFormer) are detected by the same key probes and
-rejected with ``UnsupportedModel`` naming the architecture.
+that loads there loads here.
 """
 from __future__ import annotations
 
@@ -364,57 +364,54 @@ class SwiftSRGAN(nn.Module):
         return (torch.tanh(self.final_conv(h)) + 1) / 2
 
 
-_UNSUPPORTED_PROBES = [
-    ("RestoreFormer", lambda k: "encoder.conv_in.weight" in k and "encoder.down.0.block.0.norm1.weight" in k),
-    ("CodeFormer", lambda k: "encoder.blocks.0.weight" in k and "quantize.embedding.weight" in k),
-]
+def _probe(keys: set, state_dict: dict):
+    """(name, constructor) of the architecture whose signature keys are present — the
+    reference's dispatch order (model_loading.py:38-95); None means "try ESRGAN"."""
+    from . import dat, face, lama, omnisr, swin_sr
+    if "body.0.weight" in keys and "body.1.weight" in keys:
+        return "RealESRGAN-Compact", SRVGGNetCompact
+    if "f_HR_conv1.0.weight" in keys:
+        return "SPSR", SPSRNet
+    if "model" in keys and isinstance(state_dict["model"], dict) and "initial.cnn.depthwise.weight" in state_dict["model"]:
+        return "Swift-SRGAN", SwiftSRGAN
+    if "layers.0.residual_group.blocks.0.norm1.weight" in keys:
+        if "layers.0.residual_group.blocks.0.conv_block.cab.0.weight" in keys:
+            return "HAT", swin_sr.HAT
+        if "patch_embed.proj.weight" in keys:
+            return "Swin2SR", lambda sd: swin_sr.SwinIR(sd, v2=True)
+        return "SwinIR", swin_sr.SwinIR
+    if "toRGB.0.weight" in keys and "stylegan_decoder.style_mlp.1.weight" in keys:
+        return "GFPGAN", face.GFPGANv1Clean
+    if "encoder.conv_in.weight" in keys and "encoder.down.0.block.0.norm1.weight" in keys:
+        return "RestoreFormer", face.RestoreFormer
+    if "encoder.blocks.0.weight" in keys and "quantize.embedding.weight" in keys:
+        return "CodeFormer", face.CodeFormer
+    if "model.model.1.bn_l.running_mean" in keys or "generator.model.1.bn_l.running_mean" in keys:
+        return "LaMa", lama.LaMa
+    if "residual_layer.0.residual_layer.0.layer.0.fn.0.weight" in keys:
+        return "OmniSR", omnisr.OmniSR
+    if "m_head.0.weight" in keys and "m_tail.0.weight" in keys:
+        return "SCUNet", swin_sr.SCUNet
+    if "layers.0.blocks.2.attn.attn_mask_0" in keys:
+        return "DAT", dat.DAT
+    return None
 
 
 def load_state_dict(state_dict) -> nn.Module:
-    """Architecture dispatch by key probes, in the reference's order."""
+    """Architecture dispatch by key probes, in the reference's order. A recognised family whose
+    file is malformed (missing / mis-shaped tensors) raises ``UnsupportedModel`` naming it."""
     for wrap in ("params_ema", "params-ema", "params"):
         if wrap in state_dict and isinstance(state_dict[wrap], dict):
             state_dict = state_dict[wrap]
             break
     keys = set(state_dict.keys())
-    if "body.0.weight" in keys and "body.1.weight" in keys:
-        return SRVGGNetCompact(state_dict)
-    if "f_HR_conv1.0.weight" in keys:
-        return SPSRNet(state_dict)
-    if "model" in keys and isinstance(state_dict["model"], dict) and "initial.cnn.depthwise.weight" in state_dict["model"]:
-        return SwiftSRGAN(state_dict)
-    if "toRGB.0.weight" in keys and "stylegan_decoder.style_mlp.1.weight" in keys:
-        from .face import GFPGANv1Clean
-        return GFPGANv1Clean(state_dict)
-    if "layers.0.residual_group.blocks.0.norm1.weight" in keys:
-        from . import swin_sr
+    hit = _probe(keys, state_dict)
+    if hit is not None:
+        name, ctor = hit
         try:
-            if "layers.0.residual_group.blocks.0.conv_block.cab.0.weight" in keys:
-                return swin_sr.HAT(state_dict)
-            return swin_sr.SwinIR(state_dict, v2="patch_embed.proj.weight" in keys)
-        except (KeyError, ValueError, RuntimeError) as e:
-            raise UnsupportedModel(f"malformed Swin-family upscale model: {e!r}") from e
-    if "layers.0.blocks.2.attn.attn_mask_0" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("RestoreFormer", "CodeFormer")):
-        from .dat import DAT
-        try:
-            return DAT(state_dict)
-        except (KeyError, ValueError) as e:
-            raise UnsupportedModel(f"malformed DAT upscale model: {e!r}") from e
-    if "residual_layer.0.residual_layer.0.layer.0.fn.0.weight" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("RestoreFormer", "CodeFormer")):
-        from .omnisr import OmniSR
-        return OmniSR(state_dict)
-    if "m_head.0.weight" in keys and "m_tail.0.weight" in keys and not any(
-            p(keys) for n, p in _UNSUPPORTED_PROBES if n in ("RestoreFormer", "CodeFormer")):
-        from . import swin_sr
-        return swin_sr.SCUNet(state_dict)
-    if "model.model.1.bn_l.running_mean" in keys or "generator.model.1.bn_l.running_mean" in keys:
-        from .lama import LaMa
-        return LaMa(state_dict)
-    for name, probe in _UNSUPPORTED_PROBES:
-        if probe(keys):
-            raise UnsupportedModel(f"{name} upscale models are not supported")
+            return ctor(state_dict)
+        except (KeyError, ValueError, RuntimeError, IndexError) as e:
+            raise UnsupportedModel(f"malformed {name} upscale model: {e!r}") from e
     try:
         return RRDBNet(state_dict)
     except UnsupportedModel:

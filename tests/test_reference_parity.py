@@ -197,6 +197,27 @@ elif which == "gfpgan":
         b, rgbs_b = r(x, randomize_noise=False)
     assert len(rgbs_a) == len(rgbs_b) == 7
     print(which, close(a, b, tol=2e-3), close(rgbs_a[-1], rgbs_b[-1], tol=2e-3))
+elif which in ("restoreformer", "codeformer"):
+    from comfy_gen_server_amd.models import upscalers as U
+    from comfy_gen_server_amd.models import face
+    if which == "restoreformer":
+        from comfy_extras.chainner_models.architecture.face.restoreformer_arch import RestoreFormer as R
+        m = face.RestoreFormer({}, strict=False)
+    else:
+        from comfy_extras.chainner_models.architecture.face.codeformer import CodeFormer as R
+        m = face.CodeFormer({}, strict=False)
+    init_random_(m, seed=9, std_scale=0.5)
+    sd = m.state_dict()
+    r = R(sd).eval()                       # strict loads on the reference side
+    m = U.load_state_dict(sd)
+    assert type(m).__name__ == type(r).__name__
+    x = torch.rand(1, 3, 512, 512) * 2 - 1
+    with torch.no_grad():
+        a, la = m(x)
+        b, lb = r(x)
+    if which == "codeformer":
+        assert torch.equal(la.argmax(-1), lb.argmax(-1))       # same code indices
+    print(which, close(a, b, tol=2e-3))
 elif which == "scunet":
     from comfy_extras.chainner_models.architecture.SCUNet import SCUNet as R
     from comfy_gen_server_amd.models import swin_sr, upscalers as U
@@ -270,7 +291,8 @@ elif which.startswith(("swinir", "swin2sr", "hat")):
 
 @pytest.mark.parametrize("which", ["unet", "svd", "vae", "vae_video", "spsr", "swift", "swinir_classic",
                                    "swinir_light", "swinir_real", "swinir_denoise", "swin2sr", "swin2sr_aux",
-                                   "hat", "scunet", "omnisr", "dat", "lama", "gfpgan"])
+                                   "hat", "scunet", "omnisr", "dat", "lama", "gfpgan",
+                                   "restoreformer", "codeformer"])
 def test_matches_reference(which):
     code = f"REF = {REF!r}\nROOT = {ROOT!r}\nimport sys\nsys.argv_which = {which!r}\n" + _SCRIPT
     env = dict(os.environ, CGS_FORCE_CPU="1", PYTHONDONTWRITEBYTECODE="1")

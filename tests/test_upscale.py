@@ -307,3 +307,33 @@ def test_gfpgan_gpu(cuda):
         y, _ = g(x.to(cuda, torch.bfloat16), randomize_noise=False)
     y = y.float().cpu()
     assert ((y - ref).norm() / ref.norm()).item() < 3e-2
+
+
+def _random_face(kind):
+    from comfy_gen_server_amd.models import face
+    from comfy_gen_server_amd.models.layers import init_random_
+    m = face.RestoreFormer({}, strict=False) if kind == "restoreformer" else face.CodeFormer({}, strict=False)
+    init_random_(m, seed=5, std_scale=0.5)
+    return {k: v.clone() for k, v in m.state_dict().items()}
+
+
+@pytest.mark.parametrize("kind", ["restoreformer", "codeformer"])
+def test_face_vq_dispatch(kind):
+    m = upscalers.load_state_dict(_random_face(kind))
+    assert m.model_arch == {"restoreformer": "RestoreFormer", "codeformer": "CodeFormer"}[kind] and m.scale == 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["restoreformer", "codeformer"])
+def test_face_vq_gpu(cuda, kind):
+    """VQ face restorers in bf16 on the device (multi-head / wide-head HIP attention at 16x16)."""
+    from comfy_gen_server_amd import ops
+    m = upscalers.load_state_dict(_random_face(kind))
+    x = torch.rand(1, 3, 512, 512) * 2 - 1
+    with torch.no_grad():
+        g = m.to(device=cuda, dtype=torch.bfloat16)
+        ops.reset_stats()
+        y, _ = g(x.to(cuda, torch.bfloat16))
+    assert ops.stats().get(("attention", "hip"), 0) > 0
+    y = y.float().cpu()
+    assert y.shape == (1, 3, 512, 512) and torch.isfinite(y).all()
