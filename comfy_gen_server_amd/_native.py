@@ -101,6 +101,12 @@ KERNEL_SIGNATURES = {
     "cgs_dwconv_nhwc": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     # conv implicit GEMM NHWC bf16: x[N,H,W,Cin], w[Cout,kh,kw,Cin], bias, residual, out
     "cgs_conv2d_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    # image / utility kernels (csrc/kernels/image.hip)
+    "cgs_fused_bias_act": [_P, _P, _P, _L, _I, _L, _F, _F, _I, _P],   # x, bias, y, n, C, inner, slope, scale
+    "cgs_upfirdn2d": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "cgs_resize": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],        # x, y, NC, H, W, Ho, Wo, mode, align
+    "cgs_vq_nearest": [_P, _P, _P, _P, _I, _I, _I, _I, _P],            # z, codebook, idx(i64), q, M, n, D
+    "cgs_grn_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P],          # x, gamma, beta, y, ws, N, HW, C
     "cgs_gemm_bf16_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
     "cgs_conv2d_nhwc_v": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cgs_conv2d_nhwc_ex": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],

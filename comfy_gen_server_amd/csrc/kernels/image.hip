@@ -1,0 +1,288 @@
+// Image-space and small utility kernels (SURVEY §2.4 K25 resize, K28 GRN, K31 VQ codebook,
+// K32 StyleGAN fused bias-act / upfirdn2d). All are bandwidth-bound: one thread per output
+// element (grid-stride), fp32 accumulation, bf16 / fp16 / fp32 storage selected at run time.
+#include "common.h"
+
+namespace {
+
+template <int DT>
+__device__ __forceinline__ float ldv(const void* p, long long i) {
+  if constexpr (DT == CGS_F32) return reinterpret_cast<const float*>(p)[i];
+  else return cvt_in<DT>(reinterpret_cast<const u16*>(p)[i]);
+}
+
+template <int DT>
+__device__ __forceinline__ void stv(void* p, long long i, float v) {
+  if constexpr (DT == CGS_F32) reinterpret_cast<float*>(p)[i] = v;
+  else reinterpret_cast<u16*>(p)[i] = cvt_out<DT>(v);
+}
+
+inline int grid_for(long long n, int block = 256) {
+  long long g = (n + block - 1) / block;
+  return (int)(g < 65535LL * 8 ? (g < 1 ? 1 : g) : 65535LL * 8);
+}
+
+#define CGS_DISPATCH_DT(dtype, KERNEL, ...)                                        \
+  do {                                                                             \
+    if ((dtype) == CGS_F32) KERNEL<CGS_F32> __VA_ARGS__;                           \
+    else if ((dtype) == CGS_BF16) KERNEL<CGS_BF16> __VA_ARGS__;                    \
+    else if ((dtype) == CGS_F16) KERNEL<CGS_F16> __VA_ARGS__;                      \
+    else return (int)hipErrorInvalidValue;                                         \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// K32a: y = leaky_relu(x + bias[c], slope) * scale   (StyleGAN2 FusedLeakyReLU; c = (i / inner) % C)
+// ---------------------------------------------------------------------------------------------
+template <int DT>
+__global__ void __launch_bounds__(256) fused_bias_act_kernel(const void* x, const void* b, void* y, long long n,
+                                                             int C, long long inner, float slope, float scale) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = ldv<DT>(x, i);
+    if (b) v += ldv<DT>(b, (i / inner) % C);
+    v = (v >= 0.f ? v : v * slope) * scale;
+    stv<DT>(y, i, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K32b: upfirdn2d on planar [NC, H, W]: zero-insert upsample, pad (negative = crop), FIR with the
+// flipped kernel (true convolution), keep every down-th sample. Kernel taps staged in LDS.
+// ---------------------------------------------------------------------------------------------
+template <int DT>
+__global__ void __launch_bounds__(256) upfirdn2d_kernel(const void* x, const float* k, void* y, int NC, int H, int W,
+                                                        int upx, int upy, int dnx, int dny, int px0, int py0,
+                                                        int kh, int kw, int Ho, int Wo) {
+  __shared__ float taps[32 * 32];
+  for (int t = threadIdx.x; t < kh * kw; t += 256) taps[t] = k[t];
+  __syncthreads();
+  const long long total = (long long)NC * Ho * Wo;
+  for (long long o = blockIdx.x * 256LL + threadIdx.x; o < total; o += (long long)gridDim.x * 256) {
+    int ox = (int)(o % Wo);
+    int oy = (int)((o / Wo) % Ho);
+    long long nc = o / ((long long)Wo * Ho);
+    const long long base = nc * H * W;
+    float acc = 0.f;
+    for (int i = 0; i < kh; ++i) {
+      int uy = oy * dny + i - py0;
+      if (uy < 0 || uy % upy) continue;
+      int iy = uy / upy;
+      if (iy >= H) continue;
+      for (int j = 0; j < kw; ++j) {
+        int ux = ox * dnx + j - px0;
+        if (ux < 0 || ux % upx) continue;
+        int ix = ux / upx;
+        if (ix >= W) continue;
+        acc += ldv<DT>(x, base + (long long)iy * W + ix) * taps[(kh - 1 - i) * kw + (kw - 1 - j)];
+      }
+    }
+    stv<DT>(y, o, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K25: resize planar [NC, H, W] -> [NC, Ho, Wo] with torch.nn.functional.interpolate semantics
+// (size given, no scale_factor). mode 0 nearest, 1 nearest-exact, 2 bilinear, 3 bicubic (A=-0.75,
+// clamped taps), 4 area (adaptive average pool).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float cubic1(float t, float A) { return ((A + 2.f) * t - (A + 3.f)) * t * t + 1.f; }
+__device__ __forceinline__ float cubic2(float t, float A) { return ((A * t - 5.f * A) * t + 8.f * A) * t - 4.f * A; }
+
+template <int DT>
+__global__ void __launch_bounds__(256) resize_kernel(const void* x, void* y, int NC, int H, int W, int Ho, int Wo,
+                                                     int mode, int align) {
+  const long long total = (long long)NC * Ho * Wo;
+  float sh, sw;
+  if (align && mode >= 2 && mode <= 3) {
+    sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
+    sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  } else {
+    sh = (float)H / (float)Ho;
+    sw = (float)W / (float)Wo;
+  }
+  for (long long o = blockIdx.x * 256LL + threadIdx.x; o < total; o += (long long)gridDim.x * 256) {
+    int ox = (int)(o % Wo);
+    int oy = (int)((o / Wo) % Ho);
+    long long base = (o / ((long long)Wo * Ho)) * H * W;
+    float v;
+    if (mode <= 1) {
+      float off = mode == 1 ? 0.5f : 0.f;
+      int iy = min((int)floorf((oy + off) * sh), H - 1);
+      int ix = min((int)floorf((ox + off) * sw), W - 1);
+      v = ldv<DT>(x, base + (long long)iy * W + ix);
+    } else if (mode == 2) {
+      float fy = align ? oy * sh : fmaxf((oy + 0.5f) * sh - 0.5f, 0.f);
+      float fx = align ? ox * sw : fmaxf((ox + 0.5f) * sw - 0.5f, 0.f);
+      int y0 = (int)fy, x0 = (int)fx;
+      int y1 = y0 + (y0 < H - 1), x1 = x0 + (x0 < W - 1);
+      float ly = fy - y0, lx = fx - x0;
+      v = (1.f - ly) * ((1.f - lx) * ldv<DT>(x, base + (long long)y0 * W + x0) + lx * ldv<DT>(x, base + (long long)y0 * W + x1)) +
+          ly * ((1.f - lx) * ldv<DT>(x, base + (long long)y1 * W + x0) + lx * ldv<DT>(x, base + (long long)y1 * W + x1));
+    } else if (mode == 3) {
+      const float A = -0.75f;
+      float fy = align ? oy * sh : (oy + 0.5f) * sh - 0.5f;
+      float fx = align ? ox * sw : (ox + 0.5f) * sw - 0.5f;
+      int iy = (int)floorf(fy), ix = (int)floorf(fx);
+      float ty = fy - iy, tx = fx - ix;
+      float wy[4] = {cubic2(ty + 1.f, A), cubic1(ty, A), cubic1(1.f - ty, A), cubic2(2.f - ty, A)};
+      float wx[4] = {cubic2(tx + 1.f, A), cubic1(tx, A), cubic1(1.f - tx, A), cubic2(2.f - tx, A)};
+      v = 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        int yy = min(max(iy - 1 + a, 0), H - 1);
+        float row = 0.f;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          int xx = min(max(ix - 1 + b, 0), W - 1);
+          row += wx[b] * ldv<DT>(x, base + (long long)yy * W + xx);
+        }
+        v += wy[a] * row;
+      }
+    } else {
+      int y0 = (int)(((long long)oy * H) / Ho), y1 = (int)(((long long)(oy + 1) * H + Ho - 1) / Ho);
+      int x0 = (int)(((long long)ox * W) / Wo), x1 = (int)(((long long)(ox + 1) * W + Wo - 1) / Wo);
+      float s = 0.f;
+      for (int yy = y0; yy < y1; ++yy)
+        for (int xx = x0; xx < x1; ++xx) s += ldv<DT>(x, base + (long long)yy * W + xx);
+      v = s / (float)((y1 - y0) * (x1 - x0));
+    }
+    stv<DT>(y, o, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K31: nearest codebook entry. One wave per input row; lanes stride over the codebook computing
+// sum_d (z_d - e_d)^2 in fp32, then a wave argmin (ties -> lowest index, like torch.argmin).
+// Writes the index (int64) and the gathered entry.
+// ---------------------------------------------------------------------------------------------
+template <int DT>
+__global__ void __launch_bounds__(256) vq_nearest_kernel(const void* z, const void* cb, long long* idx, void* q,
+                                                         int M, int n, int D) {
+  extern __shared__ float zs[];               // [4 waves][D]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  float* zr = zs + wave * D;
+  if (row < M)
+    for (int d = lane; d < D; d += 64) zr[d] = ldv<DT>(z, (long long)row * D + d);
+  __syncthreads();
+  if (row >= M) return;
+  float best = 3.4e38f;
+  int bi = 0x7fffffff;
+  for (int j = lane; j < n; j += 64) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float t = zr[d] - ldv<DT>(cb, (long long)j * D + d);
+      s += t * t;
+    }
+    if (s < best) { best = s; bi = j; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    float ob = __shfl_xor(best, off, 64);
+    int oi = __shfl_xor(bi, off, 64);
+    if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) idx[row] = bi;
+  for (int d = lane; d < D; d += 64) stv<DT>(q, (long long)row * D + d, ldv<DT>(cb, (long long)bi * D + d));
+}
+
+// ---------------------------------------------------------------------------------------------
+// K28: ConvNeXt-V2 global response norm on NHWC x [N, HW, C]:
+//   g[n,c] = ||x[n,:,c]||_2 ; nx = g / (mean_c g + 1e-6) ; y = beta + x * (1 + gamma * nx)
+// pass 1: partial sum of squares over an HW slice (fp32 atomics into ws[N*C]);
+// pass 2: per-sample mean over C, writes nx into ws[N*C ..]; pass 3: apply.
+// ---------------------------------------------------------------------------------------------
+template <int DT>
+__global__ void __launch_bounds__(256) grn_sumsq_kernel(const void* x, float* ss, int HW, int C, int rows_per) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int n = blockIdx.z;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(HW, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    float v = ldv<DT>(x, ((long long)n * HW + r) * C + c);
+    s += v * v;
+  }
+  atomicAdd(ss + (long long)n * C + c, s);
+}
+
+__global__ void __launch_bounds__(256) grn_finalize_kernel(const float* ss, float* nx, int C) {
+  __shared__ float red[256];
+  const int n = blockIdx.x;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) s += sqrtf(ss[(long long)n * C + c]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float inv = 1.f / (red[0] / (float)C + 1e-6f);
+  for (int c = threadIdx.x; c < C; c += 256) nx[(long long)n * C + c] = sqrtf(ss[(long long)n * C + c]) * inv;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) grn_apply_kernel(const void* x, const float* nx, const void* gamma,
+                                                        const void* beta, void* y, long long total, int HW, int C) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long long n = i / ((long long)HW * C);
+    const float v = ldv<DT>(x, i);
+    stv<DT>(y, i, ldv<DT>(beta, c) + v * (1.f + ldv<DT>(gamma, c) * nx[n * C + c]));
+  }
+}
+
+}  // namespace
+
+CGS_EXPORT int cgs_fused_bias_act(const void* x, const void* b, void* y, long long n, int C, long long inner,
+                                  float slope, float scale, int dtype, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (C <= 0 || inner <= 0) return (int)hipErrorInvalidValue;
+  CGS_DISPATCH_DT(dtype, fused_bias_act_kernel, <<<grid_for(n), 256, 0, stream>>>(x, b, y, n, C, inner, slope, scale));
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_upfirdn2d(const void* x, const float* k, void* y, int NC, int H, int W, int upx, int upy, int dnx,
+                             int dny, int px0, int px1, int py0, int py1, int kh, int kw, int dtype,
+                             hipStream_t stream) {
+  if (kh <= 0 || kw <= 0 || kh * kw > 32 * 32 || upx < 1 || upy < 1 || dnx < 1 || dny < 1)
+    return (int)hipErrorInvalidValue;
+  const int Ho = (H * upy + py0 + py1 - kh) / dny + 1;
+  const int Wo = (W * upx + px0 + px1 - kw) / dnx + 1;
+  if (Ho <= 0 || Wo <= 0) return (int)hipErrorInvalidValue;
+  const long long total = (long long)NC * Ho * Wo;
+  CGS_DISPATCH_DT(dtype, upfirdn2d_kernel, <<<grid_for(total), 256, 0, stream>>>(x, k, y, NC, H, W, upx, upy, dnx, dny,
+                                                                                px0, py0, kh, kw, Ho, Wo));
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_resize(const void* x, void* y, int NC, int H, int W, int Ho, int Wo, int mode, int align,
+                          int dtype, hipStream_t stream) {
+  if (mode < 0 || mode > 4 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return (int)hipErrorInvalidValue;
+  const long long total = (long long)NC * Ho * Wo;
+  if (total == 0) return 0;
+  CGS_DISPATCH_DT(dtype, resize_kernel, <<<grid_for(total), 256, 0, stream>>>(x, y, NC, H, W, Ho, Wo, mode, align));
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_vq_nearest(const void* z, const void* cb, long long* idx, void* q, int M, int n, int D, int dtype,
+                              hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (n <= 0 || D <= 0 || D > 4096) return (int)hipErrorInvalidValue;
+  const size_t lds = 4 * (size_t)D * sizeof(float);
+  CGS_DISPATCH_DT(dtype, vq_nearest_kernel, <<<(M + 3) / 4, 256, lds, stream>>>(z, cb, idx, q, M, n, D));
+  return (int)hipGetLastError();
+}
+
+// ws: fp32 workspace of 2*N*C floats, zeroed by the caller (first half: sum of squares).
+CGS_EXPORT int cgs_grn_nhwc(const void* x, const void* gamma, const void* beta, void* y, float* ws, int N, int HW,
+                            int C, int dtype, hipStream_t stream) {
+  if (N <= 0 || HW <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  const int rows_per = 32;
+  dim3 g1((C + 255) / 256, (HW + rows_per - 1) / rows_per, N);
+  CGS_DISPATCH_DT(dtype, grn_sumsq_kernel, <<<g1, 256, 0, stream>>>(x, ws, HW, C, rows_per));
+  grn_finalize_kernel<<<N, 256, 0, stream>>>(ws, ws + (long long)N * C, C);
+  const long long total = (long long)N * HW * C;
+  CGS_DISPATCH_DT(dtype, grn_apply_kernel, <<<grid_for(total), 256, 0, stream>>>(x, ws + (long long)N * C, gamma, beta,
+                                                                                y, total, HW, C));
+  return (int)hipGetLastError();
+}

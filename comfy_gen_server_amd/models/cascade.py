@@ -80,10 +80,7 @@ class GlobalResponseNorm(nn.Module):
         self.beta = nn.Parameter(torch.zeros(1, 1, 1, dim, dtype=dtype, device=device), requires_grad=False)
 
     def forward(self, x):
-        gx = torch.linalg.vector_norm(x, dim=(1, 2), keepdim=True, dtype=torch.float32)
-        nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
-        scale = (1.0 + self.gamma.float() * nx).to(x.dtype)
-        return torch.addcmul(_cast(self.beta, x), x, scale)
+        return ops.grn_nhwc(x, _cast(self.gamma, x), _cast(self.beta, x))
 
 
 class _ChannelMLP(nn.Sequential):
@@ -512,11 +509,8 @@ class VectorQuantize(nn.Module):
         """Nearest codebook entry per vector (along ``dim``) -> (quantized, indices)."""
         if dim != -1:
             x = x.movedim(dim, -1)
-        flat = x.reshape(-1, x.shape[-1]).float()
-        cb = self.codebook.weight.float()
-        d = (flat * flat).sum(1, keepdim=True) + (cb * cb).sum(1)[None] - 2.0 * flat @ cb.t()
-        idx = d.argmin(dim=1)
-        q = cb[idx].reshape(x.shape).to(x.dtype)
+        q, idx = ops.vq_nearest(x.reshape(-1, x.shape[-1]), self.codebook.weight)
+        q = q.reshape(x.shape)
         if dim != -1:
             q = q.movedim(-1, dim)
         return q, idx.reshape(x.shape[:-1])

@@ -264,11 +264,8 @@ class _MHAttnBlock(nn.Module):
 def _quantize(z, codebook):
     """Nearest codebook entry per position (z [B, C, H, W], codebook [n, C])."""
     B, C, H, W = z.shape
-    zf = z.permute(0, 2, 3, 1).reshape(-1, C).float()
-    cb = codebook.float()
-    d = zf.pow(2).sum(1, keepdim=True) + cb.pow(2).sum(1) - 2 * zf @ cb.t()
-    idx = d.argmin(1)
-    return codebook[idx].view(B, H, W, C).permute(0, 3, 1, 2).to(z.dtype)
+    q, _ = ops.vq_nearest(z.permute(0, 2, 3, 1).reshape(-1, C), codebook)
+    return q.view(B, H, W, C).permute(0, 3, 1, 2)
 
 
 class RestoreFormer(nn.Module):

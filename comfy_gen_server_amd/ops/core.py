@@ -509,3 +509,127 @@ def euler_step(x: torch.Tensor, denoised: torch.Tensor, noise: torch.Tensor | No
     if noise is not None and sigma_up > 0:
         x = x + noise * sigma_up
     return x
+
+
+# ----------------------------------------------------------------------------------------------
+# Image / utility ops (csrc/kernels/image.hip)
+# ----------------------------------------------------------------------------------------------
+_RESIZE_MODES = {"nearest": 0, "nearest-exact": 1, "bilinear": 2, "bicubic": 3, "area": 4}
+
+
+def interpolate(x: torch.Tensor, size, mode: str = "nearest", align_corners: bool | None = None) -> torch.Tensor:
+    """``F.interpolate(x, size=size, mode=mode)`` for 4-D tensors (K25). Device path: one HIP
+    kernel over the NC planes (fp32 accumulate); other modes / ranks go to ATen."""
+    Ho, Wo = (size, size) if isinstance(size, int) else (int(size[0]), int(size[1]))
+    m = _RESIZE_MODES.get(mode)
+    be = backend_for("resize", x, "cgs_resize")
+    if be == "hip" and m is not None and x.dim() == 4 and x.dtype in _DT and x.numel() > 0:
+        count("resize", "hip")
+        N, C, H, W = x.shape
+        xc = x.contiguous()
+        y = torch.empty((N, C, Ho, Wo), device=x.device, dtype=x.dtype)
+        _check(_lib().cgs_resize(xc.data_ptr(), y.data_ptr(), N * C, H, W, Ho, Wo, m, int(bool(align_corners)),
+                                 _DT[x.dtype], _stream()), "cgs_resize")
+        return y
+    kw = {"align_corners": align_corners} if mode in ("bilinear", "bicubic") else {}
+    return F.interpolate(x, size=(Ho, Wo), mode=mode, **kw)
+
+
+def fused_bias_act(x: torch.Tensor, bias: torch.Tensor | None, negative_slope: float = 0.2,
+                   scale: float = 2 ** 0.5) -> torch.Tensor:
+    """StyleGAN2 FusedLeakyReLU (K32, ``face/fused_act.py``): leaky_relu(x + bias[c]) * scale,
+    bias broadcast along dim 1."""
+    be = backend_for("fused_bias_act", x, "cgs_fused_bias_act")
+    C = x.shape[1] if x.dim() > 1 else x.shape[0]
+    if be == "hip" and x.dtype in _DT and x.numel() > 0:
+        count("fused_bias_act", "hip")
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        inner = 1
+        for d in x.shape[2:]:
+            inner *= d
+        b = None if bias is None else bias.to(x.dtype).contiguous()
+        _check(_lib().cgs_fused_bias_act(xc.data_ptr(), _ptr(b), y.data_ptr(), xc.numel(), C, inner,
+                                         float(negative_slope), float(scale), _DT[x.dtype], _stream()),
+               "cgs_fused_bias_act")
+        return y
+    if bias is not None:
+        x = x + bias.to(x.dtype).view(1, C, *([1] * (x.dim() - 2)))
+    return F.leaky_relu(x, negative_slope) * scale
+
+
+def upfirdn2d(x: torch.Tensor, kernel: torch.Tensor, up=1, down=1, pad=(0, 0)) -> torch.Tensor:
+    """StyleGAN2 upfirdn2d (K32, ``face/upfirdn2d.py``) on NCHW: zero-insert upsample, pad
+    (negative crops), FIR with the flipped kernel, decimate. ``pad`` = (p0, p1) for both axes or
+    (px0, px1, py0, py1)."""
+    ux, uy = (up, up) if isinstance(up, int) else up
+    dx, dy = (down, down) if isinstance(down, int) else down
+    px0, px1, py0, py1 = (pad[0], pad[1], pad[0], pad[1]) if len(pad) == 2 else pad
+    N, C, H, W = x.shape
+    kh, kw = kernel.shape
+    be = backend_for("upfirdn2d", x, "cgs_upfirdn2d")
+    if be == "hip" and x.dtype in _DT and kh * kw <= 1024:
+        count("upfirdn2d", "hip")
+        Ho = (H * uy + py0 + py1 - kh) // dy + 1
+        Wo = (W * ux + px0 + px1 - kw) // dx + 1
+        xc = x.contiguous()
+        k = kernel.to(device=x.device, dtype=torch.float32).contiguous()
+        y = torch.empty((N, C, Ho, Wo), device=x.device, dtype=x.dtype)
+        _check(_lib().cgs_upfirdn2d(xc.data_ptr(), k.data_ptr(), y.data_ptr(), N * C, H, W, ux, uy, dx, dy,
+                                    px0, px1, py0, py1, kh, kw, _DT[x.dtype], _stream()), "cgs_upfirdn2d")
+        return y
+    return upfirdn2d_reference(x, kernel, (ux, uy), (dx, dy), (px0, px1, py0, py1))
+
+
+def upfirdn2d_reference(x, kernel, up, down, pad):
+    """Plain PyTorch fp32 upfirdn2d (numerics oracle / CPU path)."""
+    (ux, uy), (dx, dy), (px0, px1, py0, py1) = up, down, pad
+    N, C, H, W = x.shape
+    xf = x.float().reshape(N * C, 1, H, W)
+    u = xf.new_zeros(N * C, 1, H * uy, W * ux)
+    u[:, :, ::uy, ::ux] = xf
+    u = F.pad(u, (max(px0, 0), max(px1, 0), max(py0, 0), max(py1, 0)))
+    u = u[:, :, max(-py0, 0):u.shape[2] - max(-py1, 0), max(-px0, 0):u.shape[3] - max(-px1, 0)]
+    w = torch.flip(kernel.float().to(x.device), [0, 1])[None, None]
+    out = F.conv2d(u, w)[:, :, ::dy, ::dx]
+    return out.reshape(N, C, out.shape[2], out.shape[3]).to(x.dtype)
+
+
+def vq_nearest(z: torch.Tensor, codebook: torch.Tensor):
+    """Nearest codebook row for every row of ``z`` [M, D] (K31: Stage A VQ, RestoreFormer /
+    CodeFormer quantizers) -> (quantized [M, D], indices int64 [M])."""
+    M, D = z.shape
+    be = backend_for("vq", z, "cgs_vq_nearest")
+    if be == "hip" and z.dtype in _DT and D <= 4096 and M > 0:
+        count("vq", "hip")
+        zc = z.contiguous()
+        cb = codebook.to(z.dtype).contiguous()
+        idx = torch.empty(M, device=z.device, dtype=torch.int64)
+        q = torch.empty_like(zc)
+        _check(_lib().cgs_vq_nearest(zc.data_ptr(), cb.data_ptr(), idx.data_ptr(), q.data_ptr(), M, cb.shape[0], D,
+                                     _DT[z.dtype], _stream()), "cgs_vq_nearest")
+        return q, idx
+    zf, cf = z.float(), codebook.float()
+    d = zf.pow(2).sum(1, keepdim=True) + cf.pow(2).sum(1)[None] - 2.0 * zf @ cf.t()
+    idx = d.argmin(1)
+    return codebook[idx].to(z.dtype), idx
+
+
+def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor) -> torch.Tensor:
+    """ConvNeXt-V2 GlobalResponseNorm on NHWC [N, H, W, C] (K28, Cascade ``common.py:77-87``):
+    beta + x * (1 + gamma * ||x||_HW / mean_C ||x||_HW)."""
+    N, H, W, C = x.shape
+    be = backend_for("grn", x, "cgs_grn_nhwc")
+    if be == "hip" and x.dtype in _DT:
+        count("grn", "hip")
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        ws = torch.zeros(2 * N * C, device=x.device, dtype=torch.float32)
+        _check(_lib().cgs_grn_nhwc(xc.data_ptr(), gamma.to(x.dtype).contiguous().data_ptr(),
+                                   beta.to(x.dtype).contiguous().data_ptr(), y.data_ptr(), ws.data_ptr(), N, H * W, C,
+                                   _DT[x.dtype], _stream()), "cgs_grn_nhwc")
+        return y
+    gx = torch.linalg.vector_norm(x, dim=(1, 2), keepdim=True, dtype=torch.float32)
+    nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
+    scale = (1.0 + gamma.float().reshape(1, 1, 1, C) * nx).to(x.dtype)
+    return torch.addcmul(beta.to(x.dtype).reshape(1, 1, 1, C), x, scale)

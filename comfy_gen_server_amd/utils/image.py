@@ -88,7 +88,8 @@ def common_upscale(samples, width, height, upscale_method, crop):
         return bislerp(s, width, height)
     if upscale_method == "lanczos":
         return lanczos(s, width, height)
-    return F.interpolate(s, size=(height, width), mode=upscale_method)
+    from .. import ops
+    return ops.interpolate(s, (height, width), upscale_method)
 
 
 def get_tiled_scale_steps(width, height, tile_x, tile_y, overlap):

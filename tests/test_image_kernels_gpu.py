@@ -1,0 +1,126 @@
+"""HIP image / utility kernels (csrc/kernels/image.hip) against plain PyTorch fp32 references:
+resize (nearest / nearest-exact / bilinear / bicubic / area), StyleGAN fused bias-act and
+upfirdn2d, VQ nearest-codebook, ConvNeXt-V2 GRN. CPU tests pin the torch fallbacks to the same
+references so both paths implement one definition."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from comfy_gen_server_amd import ops
+
+MODES = ["nearest", "nearest-exact", "bilinear", "bicubic", "area"]
+
+
+def _ref_resize(x, size, mode, align=None):
+    kw = {"align_corners": align} if mode in ("bilinear", "bicubic") else {}
+    return F.interpolate(x.float(), size=size, mode=mode, **kw)
+
+
+def _ref_fba(x, b, slope=0.2, scale=2 ** 0.5):
+    return F.leaky_relu(x.float() + b.float().view(1, -1, *([1] * (x.dim() - 2))), slope) * scale
+
+
+def _ref_grn(x, g, b):
+    gx = torch.norm(x.float(), p=2, dim=(1, 2), keepdim=True)
+    nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
+    return g.float() * (x.float() * nx) + b.float() + x.float()
+
+
+def test_cpu_fallbacks_match_references():
+    x = torch.randn(2, 3, 9, 7)
+    for m in MODES:
+        assert torch.allclose(ops.interpolate(x, (13, 5), m), _ref_resize(x, (13, 5), m), atol=1e-6)
+    b = torch.randn(3)
+    assert torch.allclose(ops.fused_bias_act(x, b), _ref_fba(x, b), atol=1e-6)
+    k = torch.tensor([1., 3., 3., 1.])
+    k = (k[None] * k[:, None]) / 64
+    y = ops.upfirdn2d(x, k, up=2, pad=(2, 1))
+    assert y.shape == (2, 3, 18, 14)
+    z, cb = torch.randn(50, 8), torch.randn(40, 8)
+    q, idx = ops.vq_nearest(z, cb)
+    assert torch.equal(idx, torch.cdist(z, cb).argmin(1)) and torch.equal(q, cb[idx])
+    xn, g, bb = torch.randn(2, 5, 6, 16), torch.randn(16), torch.randn(16)
+    assert torch.allclose(ops.grn_nhwc(xn, g, bb), _ref_grn(xn, g, bb), atol=1e-5)
+
+
+def test_upfirdn2d_reference_is_true_convolution():
+    """down=1/up=1 upfirdn2d with an asymmetric kernel == conv2d with the flipped kernel."""
+    x = torch.randn(1, 2, 8, 8)
+    k = torch.arange(1., 10.).view(3, 3)
+    y = ops.upfirdn2d_reference(x, k, (1, 1), (1, 1), (1, 1, 1, 1))
+    ref = F.conv2d(x.view(2, 1, 8, 8), torch.flip(k, [0, 1])[None, None], padding=1).view(1, 2, 8, 8)
+    assert torch.allclose(y, ref, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_resize_gpu(cuda, mode, dtype):
+    x = torch.randn(2, 4, 37, 53)
+    for size in [(64, 96), (20, 31), (37, 53)]:
+        aligns = [False, True] if mode in ("bilinear", "bicubic") else [None]
+        for al in aligns:
+            ops.reset_stats()
+            y = ops.interpolate(x.to(cuda, dtype), size, mode, align_corners=al).float().cpu()
+            assert ops.stats().get(("resize", "hip"), 0) == 1
+            ref = _ref_resize(x.to(dtype), size, mode, al)
+            tol = 1e-4 if dtype == torch.float32 else 2e-2 * max(1.0, ref.abs().max().item())
+            assert (y - ref).abs().max().item() < tol, (mode, size, al)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_fused_bias_act_gpu(cuda, dtype):
+    x, b = torch.randn(3, 24, 11, 7), torch.randn(24)
+    ops.reset_stats()
+    y = ops.fused_bias_act(x.to(cuda, dtype), b.to(cuda, dtype), 0.2, 2 ** 0.5).float().cpu()
+    assert ops.stats().get(("fused_bias_act", "hip"), 0) == 1
+    ref = _ref_fba(x.to(dtype), b.to(dtype))
+    assert (y - ref).abs().max().item() < (1e-5 if dtype == torch.float32 else 5e-2)
+    x2 = torch.randn(64, 512)                      # [rows, C] (EqualLinear activation)
+    y2 = ops.fused_bias_act(x2.to(cuda), b.new_ones(512).to(cuda)).cpu()
+    assert torch.allclose(y2, _ref_fba(x2, torch.ones(512)), atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [dict(up=2, down=1, pad=(2, 1)), dict(up=1, down=2, pad=(1, 1)),
+                                 dict(up=1, down=1, pad=(1, 2)), dict(up=2, down=2, pad=(-1, 0))])
+def test_upfirdn2d_gpu(cuda, cfg):
+    k = torch.tensor([1., 3., 3., 1.])
+    k = (k[None] * k[:, None])
+    k = k / k.sum() * (cfg["up"] ** 2)
+    x = torch.randn(2, 6, 17, 12)
+    ops.reset_stats()
+    y = ops.upfirdn2d(x.to(cuda), k, **cfg).cpu()
+    assert ops.stats().get(("upfirdn2d", "hip"), 0) == 1
+    p = cfg["pad"]
+    ref = ops.upfirdn2d_reference(x, k, (cfg["up"],) * 2, (cfg["down"],) * 2, (p[0], p[1], p[0], p[1]))
+    assert y.shape == ref.shape and torch.allclose(y, ref, atol=1e-5)
+    yb = ops.upfirdn2d(x.to(cuda, torch.bfloat16), k, **cfg).float().cpu()
+    assert (yb - ref).abs().max().item() < 5e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4096, 8192, 4), (256, 1024, 256), (33, 100, 64)])
+def test_vq_nearest_gpu(cuda, shape):
+    M, n, D = shape
+    g = torch.Generator().manual_seed(0)
+    cb = torch.randn(n, D, generator=g)
+    z = cb[torch.randint(0, n, (M,), generator=g)] + 0.01 * torch.randn(M, D, generator=g)
+    ops.reset_stats()
+    q, idx = ops.vq_nearest(z.to(cuda), cb.to(cuda))
+    assert ops.stats().get(("vq", "hip"), 0) == 1
+    ref_idx = torch.cdist(z.double(), cb.double()).argmin(1)
+    assert torch.equal(idx.cpu(), ref_idx) and torch.equal(q.cpu(), cb[ref_idx])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_grn_gpu(cuda, dtype):
+    x, g, b = torch.randn(2, 24, 24, 2048), torch.randn(2048) * 0.5, torch.randn(2048) * 0.1
+    ops.reset_stats()
+    y = ops.grn_nhwc(x.to(cuda, dtype), g.to(cuda, dtype), b.to(cuda, dtype)).float().cpu()
+    assert ops.stats().get(("grn", "hip"), 0) == 1
+    ref = _ref_grn(x.to(dtype), g.to(dtype), b.to(dtype))
+    rel = ((y - ref).norm() / ref.norm()).item()
+    assert rel < (1e-5 if dtype == torch.float32 else 1e-2)
