@@ -107,6 +107,8 @@ KERNEL_SIGNATURES = {
     "cgs_resize": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],        # x, y, NC, H, W, Ho, Wo, mode, align
     "cgs_vq_nearest": [_P, _P, _P, _P, _I, _I, _I, _I, _P],            # z, codebook, idx(i64), q, M, n, D
     "cgs_grn_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P],          # x, gamma, beta, y, ws, N, HW, C
+    # host (mmap) -> device upload through pinned double buffers (csrc/kernels/io.hip)
+    "cgs_h2d_upload": [_P, _P, _L, _L, _I, _P],                        # src, dst, nbytes, chunk, threads
     "cgs_gemm_bf16_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
     "cgs_conv2d_nhwc_v": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cgs_conv2d_nhwc_ex": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],

@@ -50,6 +50,17 @@ PYBIND11_MODULE(_cgs_runtime, m) {
              Span s{f.file(), f.tensor_ptr(k), size_t(t.end - t.begin)};
              return py::make_tuple(t.dtype, t.shape, py::memoryview(py::cast(s)));
            })
+      .def("offsets",
+           [](const SafeTensors& f, const std::string& k) {
+             const TensorInfo& t = f.info(k);
+             return py::make_tuple(t.begin, t.end);
+           })
+      .def("data_section",
+           [](const SafeTensors& f) {
+             // (address, size, keep-alive span): the address stays valid while the span lives
+             Span s{f.file(), f.data_section(), f.data_section_size()};
+             return py::make_tuple(reinterpret_cast<uintptr_t>(s.ptr), s.n, py::cast(s));
+           })
       .def("read_into",
            [](const SafeTensors& f, const std::vector<std::string>& names, const std::vector<uintptr_t>& addrs,
               int threads) {

@@ -46,6 +46,9 @@ class SafeTensors {
   uint8_t* tensor_ptr(const std::string& name) const;
   const std::map<std::string, std::string>& metadata() const { return meta_; }
   std::shared_ptr<MappedFile> file() const { return file_; }
+  // The tensor data section (everything after the header) as one span of the mapping.
+  uint8_t* data_section() const { return file_->data() + data_off_; }
+  size_t data_section_size() const { return file_->size() - data_off_; }
   // Copy tensors into caller-provided host buffers with a thread pool: page faults of a cold
   // mmap are the load bottleneck, parallel touch keeps the page cache / NVMe queue full.
   void copy_many(const std::vector<std::pair<std::string, uint8_t*>>& dst, int threads) const;

@@ -40,7 +40,50 @@ def read_metadata(path):
     return json.loads(h).get("__metadata__")
 
 
+def _element_size(dt):
+    return torch.empty(0, dtype=dt).element_size()
+
+
+def load_safetensors_to_device(path, device, dtype=None):
+    """Whole-file upload into one HBM arena: the mmap'ed data section streams to
+    the device through pinned double buffers (``cgs_h2d_upload``); tensors are views into the
+    arena. ``dtype`` converts floating tensors on the device (the arena is then released).
+    Returns None when the native pieces are unavailable."""
+    rt = _native.load_runtime()
+    lib = _native.load_kernels()
+    if rt is None or not hasattr(rt, "SafeTensorsFile") or lib is None or not hasattr(lib, "cgs_h2d_upload"):
+        return None
+    device = torch.device(device)
+    f = rt.SafeTensorsFile(path)
+    addr, size, keep = f.data_section()
+    arena = torch.empty(max(int(size), 1), dtype=torch.uint8, device=device)
+    with torch.cuda.device(device):
+        stream = torch.cuda.current_stream(device)
+        err = lib.cgs_h2d_upload(addr, arena.data_ptr(), int(size), 64 << 20, 4, stream.cuda_stream)
+    del keep
+    if err != 0:
+        raise RuntimeError(f"cgs_h2d_upload failed with hipError {err}")
+    out = {}
+    for name in f.keys():
+        dt_name, shape, _ = f.info(name)
+        dt = _DT[dt_name]
+        b, e = f.offsets(name)
+        es = _element_size(dt)
+        raw = arena[b:e]
+        if b % es:                                   # unaligned element offset: copy out
+            raw = raw.clone()
+        t = raw.view(dt).reshape(shape) if e > b else torch.empty(shape, dtype=dt, device=device)
+        if dtype is not None and t.is_floating_point() and t.dtype != dtype:
+            t = t.to(dtype)
+        out[name] = t
+    return out
+
+
 def _load_safetensors(path, device="cpu"):
+    if str(device) != "cpu" and torch.device(device).type == "cuda" and os.environ.get("CGS_DIRECT_LOAD", "1") != "0":
+        sd = load_safetensors_to_device(path, device)
+        if sd is not None:
+            return sd
     rt = _native.load_runtime()
     if rt is not None and hasattr(rt, "SafeTensorsFile") and os.environ.get("CGS_PY_SAFETENSORS") != "1":
         f = rt.SafeTensorsFile(path)

@@ -12,6 +12,7 @@ resident on the device through ``device.load_models_gpu`` (once; they stay resid
 from __future__ import annotations
 
 import logging
+import os
 import math
 
 import torch
@@ -266,9 +267,18 @@ def _materialise(model, sd_dtype, device):
     return model
 
 
+def _direct_load_device():
+    """Where checkpoint bytes should land: straight into HBM when models stay resident there
+    (HIGH_VRAM on a ROCm device — the 288 GB default), else host memory."""
+    d = dm.get_torch_device()
+    if d.type == "cuda" and dm.vram_state == dm.VRAMState.HIGH_VRAM and os.environ.get("CGS_DIRECT_LOAD", "1") != "0":
+        return d
+    return torch.device("cpu")
+
+
 def load_checkpoint_guess_config(ckpt_path, output_vae=True, output_clip=True, output_clipvision=False,
                                  embedding_directory=None, output_model=True, sd=None):
-    sd = sd if sd is not None else load_state_dict(ckpt_path)
+    sd = sd if sd is not None else load_state_dict(ckpt_path, device=_direct_load_device())
     return load_state_dict_guess_config(sd, output_vae, output_clip, output_clipvision, embedding_directory,
                                         output_model)
 
@@ -344,7 +354,7 @@ def load_unet_state_dict(sd, dtype=None):
 
 
 def load_unet(path, dtype=None):
-    sd = load_state_dict(path)
+    sd = load_state_dict(path, device=_direct_load_device())
     m = load_unet_state_dict(sd, dtype)
     if m is None:
         raise RuntimeError(f"ERROR UNSUPPORTED UNET {path}")

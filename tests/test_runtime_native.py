@@ -95,3 +95,31 @@ def test_bpe_matches_python(rt):
     python = [tok.encode(t) for t in texts]
     assert native == python
     assert native[0][:3] == [320, 1125, 539]    # "a photo of"
+
+
+@pytest.mark.gpu
+def test_safetensors_direct_hbm_upload(cuda, tmp_path):
+    """Whole-file upload into one HBM arena (pinned double-buffered H2D) == the host reader,
+    including an odd-sized uint8 tensor that leaves later tensors element-misaligned."""
+    from comfy_gen_server_amd.runtime import checkpoint
+    g = torch.Generator().manual_seed(0)
+    sd = {"a_u8": torch.randint(0, 255, (7,), dtype=torch.uint8, generator=g),
+          "b_bf16": torch.randn(33, 17, generator=g).to(torch.bfloat16),
+          "c_f32": torch.randn(1000, 257, generator=g),
+          "d_f16": torch.randn(5, generator=g).half(),
+          "e_i64": torch.arange(9, dtype=torch.int64),
+          "f_empty": torch.zeros(0, 4)}
+    p = str(tmp_path / "t.safetensors")
+    checkpoint.save_state_dict(sd, p)
+    dev = checkpoint.load_safetensors_to_device(p, cuda)
+    assert dev is not None
+    for k, v in sd.items():
+        assert dev[k].device.type == "cuda" and dev[k].dtype == v.dtype and dev[k].shape == v.shape
+        assert torch.equal(dev[k].cpu(), v), k
+    conv = checkpoint.load_safetensors_to_device(p, cuda, dtype=torch.bfloat16)
+    assert conv["c_f32"].dtype == torch.bfloat16 and conv["e_i64"].dtype == torch.int64
+    assert torch.equal(conv["c_f32"].cpu(), sd["c_f32"].to(torch.bfloat16))
+    big = {"w": torch.randn(64 << 20 // 4 + 123, generator=g)}   # > one 64 MiB staging chunk
+    p2 = str(tmp_path / "big.safetensors")
+    checkpoint.save_state_dict(big, p2)
+    assert torch.equal(checkpoint.load_state_dict(p2, device=cuda)["w"].cpu(), big["w"])
