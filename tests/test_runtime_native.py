@@ -119,7 +119,7 @@ def test_safetensors_direct_hbm_upload(cuda, tmp_path):
     conv = checkpoint.load_safetensors_to_device(p, cuda, dtype=torch.bfloat16)
     assert conv["c_f32"].dtype == torch.bfloat16 and conv["e_i64"].dtype == torch.int64
     assert torch.equal(conv["c_f32"].cpu(), sd["c_f32"].to(torch.bfloat16))
-    big = {"w": torch.randn(64 << 20 // 4 + 123, generator=g)}   # > one 64 MiB staging chunk
+    big = {"w": torch.randn((64 << 20) // 4 + 123, generator=g)}   # > one 64 MiB staging chunk
     p2 = str(tmp_path / "big.safetensors")
     checkpoint.save_state_dict(big, p2)
     assert torch.equal(checkpoint.load_state_dict(p2, device=cuda)["w"].cpu(), big["w"])
