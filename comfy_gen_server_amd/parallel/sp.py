@@ -1,0 +1,120 @@
+"""Sequence-parallel attention across the GPUs of a node (SURVEY §2.5 SP / Ulysses / ring rows,
+§5.7, §5.8 R4-R5). The reference has no multi-device sequence parallelism; these are the optional
+latency-mode building blocks for one very large image (B = 1, >= 2048² latents, VAE mid attention
+at 64 k tokens) where data parallelism has nothing to split.
+
+Both take the *local* sequence shard of q / k / v — [B, S / P, H * D] on each of the P ranks of
+``group``, shards in rank order — and return the local shard of the attention output.
+
+* ``ulysses_attention`` (R4): one all-to-all turns sequence shards into head shards
+  ([B, S, H / P * D]), every rank runs the single-GPU flash kernel (``ops.attention``) on its
+  heads over the whole sequence, a second all-to-all turns the result back. Two all-to-alls of
+  the activations per attention; needs H % P == 0. On xGMI every pair of GPUs has its own link,
+  so the all-to-all runs at full per-link bandwidth (no ring hops).
+* ``ring_attention`` (R5): K/V shards travel around the ring (send to rank + 1, receive from
+  rank - 1, overlapped with the partial attention of the block in hand); partial results are
+  merged with their log-sum-exp. Works for any head count including the single-head VAE
+  attention; memory per rank stays O(S / P).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+
+def _world(group):
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def _all_to_all(chunks, group):
+    """chunks: list of P same-shape tensors (chunk p goes to rank p) -> list received (from rank p).
+    One ``all_to_all_single`` over the stacked chunks (supported by RCCL and Gloo alike)."""
+    inp = torch.stack(chunks).contiguous()
+    out = torch.empty_like(inp)
+    dist.all_to_all_single(out, inp, group=group)
+    return list(out.unbind(0))
+
+
+def ulysses_attention(q, k, v, heads: int, group=None):
+    P, _ = _world(group)
+    if P == 1:
+        return ops.attention(q, k, v, heads)
+    if heads % P:
+        raise ValueError(f"ulysses_attention: {heads} heads not divisible by {P} ranks")
+    B, Sl, HD = q.shape
+    D = HD // heads
+    hp = heads // P
+
+    def seq_to_heads(t):
+        # [B, Sl, H*D] -> send head block p to rank p -> [B, P*Sl, hp*D] (sequence in rank order)
+        parts = [c.contiguous() for c in t.view(B, Sl, P, hp * D).unbind(2)]
+        got = _all_to_all(parts, group)
+        return torch.cat(got, dim=1)
+
+    qh, kh, vh = seq_to_heads(q), seq_to_heads(k), seq_to_heads(v)
+    o = ops.attention(qh, kh, vh, hp)                      # [B, S, hp*D]
+    back = _all_to_all([c.contiguous() for c in o.split(Sl, dim=1)], group)   # from rank p: its heads
+    return torch.stack(back, dim=2).reshape(B, Sl, HD)
+
+
+def _partial_attention(q, k, v, heads, scale):
+    """softmax-normalised partial attention of q against one K/V block + its log-sum-exp (fp32)."""
+    B, Sq, HD = q.shape
+    D = HD // heads
+    qh = q.float().view(B, Sq, heads, D).transpose(1, 2)
+    kh = k.float().view(B, k.shape[1], heads, D).transpose(1, 2)
+    vh = v.float().view(B, v.shape[1], heads, D).transpose(1, 2)
+    s = (qh @ kh.transpose(-2, -1)) * scale
+    lse = torch.logsumexp(s, dim=-1, keepdim=True)        # [B, h, Sq, 1]
+    o = torch.softmax(s, dim=-1) @ vh                      # [B, h, Sq, D]
+    return o, lse
+
+
+def ring_attention(q, k, v, heads: int, group=None):
+    P, r = _world(group)
+    if P == 1:
+        return ops.attention(q, k, v, heads)
+    B, Sl, HD = q.shape
+    D = HD // heads
+    scale = D ** -0.5
+    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(P))
+    nxt, prv = ranks[(r + 1) % P], ranks[(r - 1) % P]
+    kv = torch.cat([k, v], dim=-1).contiguous()
+    o_acc, lse_acc = None, None
+    for step in range(P):
+        reqs = []
+        if step < P - 1:                                    # overlap: ship the block while computing on it
+            recv = torch.empty_like(kv)
+            reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, kv, nxt, group),
+                                           dist.P2POp(dist.irecv, recv, prv, group)])
+        o, lse = _partial_attention(q, kv[..., :HD], kv[..., HD:], heads, scale)
+        if o_acc is None:
+            o_acc, lse_acc = o, lse
+        else:
+            m = torch.maximum(lse_acc, lse)
+            wa, wb = torch.exp(lse_acc - m), torch.exp(lse - m)
+            o_acc = (o_acc * wa + o * wb) / (wa + wb)
+            lse_acc = m + torch.log(wa + wb)
+        for req in reqs:
+            req.wait()
+        if step < P - 1:
+            kv = recv
+    return o_acc.transpose(1, 2).reshape(B, Sl, HD).to(q.dtype)
+
+
+def shard_sequence(x, group=None, dim=1):
+    """This rank's contiguous shard of ``x`` along ``dim`` (sequence length divisible by P)."""
+    P, r = _world(group)
+    return x.chunk(P, dim=dim)[r].contiguous()
+
+
+def gather_sequence(x, group=None, dim=1):
+    """Inverse of ``shard_sequence``: all-gather the shards back into the full sequence."""
+    P, _ = _world(group)
+    if P == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(P)]
+    dist.all_gather(parts, x.contiguous(), group=group)
+    return torch.cat(parts, dim=dim)
