@@ -72,6 +72,11 @@ def create_cors_middleware(allowed_origin: str):
     return cors_middleware
 
 
+def _telemetry_snapshot():
+    from ..utils import telemetry
+    return telemetry.snapshot()
+
+
 class PromptServer:
     instance = None
 
@@ -357,7 +362,8 @@ class PromptServer:
                 "devices": [{"name": dm.get_torch_device_name(device), "type": device.type, "index": device.index,
                              "vram_total": vram_total, "vram_free": vram_free, "torch_vram_total": torch_vram_total,
                              "torch_vram_free": torch_vram_free}],
-                "runtime": {"resident_models": len(dm.current_loaded_models), "metrics": dict(self.metrics)},
+                "runtime": {"resident_models": len(dm.current_loaded_models), "metrics": dict(self.metrics),
+                            "telemetry": _telemetry_snapshot()},
             }
             return web.json_response(stats)
 
@@ -477,6 +483,8 @@ class PromptServer:
             lines.append(f"cgs_queue_remaining {self.get_queue_info()['exec_info']['queue_remaining']}")
             lines.append("# TYPE cgs_resident_models gauge")
             lines.append(f"cgs_resident_models {len(dm.current_loaded_models)}")
+            from ..utils import telemetry
+            lines += telemetry.prometheus_lines()
             return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
         @routes.get("/health")

@@ -13,6 +13,7 @@ from __future__ import annotations
 import argparse
 import enum
 import logging
+import os
 
 
 class LatentPreviewMethod(enum.Enum):
@@ -111,6 +112,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--hbm-budget-gb", type=float, default=None, help="residency budget per GPU (default 90%%)")
     p.add_argument("--hip-graphs", action="store_true", help="capture denoiser steps in hipGraphs")
     p.add_argument("--queue-journal", type=str, default=None, help="JSONL journal: queued prompts survive restarts")
+    p.add_argument("--profile-dir", type=str, default=None,
+                   help="write a Perfetto/Chrome trace (torch.profiler, HIP kernels + node/step ranges) per prompt")
+    p.add_argument("--log-json", action="store_true", help="structured JSON log lines")
     p.add_argument("--disable-custom-nodes", action="store_true")
     p.add_argument("--custom-nodes-directory", type=str, default=None, nargs="+", action="append")
     return p
@@ -135,6 +139,11 @@ def parse(argv=None):
     if args.disable_auto_launch:
         args.auto_launch = False
     logging.basicConfig(format="%(message)s", level=logging.DEBUG if args.verbose else logging.INFO)
+    if getattr(args, "log_json", False):
+        from .utils.telemetry import use_json_logs
+        use_json_logs(logging.DEBUG if args.verbose else logging.INFO)
+    if getattr(args, "profile_dir", None):
+        os.environ["CGS_PROFILE_DIR"] = args.profile_dir
     for flag in ("directml", "use_split_cross_attention", "use_quad_cross_attention", "disable_xformers",
                  "disable_ipex_optimize", "cuda_malloc", "disable_cuda_malloc"):
         if getattr(args, flag, None):

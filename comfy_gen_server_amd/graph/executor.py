@@ -28,6 +28,7 @@ import traceback
 import torch
 
 from ..runtime import device as dm
+from ..utils import telemetry
 
 
 def _registry():
@@ -202,8 +203,14 @@ class PromptExecutor:
                 obj = class_def()
                 self.object_storage[(unique_id, class_type)] = obj
             t0 = time.perf_counter()
-            output_data, output_ui = get_output_data(obj, input_data_all)
-            self.node_timings[unique_id] = (class_type, time.perf_counter() - t0)
+            with telemetry.span(f"node:{class_type}:{unique_id}"):
+                telemetry.maybe_fault("node", class_type)
+                output_data, output_ui = get_output_data(obj, input_data_all)
+            dt = time.perf_counter() - t0
+            self.node_timings[unique_id] = (class_type, dt)
+            telemetry.record_node(class_type, dt)
+            if output_ui and isinstance(output_ui.get("images"), list):
+                telemetry.add("images_saved_total", len(output_ui["images"]))
             self.outputs[unique_id] = output_data
             outmap = prompt.get("outputs") if isinstance(prompt.get("outputs"), dict) else None
             if outmap and getattr(self.server, "output_map", None) is not None:

@@ -102,6 +102,7 @@ def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_inter
     """Blocking worker loop (reference ``main.py:93-146``)."""
     from .graph.executor import PromptExecutor
     from .runtime import device as dm
+    from .utils import telemetry
 
     e = PromptExecutor(server)
     last_gc = time.perf_counter()
@@ -114,7 +115,8 @@ def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_inter
             t0 = time.perf_counter()
             prompt_id = item[1]
             server.last_prompt_id = prompt_id
-            e.execute(item[2], prompt_id, item[3], item[4])
+            with telemetry.maybe_profile(prompt_id):
+                e.execute(item[2], prompt_id, item[3], item[4])
             need_gc = True
             q.task_done(item_id, e.outputs_ui,
                         status=q.ExecutionStatus(status_str="success" if e.success else "error",

@@ -96,6 +96,8 @@ class Comm:
 
     def heartbeat(self) -> int:
         """R6: returns the number of live ranks (all-reduce of ones)."""
+        from ..utils.telemetry import maybe_fault
+        maybe_fault("rank", str(self.rank))
         if not self.enabled:
             return 1
         t = torch.ones(1, dtype=torch.int32, device=self.device)

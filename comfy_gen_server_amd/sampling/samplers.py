@@ -26,6 +26,7 @@ import math
 import torch
 
 from ..runtime import device as dm
+from ..utils import telemetry
 from . import k_samplers as kds
 from . import uni_pc
 from .schedulers import SCHEDULER_NAMES, calculate_sigmas  # noqa: F401
@@ -466,10 +467,9 @@ class KSAMPLER(Sampler):
             mk.noise = noise
         ms = model_wrap.inner_model.model_sampling
         noise = ms.noise_scaling(sigmas[0], noise, latent_image, self.max_denoise(model_wrap, sigmas))
-        k_cb = None
         total = len(sigmas) - 1
-        if callback is not None:
-            k_cb = lambda x: callback(x["i"], x["denoised"], x["x"], total)  # noqa: E731
+        timed = telemetry.step_timer(callback)        # per-step wall clock + fault site
+        k_cb = lambda x: timed(x["i"], x["denoised"], x["x"], total)  # noqa: E731
         samples = self.sampler_function(mk, noise, sigmas, extra_args=extra_args, callback=k_cb, disable=disable_pbar,
                                         **self.extra_options)
         return ms.inverse_noise_scaling(sigmas[-1], samples)
