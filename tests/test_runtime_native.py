@@ -123,3 +123,10 @@ def test_safetensors_direct_hbm_upload(cuda, tmp_path):
     p2 = str(tmp_path / "big.safetensors")
     checkpoint.save_state_dict(big, p2)
     assert torch.equal(checkpoint.load_state_dict(p2, device=cuda)["w"].cpu(), big["w"])
+
+
+def test_doctor_report():
+    from comfy_gen_server_amd.tools import doctor
+    r = doctor.report()
+    assert r["kernels_lib"] and r["kernels_missing"] == [] and r["runtime_lib"]
+    assert r["distributed"]["gloo"] is True

@@ -93,3 +93,38 @@ def test_http_ws_roundtrip(env):  # noqa: F811
         worker.join(timeout=30)
 
     asyncio.run(main())
+
+
+def test_example_client_against_server(env, tmp_path):  # noqa: F811
+    """examples/api_client.py (HTTP queue + WS progress + /history + /view download) against the
+    real server; the example's workflow builder produces a valid prompt for the tiny checkpoint."""
+    import importlib.util
+    import os
+    from comfy_gen_server_amd import cli_args
+    from comfy_gen_server_amd.main import build_server, prompt_worker
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("api_client", os.path.join(root, "examples", "api_client.py"))
+    ac = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ac)
+    wf = ac.txt2img_workflow(ckpt="tiny.safetensors", steps=2, width=64, height=64, batch=2, seed=5, prefix="ex")
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        args = cli_args.parser.parse_args(["--disable-custom-nodes"])
+        server, q = build_server(args, loop)
+        stop = threading.Event()
+        threading.Thread(target=prompt_worker, args=(q, server, stop), daemon=True).start()
+        pub = asyncio.ensure_future(server.publish_loop())
+        client = TestClient(TestServer(server.app))
+        await client.start_server()
+        try:
+            pid, files, progress = await ac.run_and_fetch(None, wf, str(tmp_path), session=client)
+        finally:
+            stop.set()
+            pub.cancel()
+            await client.close()
+        return pid, files, progress
+
+    pid, files, progress = asyncio.new_event_loop().run_until_complete(main())
+    assert len(files) == 2 and all(os.path.getsize(f) > 100 for f in files)
+    assert progress and progress[-1][0] == progress[-1][1]
