@@ -78,6 +78,7 @@ def bench_sdxl_cn_lora(reps, pipe=None):
         lpatcher, lclip = load_lora_for_models(patcher, clip, lora, 0.8, 0.0)
         cfg = copy.deepcopy(SDXL_UNET)
         cfg.pop("out_channels", None)
+        cfg.update(num_heads=-1, num_head_channels=64)          # the SDXL family's unet_extra_config
         with torch.device("meta"):
             cm = CNModel(hint_channels=3, dtype=torch.bfloat16, device=torch.device("meta"), **cfg)
         cm.to_empty(device=dev)
