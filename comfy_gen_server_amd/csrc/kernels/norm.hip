@@ -13,7 +13,7 @@
 #include "common.h"
 
 #define GN_THREADS 256
-#define GN_MAX_CHUNKS_PER_LANE 4   // C <= 64*4*8 = 2048 channels per row in registers
+#define GN_MAX_CHUNKS_PER_LANE 4   // <= 64*4*8 = 2048 channels of a row per block (wider rows: channel slices)
 
 static inline int gn_pix_per_block(int N, int HW) {
   int target_blocks_per_n = (2048 + N - 1) / N;
@@ -24,21 +24,23 @@ static inline int gn_pix_per_block(int N, int HW) {
 
 template <int DT>
 __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, float* __restrict__ part,
-                                                               int HW, int C, int ppb, int nb) {
+                                                               int HW, int C, int ppb, int nb, int CS) {
+  // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget)
   const int n = blockIdx.y;
   const int blk = blockIdx.x;
+  const int c0 = blockIdx.z * CS;
   const int p0 = blk * ppb;
   const int p1 = min(HW, p0 + ppb);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int nchunk = C >> 3;
+  const int nchunk = CS >> 3;
   float s1[GN_MAX_CHUNKS_PER_LANE][8], s2[GN_MAX_CHUNKS_PER_LANE][8], sh[GN_MAX_CHUNKS_PER_LANE][8];
   int cnt = 0;
 #pragma unroll
   for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s1[k][j] = 0.f; s2[k][j] = 0.f; sh[k][j] = 0.f; }
-  const u16* xn = x + (size_t)n * HW * C;
+  const u16* xn = x + (size_t)n * HW * C + c0;
   bool first = true;
   for (int p = p0 + wave; p < p1; p += 4) {
     const u16* row = xn + (size_t)p * C;
@@ -62,8 +64,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   }
   // per-wave (mean, M2) per channel -> LDS, then Chan-combine the 4 waves
   extern __shared__ __attribute__((aligned(16))) float gn_smem[];
-  float* lmean = gn_smem;             // [4][C]
-  float* lm2 = gn_smem + 4 * C;       // [4][C]
+  float* lmean = gn_smem;             // [4][CS]
+  float* lm2 = gn_smem + 4 * CS;      // [4][CS]
   __shared__ int lcnt[4];
   if (lane == 0) lcnt[wave] = cnt;
 #pragma unroll
@@ -77,25 +79,25 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
           m = sh[k][j] + s1[k][j] / cnt;
           m2 = fmaxf(0.f, s2[k][j] - s1[k][j] * s1[k][j] / cnt);
         }
-        lmean[wave * C + ch * 8 + j] = m;
-        lm2[wave * C + ch * 8 + j] = m2;
+        lmean[wave * CS + ch * 8 + j] = m;
+        lm2[wave * CS + ch * 8 + j] = m2;
       }
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += GN_THREADS) {
+  for (int c = threadIdx.x; c < CS; c += GN_THREADS) {
     float n_a = 0.f, mean = 0.f, m2 = 0.f;
     for (int w = 0; w < 4; ++w) {
       float n_b = (float)lcnt[w];
       if (n_b <= 0.f) continue;
-      float mb = lmean[w * C + c], m2b = lm2[w * C + c];
+      float mb = lmean[w * CS + c], m2b = lm2[w * CS + c];
       float nn = n_a + n_b;
       float d = mb - mean;
       mean += d * n_b / nn;
       m2 += m2b + d * d * n_a * n_b / nn;
       n_a = nn;
     }
-    size_t o = (((size_t)n * nb + blk) * C + c) * 2;
+    size_t o = (((size_t)n * nb + blk) * C + c0 + c) * 2;
     part[o] = mean;
     part[o + 1] = m2;
   }
@@ -195,16 +197,21 @@ CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
 CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,
                                      void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
                                      hipStream_t stream) {
-  if (C % 8 || C > 2048 || C % G) return (int)hipErrorInvalidValue;
+  // channel slices of <= 2048 (the per-lane register budget of gn_partial), equal and 8-aligned
+  const int ns = (C + 2047) / 2048;
+  if (C % 8 || C % G || C % (8 * ns) || C > 8192) return (int)hipErrorInvalidValue;
+  const int CS = C / ns;
   int ppb = gn_pix_per_block(N, HW);
   int nb = (HW + ppb - 1) / ppb;
   float* part = (float*)ws;
   float* ab = part + (size_t)N * nb * C * 2;
-  dim3 g1(nb, N);
+  dim3 g1(nb, N, ns);
   if (dtype == CGS_BF16)
-    gn_partial_kernel<CGS_BF16><<<g1, GN_THREADS, 8 * C * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb);
+    gn_partial_kernel<CGS_BF16><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb,
+                                                                                    nb, CS);
   else
-    gn_partial_kernel<CGS_F16><<<g1, GN_THREADS, 8 * C * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb);
+    gn_partial_kernel<CGS_F16><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb,
+                                                                                   nb, CS);
   gn_finalize_kernel<<<dim3(G, N), 64, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
   long long chunks = (long long)N * HW * (C / 8);
   long long nbk = (chunks + 255) / 256;

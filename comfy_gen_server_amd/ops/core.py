@@ -294,7 +294,8 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
     """
     be = backend_for("groupnorm", x, "cgs_groupnorm_nhwc_ws")
     if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16) and \
-            weight is not None and x.shape[1] % 8 == 0 and x.shape[1] <= 2048 and x.shape[1] % groups == 0:
+            weight is not None and x.shape[1] % 8 == 0 and x.shape[1] % groups == 0 and x.shape[1] <= 8192 and \
+            x.shape[1] % (8 * ((x.shape[1] + 2047) // 2048)) == 0:
         count("groupnorm", "hip")
         N, C, H, W = x.shape
         xc = x.contiguous(memory_format=torch.channels_last)

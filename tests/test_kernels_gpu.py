@@ -26,7 +26,9 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("N,C,H,W,G", [(2, 320, 32, 32, 32), (2, 640, 16, 16, 32), (1, 1280, 8, 8, 32),
-                                       (2, 960, 16, 16, 32), (1, 128, 64, 64, 32), (3, 64, 5, 7, 32)])
+                                       (2, 960, 16, 16, 32), (1, 128, 64, 64, 32), (3, 64, 5, 7, 32),
+                                       (2, 2560, 16, 16, 32), (2, 1920, 8, 8, 32), (1, 3840, 4, 5, 32),
+                                       (1, 4096, 6, 6, 32)])
 @pytest.mark.parametrize("silu", [False, True])
 def test_groupnorm(cuda, N, C, H, W, G, silu):
     torch.manual_seed(0)
