@@ -119,7 +119,7 @@ def test_layernorm_no_affine(cuda):
     assert _rel(y, F.layer_norm(x.float(), (2048,), eps=1e-6)) < 1e-2
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["generic", "d64fast", "shortkv"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["generic", "d64fast", "shortkv", "d64r2"])
 def attn_variant(request):
     lib = _native.load_kernels()
     lib.cgs_attn_set_variant(request.param)
