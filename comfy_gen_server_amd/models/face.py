@@ -17,7 +17,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import Conv2d, DerivedMixin, Linear
+from . import vae as _vae          # ResnetBlock / Downsample / Upsample share the ldm key layout
+from .layers import Conv2d, DerivedMixin, GroupNorm, LayerNorm, Linear
 
 
 def _lrelu(x):
@@ -227,8 +228,6 @@ class GFPGANv1Clean(nn.Module):
 # whose 16x16 attention layers cross-attend from the encoder's features (multi-head, d=64).
 # ----------------------------------------------------------------------------------------------
 
-from . import vae as _vae  # noqa: E402  (ResnetBlock / Downsample / Upsample share the ldm key layout)
-from .layers import GroupNorm, LayerNorm  # noqa: E402
 
 
 def _gn(c):
