@@ -94,6 +94,10 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def heartbeat_fault_site(self):
+        from ..utils.telemetry import maybe_fault
+        maybe_fault("rank", str(self.rank))
+
     def heartbeat(self) -> int:
         """R6: returns the number of live ranks (all-reduce of ones)."""
         from ..utils.telemetry import maybe_fault
@@ -103,6 +107,46 @@ class Comm:
         t = torch.ones(1, dtype=torch.int32, device=self.device)
         dist.all_reduce(t)
         return int(t.item())
+
+    # ---- control plane (R6): the c10d TCPStore (hosted by rank 0) outlives a dead peer, unlike a
+    # collective ring, so liveness and degraded-mode result shipping go through it ----
+    def store(self):
+        return dist.distributed_c10d._get_default_store() if self.enabled else None
+
+    def _seq(self):
+        self._job_seq = getattr(self, "_job_seq", 0) + 1
+        return self._job_seq
+
+    def liveness_round(self, timeout_s: float = 30.0):
+        """Every rank checks in; rank 0 waits up to ``timeout_s`` and publishes the verdict.
+        Returns (round_id, dead_ranks) identically on every live rank."""
+        st, rid = self.store(), self._seq()
+        st.set(f"cgs/live/{rid}/{self.rank}", "1")
+        if self.rank == 0:
+            import time as _t
+            deadline = _t.time() + timeout_s
+            pending = set(range(1, self.world))
+            while pending and _t.time() < deadline:
+                pending = {r for r in pending if not st.check([f"cgs/live/{rid}/{r}"])}
+                if pending:
+                    _t.sleep(0.05)
+            st.set(f"cgs/verdict/{rid}", ",".join(str(r) for r in sorted(pending)))
+            return rid, sorted(pending)
+        st.wait([f"cgs/verdict/{rid}"], datetime.timedelta(seconds=timeout_s * 2 + 30))
+        v = st.get(f"cgs/verdict/{rid}").decode()
+        return rid, [int(x) for x in v.split(",") if x]
+
+    def store_put_tensor(self, key, t):
+        import io
+        buf = io.BytesIO()
+        torch.save(t.cpu(), buf)
+        self.store().set(key, buf.getvalue())
+
+    def store_get_tensor(self, key, timeout_s=120.0):
+        import io
+        st = self.store()
+        st.wait([key], datetime.timedelta(seconds=timeout_s))
+        return torch.load(io.BytesIO(st.get(key)), weights_only=True)
 
     def shutdown(self):
         if self.enabled and dist.is_initialized():

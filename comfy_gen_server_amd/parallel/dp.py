@@ -105,16 +105,35 @@ class DataParallelGenerator:
         if self.vae is not None:
             c.broadcast_module(self.vae.first_stage_model)
 
-    def run(self, job: Job, gather=True):
-        """Whole-node job: ``job.batch`` images split evenly across ranks -> uint8 [B,H,W,3] on rank 0."""
+    def _shard(self, job, r):
         c = self.comm
+        per, rem = job.batch // c.world, job.batch % c.world
+        return r * per + min(r, rem), per + (1 if r < rem else 0)
+
+    def run(self, job: Job, gather=True, fault_tolerant=None):
+        """Whole-node job: ``job.batch`` images split evenly across ranks -> uint8 [B,H,W,3] on rank 0.
+
+        ``fault_tolerant`` (default: env ``CGS_DP_FAULT_TOLERANT=1``): before gathering, liveness is
+        checked on the gloo control group; if ranks died, the survivors ship their shards to rank 0
+        point-to-point and rank 0 regenerates the dead ranks' shards itself (per-image noise replay
+        makes them identical to what the dead rank would have produced) — the job completes, and
+        the engine marks itself degraded (later jobs run on rank 0 alone)."""
+        c = self.comm
+        if fault_tolerant is None:
+            fault_tolerant = os.environ.get("CGS_DP_FAULT_TOLERANT", "0") == "1"
+        if getattr(self, "degraded", False):
+            return to_uint8(generate_local(self.patcher, self.clip, self.vae, job, 0, job.batch))
         job = c.broadcast_object(job)
         per = job.batch // c.world
         rem = job.batch % c.world
-        local = per + (1 if c.rank < rem else 0)
-        offset = c.rank * per + min(c.rank, rem)
+        offset, local = self._shard(job, c.rank)
         imgs = generate_local(self.patcher, self.clip, self.vae, job, offset, local)
         u8 = to_uint8(imgs)
+        if gather and c.enabled and fault_tolerant:
+            c.heartbeat_fault_site()
+            rid, dead = c.liveness_round(float(os.environ.get("CGS_DP_LIVENESS_TIMEOUT", "30")))
+            if dead:
+                return self._recover(job, u8, dead, rid)
         if gather and c.enabled:
             if rem:
                 pad = torch.zeros((per + 1 - local,) + tuple(u8.shape[1:]), dtype=u8.dtype, device=u8.device)
@@ -128,6 +147,26 @@ class DataParallelGenerator:
                 allimgs = torch.cat(keep)
             return allimgs
         return u8
+
+
+    def _recover(self, job, u8, dead, rid):
+        """Degraded gather: survivors hand their shards to rank 0 through the store,
+        rank 0 recomputes the dead ranks' shards and assembles the whole batch."""
+        import logging
+        c = self.comm
+        self.degraded = True
+        if c.rank != 0:
+            c.store_put_tensor(f"cgs/shard/{rid}/{c.rank}", u8)
+            return None
+        logging.error("DP ranks %s failed; recomputing their shards on rank 0", dead)
+        parts = {0: u8.cpu()}
+        for r in range(1, c.world):
+            if r in dead:
+                off, n = self._shard(job, r)
+                parts[r] = to_uint8(generate_local(self.patcher, self.clip, self.vae, job, off, n)).cpu()
+            else:
+                parts[r] = c.store_get_tensor(f"cgs/shard/{rid}/{r}")
+        return torch.cat([parts[r] for r in range(c.world)])
 
 
 def images_per_sec(batch, seconds):
