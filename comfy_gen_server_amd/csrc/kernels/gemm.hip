@@ -23,10 +23,34 @@
 #define EPI_RESIDUAL 2
 #define EPI_GEGLU 4
 
+// fp8 e4m3fn (OCP) -> bf16 bits, exact (every e4m3 value is a bf16 value); NaN stays NaN.
+__device__ __forceinline__ u16 fp8e4m3_to_bf16(uint32_t b) {
+  const uint32_t s = (b & 0x80u) << 8, e = (b >> 3) & 15u, m = b & 7u;
+  uint32_t mag = e ? (((e + 120u) << 7) | (m << 4)) : (__float_as_uint((float)m * 0.001953125f) >> 16);
+  if ((b & 0x7fu) == 0x7fu) mag = 0x7fc0u;
+  return (u16)(s | mag);
+}
+
+__device__ __forceinline__ s16x8 fp8x8_to_bf16x8(uint2 w) {
+  s16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = (short)fp8e4m3_to_bf16((w.x >> (8 * j)) & 0xffu);
+    o[4 + j] = (short)fp8e4m3_to_bf16((w.y >> (8 * j)) & 0xffu);
+  }
+  return o;
+}
+
+// W8 = true: W is fp8 e4m3fn (K21: fp8-stored weights, e.g. --fp8_e4m3fn-unet), widened to bf16 in
+// the global->register staging step, so LDS / MFMA see bf16 exactly as for bf16 weights and the
+// weight stream from HBM is halved.
+template <bool W8>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(
-    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ A, const void* __restrict__ Wv, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
     int epi, float alpha, int tiles_n) {
+  const u16* __restrict__ W = static_cast<const u16*>(Wv);
+  const uint8_t* __restrict__ W8p = static_cast<const uint8_t*>(Wv);
   __shared__ __attribute__((aligned(16))) u16 As[2][G_BM * G_LDW];
   __shared__ __attribute__((aligned(16))) u16 Ws[2][G_BN * G_LDW];
 
@@ -55,7 +79,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(
       int gm = m0 + r;
       ra[i] = (gm < M && gk < K) ? *reinterpret_cast<const s16x8*>(A + gm * lda + gk) : z;
       int gn = n0 + r;
-      rw[i] = (gn < N && gk < K) ? *reinterpret_cast<const s16x8*>(W + gn * ldw + gk) : z;
+      if constexpr (W8)
+        rw[i] = (gn < N && gk < K) ? fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(W8p + gn * ldw + gk)) : z;
+      else
+        rw[i] = (gn < N && gk < K) ? *reinterpret_cast<const s16x8*>(W + gn * ldw + gk) : z;
     }
   };
   auto sstore = [&](int buf) {
@@ -514,9 +541,22 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   int tiles_m = (M + G_BM - 1) / G_BM;
   int tiles_n = (N + G_BN - 1) / G_BN;
   long long nwg = (long long)tiles_m * tiles_n;
-  gemm_bf16_nt_kernel<<<(unsigned)nwg, 256, 0, stream>>>((const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias,
-                                                        (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
-                                                        tiles_n);
+  gemm_bf16_nt_kernel<false><<<(unsigned)nwg, 256, 0, stream>>>((const u16*)A, W, (u16*)C, (const u16*)bias,
+                                                               (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+                                                               tiles_n);
+  return (int)hipGetLastError();
+}
+
+// C = A (bf16) x W^T (fp8 e4m3fn, ldw in elements = bytes) with the same epilogues.
+CGS_EXPORT int cgs_gemm_bf16_w8(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                                int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                                float alpha, hipStream_t stream) {
+  if (K % 8 || lda % 8 || ldw % 8 || ((uintptr_t)W & 7) || ((uintptr_t)A & 15)) return (int)hipErrorInvalidValue;
+  if ((epi & EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0) return 0;
+  const int tiles_m = (M + G_BM - 1) / G_BM, tiles_n = (N + G_BN - 1) / G_BN;
+  gemm_bf16_nt_kernel<true><<<(unsigned)((long long)tiles_m * tiles_n), 256, 0, stream>>>(
+      (const u16*)A, W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_n);
   return (int)hipGetLastError();
 }
 

@@ -61,6 +61,9 @@ class Linear(nn.Module, DerivedMixin):
 
     def forward(self, x, residual=None):
         w, b = self.weight, self.bias
+        if w.dtype == torch.float8_e4m3fn and w.device == x.device and x.dtype == torch.bfloat16 and x.is_cuda:
+            # fp8-stored weights go to the fp8-weight GEMM as they are (widened inside the kernel)
+            return ops.linear(x, w, None if b is None else b.to(dtype=x.dtype), residual=residual)
         if w.dtype != x.dtype or w.device != x.device:  # manual cast (comfy/ops.py:22-32)
             w = w.to(device=x.device, dtype=x.dtype)
             b = None if b is None else b.to(device=x.device, dtype=x.dtype)

@@ -56,6 +56,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
 
     Device path: the HIP GEMM family (v5 ping-pong 256x256x64, v3 8-wave 32x32 MFMA, v1 128x128),
     the kernel picked per shape by ``ops.autotune`` among those and hipBLASLt (through ATen)."""
+    if weight.dtype == torch.float8_e4m3fn:
+        return _linear_w8(x, weight, bias, residual)
     be = backend_for("gemm", x, "cgs_gemm_bf16")
     # K % 8: the kernels' 16-byte row loads (a K=2 coordinate MLP is not GEMM-shaped work anyway)
     if be == "hip" and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
@@ -114,6 +116,31 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     if residual is not None:
         y = y + residual
     return y
+
+
+def _linear_w8(x, weight, bias, residual):
+    """fp8-e4m3fn stored weights (K21, ``--fp8_e4m3fn-unet``): the device kernel widens the weight
+    tiles to bf16 while staging them (exact), so HBM streams half the weight bytes; elsewhere the
+    weight is cast up front (reference ``comfy/ops.py`` manual cast)."""
+    be = backend_for("gemm", x, "cgs_gemm_bf16_w8")
+    K = x.shape[-1]
+    N = weight.shape[0]
+    if be == "hip" and x.dtype == torch.bfloat16 and K % 8 == 0:
+        count("gemm_w8", "hip")
+        a = x.reshape(-1, K)
+        if a.stride(-1) != 1 or (a.shape[0] > 1 and a.stride(0) < K) or a.stride(0) % 8 or a.data_ptr() % 16:
+            a = a.contiguous()
+        M = a.shape[0]
+        w = weight.contiguous()
+        epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0)
+        r = None if residual is None else residual.reshape(M, N).contiguous()
+        b = None if bias is None else bias.to(torch.bfloat16).contiguous()
+        out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+        _check(_lib().cgs_gemm_bf16_w8(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(b), _ptr(r), M, N, K,
+                                       a.stride(0), K, N, N if r is not None else 0, epi, 1.0, _stream()),
+               "cgs_gemm_bf16_w8")
+        return out.view(*x.shape[:-1], N)
+    return linear(x, weight.to(x.dtype), None if bias is None else bias.to(x.dtype), residual)
 
 
 def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:

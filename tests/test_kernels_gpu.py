@@ -322,3 +322,34 @@ def test_vae_mid_attention_block_native(cuda):
     st = ops.stats()
     assert st.get(("attention", "hip"), 0) == 1 and st.get(("attention", "lib"), 0) == 0, st
     assert _rel(out.cpu(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 640, 640), (77, 1280, 2048), (1000, 333 * 8, 96)])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
+def test_gemm_fp8_weights(cuda, M, N, K, epi):
+    """K21: bf16 activations x fp8-e4m3fn weights; the kernel's in-register widening is exact, so the
+    result matches the GEMM on the upcast weights (fp32 reference)."""
+    torch.manual_seed(4)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w8 = (torch.randn(N, K, device=cuda) * 0.5).to(torch.float8_e4m3fn)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
+    y = ops.linear(x, w8, b, residual=r)
+    assert ops.stats().get(("gemm_w8", "hip"), 0) == 1
+    ref = x.float() @ w8.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if r is not None:
+        ref = ref + r.float()
+    assert _rel(y, ref) < 1e-2
+
+
+def test_fp8_e4m3_decode_rule_is_exact():
+    """The kernel's e4m3fn -> bf16 bit rule reproduces torch's own cast for every non-NaN byte."""
+    idx = torch.arange(256)
+    ref = torch.arange(256, dtype=torch.uint8).view(torch.float8_e4m3fn).float().to(torch.bfloat16)
+    ref = ref.view(torch.int16).int() & 0xFFFF
+    s, e, m = (idx & 0x80) << 8, (idx >> 3) & 15, idx & 7
+    mag = torch.where(e > 0, ((e + 120) << 7) | (m << 4), (m.float() * 0.001953125).view(torch.int32) >> 16)
+    nan = (idx & 0x7F) == 0x7F
+    assert torch.equal((s | mag)[~nan], ref[~nan])
