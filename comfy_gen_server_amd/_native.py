@@ -109,6 +109,7 @@ KERNEL_SIGNATURES = {
     "cgs_grn_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P],          # x, gamma, beta, y, ws, N, HW, C
     # host (mmap) -> device upload through pinned double buffers (csrc/kernels/io.hip)
     "cgs_h2d_upload": [_P, _P, _L, _L, _I, _P],                        # src, dst, nbytes, chunk, threads
+    "cgs_softmax_rows": [_P, _P, _L, _I, _F, _I, _P],                  # x, y(f32), rows, cols, scale, dtype
     # bf16 activations x fp8-e4m3fn weights (K21), same epilogues as cgs_gemm_bf16
     "cgs_gemm_bf16_w8": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
     "cgs_gemm_bf16_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],

@@ -286,3 +286,39 @@ CGS_EXPORT int cgs_grn_nhwc(const void* x, const void* gamma, const void* beta, 
                                                                                 y, total, HW, C));
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// K05: row softmax that materialises the probabilities (SAG / PAG need the attention map):
+// y[r, :] = softmax(scale * x[r, :]) in fp32. One wave per row, three passes over the row
+// (max, sum of exp, normalised write) straight from L2 for rows up to a few thousand columns.
+// ---------------------------------------------------------------------------------------------
+namespace {
+template <int DT>
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const void* x, float* y, long long rows, int cols,
+                                                           float scale) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long r = blockIdx.x * 4LL + wave;
+  if (r >= rows) return;
+  const long long base = r * cols;
+  float mx = -INFINITY;
+  for (int c = lane; c < cols; c += 64) mx = fmaxf(mx, ldv<DT>(x, base + c) * scale);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += __expf(ldv<DT>(x, base + c) * scale - mx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float inv = 1.f / s;
+  for (int c = lane; c < cols; c += 64) y[base + c] = __expf(ldv<DT>(x, base + c) * scale - mx) * inv;
+}
+}  // namespace
+
+CGS_EXPORT int cgs_softmax_rows(const void* x, float* y, long long rows, int cols, float scale, int dtype,
+                                hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (cols <= 0) return (int)hipErrorInvalidValue;
+  const long long blocks = (rows + 3) / 4;
+  if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  CGS_DISPATCH_DT(dtype, softmax_rows_kernel, <<<(unsigned)blocks, 256, 0, stream>>>(x, y, rows, cols, scale));
+  return (int)hipGetLastError();
+}

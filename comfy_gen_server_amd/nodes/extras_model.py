@@ -219,15 +219,8 @@ class PerpNeg:
 
 # ================================================================ attention-based guidance
 def attention_with_probs(q, k, v, heads):
-    """Attention that also returns the softmax probabilities [(b*h), Sq, Sk] (fp32)."""
-    b, sq, hd = q.shape
-    d = hd // heads
-    qh = q.reshape(b, sq, heads, d).permute(0, 2, 1, 3).reshape(b * heads, sq, d).float()
-    kh = k.reshape(b, -1, heads, d).permute(0, 2, 1, 3).reshape(b * heads, -1, d).float()
-    vh = v.reshape(b, -1, heads, d).permute(0, 2, 1, 3).reshape(b * heads, -1, d).float()
-    p = torch.softmax(torch.bmm(qh, kh.transpose(1, 2)) * (d ** -0.5), dim=-1)
-    o = torch.bmm(p, vh).reshape(b, heads, sq, d).permute(0, 2, 1, 3).reshape(b, sq, hd)
-    return o.to(q.dtype), p
+    """Attention that also returns the softmax probabilities [(b*h), Sq, Sk] (fp32); K05 op."""
+    return ops.attention_with_probs(q, k, v, heads)
 
 
 def gaussian_blur_2d(img, kernel_size, sigma):

@@ -661,3 +661,30 @@ def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor) -> torch.
     nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
     scale = (1.0 + gamma.float().reshape(1, 1, 1, C) * nx).to(x.dtype)
     return torch.addcmul(beta.to(x.dtype).reshape(1, 1, 1, C), x, scale)
+
+
+def softmax_rows(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """fp32 softmax over the last dim of ``scale * x`` (K05: the materialised attention map SAG /
+    PAG read). Device path: one wave per row."""
+    be = backend_for("softmax", x, "cgs_softmax_rows")
+    if be == "hip" and x.dtype in _DT and x.numel() > 0:
+        count("softmax", "hip")
+        xc = x.contiguous()
+        y = torch.empty(xc.shape, device=x.device, dtype=torch.float32)
+        _check(_lib().cgs_softmax_rows(xc.data_ptr(), y.data_ptr(), xc.numel() // xc.shape[-1], xc.shape[-1],
+                                       float(scale), _DT[x.dtype], _stream()), "cgs_softmax_rows")
+        return y
+    return torch.softmax(x.float() * scale, dim=-1)
+
+
+def attention_with_probs(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int):
+    """Attention that also returns the probabilities [(b*heads), Sq, Sk] in fp32 (K05). Scores and
+    the PV product are fp32 batched GEMMs (hipBLASLt); the softmax writing P is the HIP kernel."""
+    b, sq, hd = q.shape
+    d = hd // heads
+    qh = q.reshape(b, sq, heads, d).permute(0, 2, 1, 3).reshape(b * heads, sq, d).float()
+    kh = k.reshape(b, -1, heads, d).permute(0, 2, 1, 3).reshape(b * heads, -1, d).float()
+    vh = v.reshape(b, -1, heads, d).permute(0, 2, 1, 3).reshape(b * heads, -1, d).float()
+    p = softmax_rows(torch.bmm(qh, kh.transpose(1, 2)), d ** -0.5)
+    o = torch.bmm(p, vh).reshape(b, heads, sq, d).permute(0, 2, 1, 3).reshape(b, sq, hd)
+    return o.to(q.dtype), p

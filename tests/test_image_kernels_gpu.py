@@ -124,3 +124,27 @@ def test_grn_gpu(cuda, dtype):
     ref = _ref_grn(x.to(dtype), g.to(dtype), b.to(dtype))
     rel = ((y - ref).norm() / ref.norm()).item()
     assert rel < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_softmax_rows_and_attention_probs_gpu(cuda, dtype):
+    """K05: the materialised attention map (SAG / PAG) from the HIP row softmax == fp32 reference."""
+    x = torch.randn(37, 1024) * 4
+    ops.reset_stats()
+    y = ops.softmax_rows(x.to(cuda, dtype), 0.125).cpu()
+    assert ops.stats().get(("softmax", "hip"), 0) == 1
+    assert torch.allclose(y, torch.softmax(x.to(dtype).float() * 0.125, -1), atol=1e-5)
+    q, k, v = (torch.randn(2, 256, 4 * 64) for _ in range(3))
+    o, p = ops.attention_with_probs(q.to(cuda), k.to(cuda), v.to(cuda), 4)
+    qh, kh = (t.view(2, 256, 4, 64).transpose(1, 2).reshape(8, 256, 64) for t in (q, k))
+    pref = torch.softmax(qh @ kh.transpose(1, 2) / 8.0, -1)
+    assert torch.allclose(p.cpu(), pref, atol=1e-5)
+    from comfy_gen_server_amd.ops.core import attention_reference
+    assert torch.allclose(o.cpu(), attention_reference(q, k, v, 4), atol=1e-4)
+
+
+def test_attention_probs_cpu():
+    q, k, v = (torch.randn(1, 16, 2 * 8) for _ in range(3))
+    o, p = ops.attention_with_probs(q, k, v, 2)
+    assert p.shape == (2, 16, 16) and torch.allclose(p.sum(-1), torch.ones(2, 16))
