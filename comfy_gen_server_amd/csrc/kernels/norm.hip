@@ -6,9 +6,9 @@
 //   1. gn_partial : block = (pixel chunk, n); each lane owns fixed 8-channel chunks of the row and
 //      accumulates shifted sums (shift = first pixel) -> per-wave (mean, M2) -> Chan combine over
 //      the 4 waves in LDS -> per-(n, block, c) partial.
-//   2. gn_finalize: one wave per (n, g) combines blocks x channels (Chan) -> mean/rstd -> per-(n,c)
-//      affine a, b (the pre-add shifts the channel mean only, so it folds into b).
-//   3. gn_apply   : y = x*a + b (+SiLU), 16-byte vectors.
+//   2. gn_finalize: one block per (n, g), exact two-pass combine of the blocks x channels partials ->
+//      mean/rstd -> per-(n,c) affine a, b (the pre-add shifts the channel mean only, so it folds into b).
+//   3. gn_apply   : y = x*a + b (+SiLU), 16-byte vectors, per-thread channel chunk fixed (a, b in registers).
 // LayerNorm: one wave per row, two-pass mean/var from registers, 16-byte vectors.
 #include "common.h"
 
@@ -103,82 +103,98 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   }
 }
 
-__global__ void gn_finalize_kernel(const float* __restrict__ part, const void* __restrict__ gamma,
-                                   const void* __restrict__ beta, const void* __restrict__ pre_add,
-                                   float* __restrict__ ab, int HW, int C, int G, int ppb, int nb, float eps,
-                                   int wdt) {
-  // one wave per (n, g); blockDim = 64
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ part, const void* __restrict__ gamma,
+                                                         const void* __restrict__ beta, const void* __restrict__ pre_add,
+                                                         float* __restrict__ ab, int HW, int C, int G, int ppb, int nb,
+                                                         float eps, int wdt) {
+  // one 256-thread block per (n, g). Every channel of a pixel block shares that block's pixel count, so
+  // the group statistics are an exact two-pass combine of the per-(block, channel) (mean, M2) partials:
+  //   mean = sum n_b*mean_b / sum n_b,   M2 = sum M2_b + sum n_b*(mean_b - mean)^2
+  // (no per-item divisions or serial Chan chain: the partials are re-read from L2 in the second pass).
   const int g = blockIdx.x;
   const int n = blockIdx.y;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
   const int Cg = C / G;
   const int items = Cg * nb;
-  float n_a = 0.f, mean = 0.f, m2 = 0.f;
-  for (int it = lane; it < items; it += 64) {
-    int b = it / Cg, cc = it % Cg;
+  __shared__ float red[2][4];
+  auto chan_shift = [&](int c) -> float {
+    if (!pre_add) return 0.f;
+    return (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
+                             : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c]) : ((const float*)pre_add)[n * C + c]);
+  };
+  auto block_sum2 = [&](float& a, float& b) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if ((tid & 63) == 0) { red[0][tid >> 6] = a; red[1][tid >> 6] = b; }
+    __syncthreads();
+    a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    __syncthreads();
+  };
+  float sw = 0.f, cntsum = 0.f;
+  for (int it = tid; it < items; it += 256) {
+    int b = it / Cg, cc = it - b * Cg;
     int c = g * Cg + cc;
-    int p0 = b * ppb;
-    float n_b = (float)(min(HW, p0 + ppb) - p0);
-    if (n_b <= 0.f) continue;
+    float n_b = (float)(min(HW, b * ppb + ppb) - b * ppb);
+    float mb = part[(((size_t)n * nb + b) * C + c) * 2] + chan_shift(c);
+    sw += n_b * mb;
+    cntsum += n_b;
+  }
+  block_sum2(sw, cntsum);
+  const float mean = sw / fmaxf(cntsum, 1.f);
+  float m2 = 0.f, dummy = 0.f;
+  for (int it = tid; it < items; it += 256) {
+    int b = it / Cg, cc = it - b * Cg;
+    int c = g * Cg + cc;
+    float n_b = (float)(min(HW, b * ppb + ppb) - b * ppb);
     size_t o = (((size_t)n * nb + b) * C + c) * 2;
-    float mb = part[o], m2b = part[o + 1];
-    if (pre_add) {
-      float e = (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
-                                  : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c])
-                                                     : ((const float*)pre_add)[n * C + c]);
-      mb += e;
-    }
-    float nn = n_a + n_b;
-    float d = mb - mean;
-    mean += d * n_b / nn;
-    m2 += m2b + d * d * n_a * n_b / nn;
-    n_a = nn;
+    float d = part[o] + chan_shift(c) - mean;
+    m2 += part[o + 1] + n_b * d * d;
   }
-  // butterfly Chan-combine across the wave
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float n_b = __shfl_xor(n_a, o, 64);
-    float mb = __shfl_xor(mean, o, 64);
-    float m2b = __shfl_xor(m2, o, 64);
-    float nn = n_a + n_b;
-    if (nn > 0.f) {
-      float d = mb - mean;
-      mean += d * n_b / nn;
-      m2 += m2b + d * d * n_a * n_b / nn;
-      n_a = nn;
-    }
-  }
-  float var = m2 / fmaxf(n_a, 1.f);
+  block_sum2(m2, dummy);
+  float var = m2 / fmaxf(cntsum, 1.f);
   float rstd = rsqrtf(var + eps);
-  for (int cc = lane; cc < Cg; cc += 64) {
+  for (int cc = tid; cc < Cg; cc += 256) {
     int c = g * Cg + cc;
-    float gm = 1.f, bt = 0.f, e = 0.f;
+    float gm = 1.f, bt = 0.f;
     if (gamma) gm = (wdt == CGS_BF16) ? bf2f(((const u16*)gamma)[c]) : (wdt == CGS_F16 ? h2f(((const u16*)gamma)[c]) : ((const float*)gamma)[c]);
     if (beta) bt = (wdt == CGS_BF16) ? bf2f(((const u16*)beta)[c]) : (wdt == CGS_F16 ? h2f(((const u16*)beta)[c]) : ((const float*)beta)[c]);
-    if (pre_add) e = (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
-                                        : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c]) : ((const float*)pre_add)[n * C + c]);
     float a = rstd * gm;
     ab[((size_t)n * C + c) * 2] = a;
-    ab[((size_t)n * C + c) * 2 + 1] = (e - mean) * a + bt;
+    ab[((size_t)n * C + c) * 2 + 1] = (chan_shift(c) - mean) * a + bt;
   }
 }
 
 template <int DT, bool SILU>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y,
-                                                      const float* __restrict__ ab, long long total_chunks, int HW,
-                                                      int C) {
+                                                      const float* __restrict__ ab, int rows_total, int rows_per_iter,
+                                                      int HW, int C) {
+  // The grid stride is a whole number of rows, so every thread keeps ONE 8-channel chunk for its whole
+  // life: its 16 affine coefficients stay in registers and are reloaded only when the image index n
+  // changes (no 64-bit index divisions, no per-element coefficient loads).
   const int cpr = C >> 3;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_chunks;
-       i += (long long)gridDim.x * blockDim.x) {
-    long long row = i / cpr;
-    int ch = (int)(i - row * cpr);
-    int n = (int)(row / HW);
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= rows_per_iter * cpr) return;
+  const int ch = tid % cpr;
+  int cur_n = -1;
+  float a[8], bb[8];
+  for (int row = tid / cpr; row < rows_total; row += rows_per_iter) {
+    const int n = row / HW;
+    if (n != cur_n) {
+      cur_n = n;
+      const float4* abp = reinterpret_cast<const float4*>(ab + ((size_t)n * C + ch * 8) * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float4 t = abp[j];
+        a[2 * j] = t.x; bb[2 * j] = t.y; a[2 * j + 1] = t.z; bb[2 * j + 1] = t.w;
+      }
+    }
+    const size_t i = (size_t)row * cpr + ch;
     s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
-    const float* abp = ab + ((size_t)n * C + ch * 8) * 2;
     s16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float f = cvt_in<DT>((u16)v[j]) * abp[2 * j] + abp[2 * j + 1];
+      float f = cvt_in<DT>((u16)v[j]) * a[j] + bb[j];
       if (SILU) f = silu_f(f);
       o[j] = (short)cvt_out<DT>(f);
     }
@@ -212,16 +228,22 @@ CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, 
   else
     gn_partial_kernel<CGS_F16><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb,
                                                                                    nb, CS);
-  gn_finalize_kernel<<<dim3(G, N), 64, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
-  long long chunks = (long long)N * HW * (C / 8);
+  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
+  const int cpr = C / 8;
+  const long long rows_total = (long long)N * HW;
+  if (rows_total == 0) return (int)hipGetLastError();
+  if (rows_total * cpr >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  long long chunks = rows_total * cpr;
   long long nbk = (chunks + 255) / 256;
   int blocks = (int)(nbk < 8192 ? nbk : 8192);
+  int rows_per_iter = (blocks * 256) / cpr;  // cpr <= 1024 <= blocks * 256 whenever chunks >= cpr
+  if (rows_per_iter < 1) rows_per_iter = 1, blocks = (cpr + 255) / 256;
   if (dtype == CGS_BF16) {
-    if (silu) gn_apply_kernel<CGS_BF16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
-    else gn_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
+    if (silu) gn_apply_kernel<CGS_BF16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
+    else gn_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
   } else {
-    if (silu) gn_apply_kernel<CGS_F16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
-    else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, chunks, HW, C);
+    if (silu) gn_apply_kernel<CGS_F16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
+    else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
   }
   return (int)hipGetLastError();
 }

@@ -44,6 +44,22 @@ def test_groupnorm(cuda, N, C, H, W, G, silu):
     assert _rel(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,C,H,W,pre,shift", [(4, 320, 128, 128, False, 1.0), (3, 640, 96, 80, True, 1.0),
+                                                 (2, 128, 256, 256, False, 40.0), (5, 512, 33, 17, False, 8.0)])
+def test_groupnorm_large_and_no_preadd(cuda, N, C, H, W, pre, shift):
+    # grid-stride rows cross image boundaries (per-thread coefficient reload), no pre-add, large means
+    torch.manual_seed(1)
+    x = (torch.randn(N, C, H, W, device=cuda) + shift).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(C, device=cuda).to(torch.bfloat16)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16)
+    p = torch.randn(N, C, device=cuda).to(torch.bfloat16) if pre else None
+    y = ops.group_norm(x, 32, w, b, 1e-6, silu=True, pre_add=p)
+    xf = x.float() + (p.float()[:, :, None, None] if pre else 0.0)
+    ref = F.silu(F.group_norm(xf, 32, w.float(), b.float(), 1e-6))
+    assert ops.stats().get(("groupnorm", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
 @pytest.mark.parametrize("rows,C", [(100, 640), (4096, 1280), (77, 768), (33, 2048), (5, 5120)])
 def test_layernorm(cuda, rows, C):
     torch.manual_seed(0)
