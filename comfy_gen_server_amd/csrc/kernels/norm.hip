@@ -9,7 +9,7 @@
 //   2. gn_finalize: one block per (n, g), exact two-pass combine of the blocks x channels partials ->
 //      mean/rstd -> per-(n,c) affine a, b (the pre-add shifts the channel mean only, so it folds into b).
 //   3. gn_apply   : y = x*a + b (+SiLU), 16-byte vectors, per-thread channel chunk fixed (a, b in registers).
-// LayerNorm: one wave per row, two-pass mean/var from registers, 16-byte vectors.
+// LayerNorm: 8-64 lanes per row (sized to the row), two-pass mean/var from registers, 16-byte vectors.
 #include "common.h"
 
 #define GN_THREADS 256
@@ -253,41 +253,54 @@ CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, 
 // ------------------------------------------------------------------------------------------------
 #define LN_MAXK 8  // chunks of 8 per lane -> C <= 4096 in registers
 
-template <int DT>
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+  // butterfly over the LPR lanes of one row (LPR-aligned lane groups of the 64-wide wave)
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LPR lanes per row (64/LPR rows per wave): SDXL's C=640 rows are 80 16-byte chunks = 5 per lane at
+// LPR=16 and C=1280 rows 5 per lane at LPR=32, so every lane slot carries data (one row per full wave
+// would leave 37-75 % of the second chunk round idle) and the shuffle reductions are shorter.
+template <int DT, int LPR>
 __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ x, u16* __restrict__ y,
                                                        const u16* __restrict__ w, const u16* __restrict__ b, int rows,
                                                        int C, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  constexpr int RPB = 256 / LPR;  // rows per block
+  const int lane = threadIdx.x % LPR;
+  const int row = blockIdx.x * RPB + threadIdx.x / LPR;
+  const bool live = row < rows;   // dead rows still join the shuffles (whole wave stays converged)
   const int nch = C >> 3;
-  const u16* xr = x + (size_t)row * C;
+  const u16* xr = x + (size_t)(live ? row : 0) * C;
   float v[LN_MAXK][8];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < LN_MAXK; ++k) {
-    int ch = lane + 64 * k;
-    if (ch < nch) {
+    int ch = lane + LPR * k;
+    if (live && ch < nch) {
       s16x8 t = reinterpret_cast<const s16x8*>(xr)[ch];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { v[k][j] = cvt_in<DT>((u16)t[j]); s += v[k][j]; }
     }
   }
-  float mean = wave_sum(s) / C;
+  float mean = group_sum<LPR>(s) / C;
   float q = 0.f;
 #pragma unroll
   for (int k = 0; k < LN_MAXK; ++k) {
-    int ch = lane + 64 * k;
-    if (ch < nch) {
+    int ch = lane + LPR * k;
+    if (live && ch < nch) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { float d = v[k][j] - mean; q += d * d; }
     }
   }
-  float rstd = rsqrtf(wave_sum(q) / C + eps);
+  float rstd = rsqrtf(group_sum<LPR>(q) / C + eps);
+  if (!live) return;
   u16* yr = y + (size_t)row * C;
 #pragma unroll
   for (int k = 0; k < LN_MAXK; ++k) {
-    int ch = lane + 64 * k;
+    int ch = lane + LPR * k;
     if (ch < nch) {
       s16x8 wv, bv;
       if (w) wv = reinterpret_cast<const s16x8*>(w)[ch];
@@ -325,13 +338,20 @@ __global__ __launch_bounds__(256) void layernorm_big_kernel(const u16* __restric
 CGS_EXPORT int cgs_layernorm(const void* x, void* y, const void* w, const void* b, int rows, int C, float eps,
                              int dtype, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  dim3 grid((rows + 3) / 4);
-  if (C <= 64 * 8 * LN_MAXK) {
-    if (dtype == CGS_BF16)
-      layernorm_kernel<CGS_BF16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
-    else
-      layernorm_kernel<CGS_F16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
+  const int nch = C / 8;
+  if (nch <= 64 * LN_MAXK) {
+    // fewest lanes per row that still fits the row in LN_MAXK chunks per lane
+    const int lpr = nch <= 8 * LN_MAXK ? 8 : nch <= 16 * LN_MAXK ? 16 : nch <= 32 * LN_MAXK ? 32 : 64;
+    dim3 grid((rows + 256 / lpr - 1) / (256 / lpr));
+#define CGS_LN_LAUNCH(L)                                                                                           \
+  if (dtype == CGS_BF16)                                                                                           \
+    layernorm_kernel<CGS_BF16, L><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps); \
+  else                                                                                                             \
+    layernorm_kernel<CGS_F16, L><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
+    if (lpr == 8) { CGS_LN_LAUNCH(8) } else if (lpr == 16) { CGS_LN_LAUNCH(16) } else if (lpr == 32) { CGS_LN_LAUNCH(32) } else { CGS_LN_LAUNCH(64) }
+#undef CGS_LN_LAUNCH
   } else {
+    dim3 grid((rows + 3) / 4);
     if (dtype == CGS_BF16)
       layernorm_big_kernel<CGS_BF16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
     else

@@ -60,7 +60,8 @@ def test_groupnorm_large_and_no_preadd(cuda, N, C, H, W, pre, shift):
     assert _rel(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("rows,C", [(100, 640), (4096, 1280), (77, 768), (33, 2048), (5, 5120)])
+@pytest.mark.parametrize("rows,C", [(100, 640), (4096, 1280), (77, 768), (33, 2048), (5, 5120), (1001, 320),
+                                    (37, 512), (16384, 640), (3, 4096), (70, 1024)])
 def test_layernorm(cuda, rows, C):
     torch.manual_seed(0)
     x = (torch.randn(rows, C, device=cuda) * 2 + 0.5).to(torch.bfloat16)
