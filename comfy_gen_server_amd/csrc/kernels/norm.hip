@@ -4,7 +4,7 @@
 //
 // GroupNorm = 3 small launches, every one fully coalesced on NHWC rows:
 //   1. gn_partial : block = (pixel chunk, n); each lane owns fixed 8-channel chunks of the row and
-//      accumulates shifted sums (shift = first pixel) -> per-wave (mean, M2) -> Chan combine over
+//      accumulates shifted sums (shift = the block's first pixel; 4 rows of loads in flight per wave) -> per-wave (mean, M2) -> Chan combine over
 //      the 4 waves in LDS -> per-(n, block, c) partial.
 //   2. gn_finalize: one block per (n, g), exact two-pass combine of the blocks x channels partials ->
 //      mean/rstd -> per-(n,c) affine a, b (the pre-add shifts the channel mean only, so it folds into b).
@@ -22,10 +22,13 @@ static inline int gn_pix_per_block(int N, int HW) {
   return ppb;
 }
 
-template <int DT>
+template <int DT, int KM>
 __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, float* __restrict__ part,
                                                                int HW, int C, int ppb, int nb, int CS) {
-  // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget)
+  // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget).
+  // KM = 16-byte chunk rounds per lane (ceil(CS / 512)); each wave keeps GN_UNROLL rows of loads in
+  // flight before accumulating (one row per wave per trip left the HBM pipe half empty).
+  constexpr int GN_UNROLL = 4;
   const int n = blockIdx.y;
   const int blk = blockIdx.x;
   const int c0 = blockIdx.z * CS;
@@ -34,33 +37,46 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nchunk = CS >> 3;
-  float s1[GN_MAX_CHUNKS_PER_LANE][8], s2[GN_MAX_CHUNKS_PER_LANE][8], sh[GN_MAX_CHUNKS_PER_LANE][8];
-  int cnt = 0;
-#pragma unroll
-  for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { s1[k][j] = 0.f; s2[k][j] = 0.f; sh[k][j] = 0.f; }
   const u16* xn = x + (size_t)n * HW * C + c0;
-  bool first = true;
-  for (int p = p0 + wave; p < p1; p += 4) {
-    const u16* row = xn + (size_t)p * C;
+  // shift = the block's first pixel (shared by all 4 waves): keeps the shifted sums well conditioned
+  float s1[KM][8], s2[KM][8], sh[KM][8];
 #pragma unroll
-    for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k) {
-      int ch = lane + 64 * k;
-      if (ch < nchunk) {
-        s16x8 v = *reinterpret_cast<const s16x8*>(row + ch * 8);
+  for (int k = 0; k < KM; ++k) {
+    int ch = lane + 64 * k;
+    s16x8 v = {};
+    if (ch < nchunk && p0 < p1) v = *reinterpret_cast<const s16x8*>(xn + (size_t)p0 * C + ch * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float f = cvt_in<DT>((u16)v[j]);
-          if (first) sh[k][j] = f;
-          float d = f - sh[k][j];
-          s1[k][j] += d;
-          s2[k][j] += d * d;
+    for (int j = 0; j < 8; ++j) { sh[k][j] = cvt_in<DT>((u16)v[j]); s1[k][j] = 0.f; s2[k][j] = 0.f; }
+  }
+  int cnt = 0;
+  for (int p = p0 + wave; p < p1; p += 4 * GN_UNROLL) {
+    s16x8 buf[GN_UNROLL][KM];
+#pragma unroll
+    for (int u = 0; u < GN_UNROLL; ++u) {
+      const int pu = p + 4 * u;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        int ch = lane + 64 * k;
+        if (pu < p1 && ch < nchunk) buf[u][k] = *reinterpret_cast<const s16x8*>(xn + (size_t)pu * C + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GN_UNROLL; ++u) {
+      if (p + 4 * u < p1) {
+        cnt++;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          if (lane + 64 * k < nchunk) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float d = cvt_in<DT>((u16)buf[u][k][j]) - sh[k][j];
+              s1[k][j] += d;
+              s2[k][j] += d * d;
+            }
+          }
         }
       }
     }
-    first = false;
-    cnt++;
   }
   // per-wave (mean, M2) per channel -> LDS, then Chan-combine the 4 waves
   extern __shared__ __attribute__((aligned(16))) float gn_smem[];
@@ -69,7 +85,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   __shared__ int lcnt[4];
   if (lane == 0) lcnt[wave] = cnt;
 #pragma unroll
-  for (int k = 0; k < GN_MAX_CHUNKS_PER_LANE; ++k) {
+  for (int k = 0; k < KM; ++k) {
     int ch = lane + 64 * k;
     if (ch < nchunk) {
 #pragma unroll
@@ -222,12 +238,14 @@ CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, 
   float* part = (float*)ws;
   float* ab = part + (size_t)N * nb * C * 2;
   dim3 g1(nb, N, ns);
-  if (dtype == CGS_BF16)
-    gn_partial_kernel<CGS_BF16><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb,
-                                                                                    nb, CS);
-  else
-    gn_partial_kernel<CGS_F16><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb,
-                                                                                   nb, CS);
+  const int km = (CS / 8 + 63) / 64;  // 1..4
+#define CGS_GN_PARTIAL(KMV)                                                                                     \
+  if (dtype == CGS_BF16)                                                                                        \
+    gn_partial_kernel<CGS_BF16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb, CS); \
+  else                                                                                                          \
+    gn_partial_kernel<CGS_F16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb, CS);
+  if (km == 1) { CGS_GN_PARTIAL(1) } else if (km == 2) { CGS_GN_PARTIAL(2) } else if (km == 3) { CGS_GN_PARTIAL(3) } else { CGS_GN_PARTIAL(4) }
+#undef CGS_GN_PARTIAL
   gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
   const int cpr = C / 8;
   const long long rows_total = (long long)N * HW;
