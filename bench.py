@@ -34,8 +34,16 @@ def main():
     ap.add_argument("--cfg", type=float, default=8.0)
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (use with --family tiny)")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the denoiser")
-    ap.add_argument("--profile-ops", action="store_true")
+    ap.add_argument("--profile-ops", action="store_true", help="(kept for compatibility; op backends are always reported)")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        # No launcher: become the launcher. This parent never imports torch / touches the GPU; it
+        # starts one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* like torchrun).
+        sys.exit(_spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; launch {args.gpus} ranks")
 
     if args.cpu:
         os.environ["CGS_FORCE_CPU"] = "1"
@@ -47,6 +55,7 @@ def main():
     import torch
     from comfy_gen_server_amd.parallel.comm import init_from_env
     comm = init_from_env(backend="gloo" if args.cpu else None)
+    assert comm.world == args.gpus, f"communicator has {comm.world} ranks, --gpus {args.gpus}"
     from comfy_gen_server_amd.runtime import device as dm
     if not args.cpu:
         dm.set_device_index(comm.local_rank)
@@ -113,6 +122,8 @@ def main():
             "value": round(imgs_per_sec, 4),
             "unit": "images/s",
             "n_gpus": N,
+            "ranks": comm.world,
+            "backend": comm.backend or "single",
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 2),
@@ -133,10 +144,25 @@ def main():
         from comfy_gen_server_amd.parallel import dp as _dp
         if _dp.STAGE_TIMES:
             res["stage_seconds"] = {k: [round(x, 3) for x in v] for k, v in _dp.STAGE_TIMES.items()}
-        if args.profile_ops:
-            res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
+        res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
         print(json.dumps(res), flush=True)
     comm.shutdown()
+
+
+def _spawn_ranks(n: int) -> int:
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max((abs(rc) for rc in rcs), default=0)
 
 
 if __name__ == "__main__":

@@ -683,7 +683,8 @@ def common_ksampler(model, seed, steps, cfg, sampler_name, scheduler, positive, 
     callback = NH.prepare_callback(model, steps)
     samples = S.sample(model, noise, steps, cfg, sampler_name, scheduler, positive, negative, latent_image,
                        denoise=denoise, disable_noise=disable_noise, start_step=start_step, last_step=last_step,
-                       force_full_denoise=force_full_denoise, noise_mask=noise_mask, callback=callback, seed=seed)
+                       force_full_denoise=force_full_denoise, noise_mask=noise_mask, callback=callback, seed=seed,
+                       noise_inds=latent.get("batch_index"))
     out = latent.copy()
     out["samples"] = samples
     return (out,)

@@ -475,7 +475,8 @@ class SamplerCustom:
         cb = NH.prepare_callback(model, sigmas.shape[-1] - 1, x0_output)
         samples = S.sample_custom(model, noise, cfg, sampler, sigmas, positive, negative, latent["samples"],
                                   noise_mask=latent.get("noise_mask"), callback=cb,
-                                  disable_pbar=not progress.PROGRESS_BAR_ENABLED, seed=noise_seed)
+                                  disable_pbar=not progress.PROGRESS_BAR_ENABLED, seed=noise_seed,
+                                  noise_inds=latent.get("batch_index"))
         return _finish(latent, samples, x0_output, model.model.process_latent_out)
 
 

@@ -325,6 +325,11 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
             x.shape[1] % (8 * ((x.shape[1] + 2047) // 2048)) == 0:
         count("groupnorm", "hip")
         N, C, H, W = x.shape
+        # the kernel reads gamma/beta in the activation dtype: cast fp8 / offloaded / mixed-dtype params
+        if weight.dtype != x.dtype or weight.device != x.device or not weight.is_contiguous():
+            weight = weight.to(device=x.device, dtype=x.dtype).contiguous()
+        if bias is not None and (bias.dtype != x.dtype or bias.device != x.device or not bias.is_contiguous()):
+            bias = bias.to(device=x.device, dtype=x.dtype).contiguous()
         xc = x.contiguous(memory_format=torch.channels_last)
         y = torch.empty_like(xc, memory_format=torch.channels_last)
         pa = None
@@ -340,8 +345,8 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
     count("groupnorm", "torch" if x.device.type == "cpu" else "lib")
     if pre_add is not None:
         x = x + pre_add.to(x.dtype)[:, :, None, None]
-    y = F.group_norm(x.float(), groups, None if weight is None else weight.float(),
-                     None if bias is None else bias.float(), eps)
+    y = F.group_norm(x.float(), groups, None if weight is None else weight.to(x.device, torch.float32),
+                     None if bias is None else bias.to(x.device, torch.float32), eps)
     if silu:
         y = F.silu(y)
     return y.to(x.dtype)
@@ -537,6 +542,85 @@ def euler_step(x: torch.Tensor, denoised: torch.Tensor, noise: torch.Tensor | No
     if noise is not None and sigma_up > 0:
         x = x + noise * sigma_up
     return x
+
+
+# ----------------------------------------------------------------------------------------------
+# Counter-based noise (csrc/kernels/rng.hip; CPU mirror sampling/rng.py)
+# ----------------------------------------------------------------------------------------------
+def _numel1(shape):
+    n = 1
+    for d in shape[1:]:
+        n *= int(d)
+    return n
+
+
+def philox_randn(shape, seed: int, inds, stream: int, device=None, dtype=torch.float32,
+                 dev_step: torch.Tensor | None = None) -> torch.Tensor:
+    """N(0,1) noise [B, ...] where image b's values depend only on (seed, inds[b], stream).
+
+    ``dev_step`` (device int64 scalar) is added to ``stream`` inside the kernel, so a captured graph
+    can advance the stream per replay without re-recording."""
+    from ..sampling import rng
+    device = torch.device("cpu") if device is None else torch.device(device)
+    probe = torch.empty(0, device=device)
+    be = backend_for("rng", probe, "cgs_philox_randn")
+    index0, contiguous = rng.contiguous_inds(inds)
+    if be == "hip" and dtype in (torch.float32, torch.bfloat16) and contiguous:
+        count("rng", "hip")
+        out = torch.empty(tuple(shape), device=device, dtype=dtype)
+        _check(_lib().cgs_philox_randn(out.data_ptr(), int(shape[0]), _numel1(shape), int(seed) & ((1 << 64) - 1),
+                                       index0, int(stream), _ptr(dev_step), 1.0, _DT[dtype], _stream()),
+               "cgs_philox_randn")
+        return out
+    if be == "hip" and dtype in (torch.float32, torch.bfloat16):   # scattered indices: one launch per image
+        return torch.cat([philox_randn((1,) + tuple(shape[1:]), seed, [i], stream, device, dtype, dev_step)
+                          for i in inds])
+    count("rng", "torch")
+    if dev_step is not None:
+        stream = int(stream) + int(dev_step.item())
+    return rng.randn_reference(tuple(shape), seed, inds, stream).to(device=device, dtype=dtype)
+
+
+def euler_ancestral_philox(x: torch.Tensor, denoised: torch.Tensor, sigma: float, sigma_down: float,
+                           sigma_up: float, seed: int, inds, stream: int) -> torch.Tensor:
+    """Euler-ancestral update with the step's noise generated in registers (K16+K18): equals
+    ``euler_step(x, denoised, philox_randn(x.shape, seed, inds, stream), ...)`` without the noise tensor."""
+    from ..sampling import rng
+    be = backend_for("euler", x, "cgs_euler_ancestral_philox")
+    index0, contiguous = rng.contiguous_inds(inds)
+    if be == "hip" and contiguous and x.dtype == torch.float32 and denoised.dtype == torch.float32 \
+            and x.is_contiguous() and denoised.is_contiguous() and _numel1(x.shape) % 4 == 0:
+        count("euler", "hip")
+        x = x.clone()
+        _check(_lib().cgs_euler_ancestral_philox(x.data_ptr(), denoised.data_ptr(), int(x.shape[0]), _numel1(x.shape),
+                                                 float(sigma), float(sigma_down), float(sigma_up),
+                                                 int(seed) & ((1 << 64) - 1), index0, int(stream), _stream()),
+               "cgs_euler_ancestral_philox")
+        return x
+    noise = philox_randn(x.shape, seed, inds, stream, device=x.device, dtype=x.dtype) if sigma_up > 0 else None
+    return euler_step(x, denoised, noise, sigma, sigma_down, sigma_up)
+
+
+def brownian_increment(shape, seed: int, inds, t0: float, t1: float, ta: float, tb: float, tol: float,
+                       max_depth: int, scale: float, device=None) -> torch.Tensor:
+    """(W(tb) - W(ta)) * scale of the per-image virtual Brownian tree on [t0, t1] (fp32)."""
+    from ..sampling import rng
+    device = torch.device("cpu") if device is None else torch.device(device)
+    be = backend_for("rng", torch.empty(0, device=device), "cgs_brownian_increment")
+    index0, contiguous = rng.contiguous_inds(inds)
+    if be == "hip" and _numel1(shape) % 4 == 0:
+        if not contiguous:
+            return torch.cat([brownian_increment((1,) + tuple(shape[1:]), seed, [i], t0, t1, ta, tb, tol, max_depth,
+                                                 scale, device) for i in inds])
+        count("rng", "hip")
+        out = torch.empty(tuple(shape), device=device, dtype=torch.float32)
+        _check(_lib().cgs_brownian_increment(out.data_ptr(), int(shape[0]), _numel1(shape),
+                                             int(seed) & ((1 << 64) - 1), index0, float(t0), float(t1), float(ta),
+                                             float(tb), float(tol), int(max_depth), float(scale), _stream()),
+               "cgs_brownian_increment")
+        return out
+    count("rng", "torch")
+    return rng.brownian_reference(tuple(shape), seed, inds, t0, t1, ta, tb, tol, max_depth, scale).to(device)
 
 
 # ----------------------------------------------------------------------------------------------

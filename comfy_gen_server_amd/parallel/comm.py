@@ -28,9 +28,11 @@ class Comm:
         self.backend = None
         self.device = torch.device("cpu")
 
+    degraded = False   # set by the DP engine after a rank failure: the process group is unusable
+
     @property
     def enabled(self):
-        return self.world > 1
+        return self.world > 1 and not self.degraded
 
     def barrier(self):
         if self.enabled:
@@ -111,7 +113,7 @@ class Comm:
     # ---- control plane (R6): the c10d TCPStore (hosted by rank 0) outlives a dead peer, unlike a
     # collective ring, so liveness and degraded-mode result shipping go through it ----
     def store(self):
-        return dist.distributed_c10d._get_default_store() if self.enabled else None
+        return dist.distributed_c10d._get_default_store() if self.world > 1 and dist.is_initialized() else None
 
     def _seq(self):
         self._job_seq = getattr(self, "_job_seq", 0) + 1
@@ -149,7 +151,7 @@ class Comm:
         return torch.load(io.BytesIO(st.get(key)), weights_only=True)
 
     def shutdown(self):
-        if self.enabled and dist.is_initialized():
+        if self.world > 1 and dist.is_initialized():
             dist.destroy_process_group()
 
 

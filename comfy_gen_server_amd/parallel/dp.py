@@ -3,8 +3,9 @@
 One process per GPU. A job = (prompt, negative, batch, seed, steps, cfg, sampler, scheduler, size).
 Rank 0 owns the job and broadcasts it (R1); each rank generates its slice of the batch with the
 reference's per-index noise replay (``prepare_noise`` with ``batch_index`` = the image's global
-index, so the DP result is bit-identical in noise to a single-GPU run of the whole batch); the
-decoded uint8 images are all-gathered (R2) so rank 0 can encode/save them.
+index) for the initial latent, and the per-step ancestral/SDE noise keyed by the same global index
+(``sampling/rng.py``), so a DP run is identical to a single-GPU run of the whole batch; the decoded
+uint8 images are all-gathered (R2) so rank 0 can encode/save them.
 
 Everything per rank is the standard single-GPU path (CLIP -> CFGGuider/KSampler -> VAE), so the
 DP engine scales whatever the kernels deliver on one GPU.
@@ -65,8 +66,9 @@ class _stage:
             STAGE_TIMES.setdefault(self.name, []).append(time.perf_counter() - self.t)
 
 
-def generate_local(patcher, clip, vae, job: Job, index_offset: int, local_batch: int, conds=None):
-    """Generate images [index_offset, index_offset+local_batch) of ``job`` on this rank."""
+def generate_local(patcher, clip, vae, job: Job, index_offset: int, local_batch: int, conds=None, decode=True):
+    """Generate images [index_offset, index_offset+local_batch) of ``job`` on this rank
+    (``decode=False``: return the sampled latents instead of decoded images)."""
     lat_c = 4
     latent = torch.zeros([local_batch, lat_c, job.height // 8, job.width // 8])
     with _stage("clip"):
@@ -80,7 +82,9 @@ def generate_local(patcher, clip, vae, job: Job, index_offset: int, local_batch:
     noise = S.prepare_noise(latent, job.seed, noise_inds=inds)
     with _stage("sample"):
         samples = S.sample(patcher, noise, job.steps, job.cfg, job.sampler, job.scheduler, pos, neg, latent,
-                           denoise=1.0, seed=job.seed)
+                           denoise=1.0, seed=job.seed, noise_inds=inds)
+    if not decode:
+        return samples
     with _stage("vae"):
         return vae.decode(samples)
 
@@ -122,6 +126,9 @@ class DataParallelGenerator:
         if fault_tolerant is None:
             fault_tolerant = os.environ.get("CGS_DP_FAULT_TOLERANT", "0") == "1"
         if getattr(self, "degraded", False):
+            # degraded (after a rank failure): rank 0 alone serves whole jobs; other survivors idle
+            if c.rank != 0:
+                return None
             return to_uint8(generate_local(self.patcher, self.clip, self.vae, job, 0, job.batch))
         job = c.broadcast_object(job)
         per = job.batch // c.world
@@ -155,6 +162,7 @@ class DataParallelGenerator:
         import logging
         c = self.comm
         self.degraded = True
+        c.degraded = True     # collectives over the broken group become local no-ops from here on
         if c.rank != 0:
             c.store_put_tensor(f"cgs/shard/{rid}/{c.rank}", u8)
             return None

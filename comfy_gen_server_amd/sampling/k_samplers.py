@@ -8,9 +8,13 @@ reference evaluates them on device tensors (``get_ancestral_step`` min on tensor
 which costs a device sync per step and breaks hipGraph capture. The element-wise updates of
 Euler / Euler-a run as one fused HIP kernel on the device (``ops.euler_step``).
 
-Noise: the ancestral / SDE noise is drawn from a seeded device Philox generator
-(``extra_args['seed']``), so results are reproducible per seed (the reference draws from the
-global RNG). SDE samplers use an in-tree Brownian tree (``brownian.py``) instead of torchsde.
+Noise: ancestral / SDE noise is counter-based (``rng.py`` / ``csrc/kernels/rng.hip``): the value
+for image b at sampler call k is a function of (``extra_args['seed']``, the image's GLOBAL batch
+index ``extra_args['noise_inds'][b]``, k) only, so a data-parallel split of a batch reproduces the
+one-GPU run exactly (the reference draws ``randn_like`` from the global RNG,
+``comfy/k_diffusion/sampling.py:60-61``). Euler-a generates its noise inside the update kernel.
+SDE samplers use a per-image virtual Brownian tree walked on the device (``brownian.py``) instead of
+torchsde.
 """
 from __future__ import annotations
 
@@ -20,6 +24,7 @@ import torch
 
 from .. import ops
 from .brownian import BrownianTreeNoiseSampler
+from .rng import StepNoise
 
 
 def _f(sigmas):
@@ -38,14 +43,10 @@ def get_ancestral_step(sigma_from: float, sigma_to: float, eta: float = 1.0):
     return down, up
 
 
-def default_noise_sampler(x, seed=None):
+def default_noise_sampler(x, seed=None, inds=None):
     if seed is None:
         return lambda sigma, sigma_next: torch.randn_like(x)
-    gen = torch.Generator(device=x.device).manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
-
-    def sample(sigma, sigma_next):
-        return torch.randn(x.shape, generator=gen, device=x.device, dtype=x.dtype)
-    return sample
+    return StepNoise(x, seed, inds)
 
 
 def _s_in(x):
@@ -69,7 +70,12 @@ def _cb(callback, i, x, sigma, sigma_hat, denoised):
 def _noise_sampler(x, extra_args, noise_sampler):
     if noise_sampler is not None:
         return noise_sampler
-    return default_noise_sampler(x, extra_args.get("seed"))
+    return default_noise_sampler(x, extra_args.get("seed"), extra_args.get("noise_inds"))
+
+
+def _brownian(x, extra_args, sigma_min, sigma_max, cpu=False):
+    return BrownianTreeNoiseSampler(x, sigma_min, sigma_max, seed=extra_args.get("seed"), cpu=cpu,
+                                    inds=extra_args.get("noise_inds"))
 
 
 @torch.no_grad()
@@ -102,8 +108,14 @@ def sample_euler_ancestral(model, x, sigmas, extra_args=None, callback=None, dis
         denoised = _model(model, x, s[i], extra_args, s_in)
         down, up = get_ancestral_step(s[i], s[i + 1], eta=eta)
         _cb(callback, i, x, s[i], s[i], denoised)
-        noise = ns(s[i], s[i + 1]) * s_noise if s[i + 1] > 0 else None
-        x = ops.euler_step(x, denoised, noise, s[i], down, up if s[i + 1] > 0 else 0.0)
+        if s[i + 1] <= 0:
+            x = ops.euler_step(x, denoised, None, s[i], down, 0.0)
+        elif isinstance(ns, StepNoise) and s_noise == 1.0:
+            # noise generated in the update kernel's registers (stream = this sampler's call count)
+            x = ops.euler_ancestral_philox(x, denoised, s[i], down, up, ns.seed, ns.inds, ns.calls)
+            ns.calls += 1
+        else:
+            x = ops.euler_step(x, denoised, ns(s[i], s[i + 1]) * s_noise, s[i], down, up)
     return x
 
 
@@ -252,7 +264,7 @@ def sample_dpmpp_sde(model, x, sigmas, extra_args=None, callback=None, disable=N
     extra_args = {} if extra_args is None else extra_args
     s = _f(sigmas)
     pos = [v for v in s if v > 0]
-    ns = noise_sampler or BrownianTreeNoiseSampler(x, min(pos), max(s), seed=extra_args.get("seed"), cpu=True)
+    ns = noise_sampler or _brownian(x, extra_args, min(pos), max(s), cpu=True)
     s_in = _s_in(x)
     for i in range(len(s) - 1):
         denoised = _model(model, x, s[i], extra_args, s_in)
@@ -314,7 +326,7 @@ def sample_dpmpp_2m_sde(model, x, sigmas, extra_args=None, callback=None, disabl
     extra_args = {} if extra_args is None else extra_args
     s = _f(sigmas)
     pos = [v for v in s if v > 0]
-    ns = noise_sampler or BrownianTreeNoiseSampler(x, min(pos), max(s), seed=extra_args.get("seed"), cpu=_cpu_tree)
+    ns = noise_sampler or _brownian(x, extra_args, min(pos), max(s), cpu=_cpu_tree)
     s_in = _s_in(x)
     old = None
     h_last = None
@@ -348,7 +360,7 @@ def sample_dpmpp_3m_sde(model, x, sigmas, extra_args=None, callback=None, disabl
     extra_args = {} if extra_args is None else extra_args
     s = _f(sigmas)
     pos = [v for v in s if v > 0]
-    ns = noise_sampler or BrownianTreeNoiseSampler(x, min(pos), max(s), seed=extra_args.get("seed"), cpu=_cpu_tree)
+    ns = noise_sampler or _brownian(x, extra_args, min(pos), max(s), cpu=_cpu_tree)
     s_in = _s_in(x)
     d1 = d2 = None
     h1 = h2 = None
@@ -389,7 +401,7 @@ def sample_dpmpp_sde_gpu(model, x, sigmas, extra_args=None, callback=None, disab
     extra_args = {} if extra_args is None else extra_args
     s = _f(sigmas)
     pos = [v for v in s if v > 0]
-    ns = noise_sampler or BrownianTreeNoiseSampler(x, min(pos), max(s), seed=extra_args.get("seed"), cpu=False)
+    ns = noise_sampler or _brownian(x, extra_args, min(pos), max(s), cpu=False)
     return sample_dpmpp_sde(model, x, sigmas, extra_args, callback, disable, eta, s_noise, ns, r)
 
 
@@ -552,7 +564,7 @@ class DPMSolver:
         return x - self.sigma(t_next) * math.expm1(h) * eps - self.sigma(t_next) / r2 * (math.expm1(h) / h - 1) * (eps_r2 - eps), eps_cache
 
     def dpm_solver_fast(self, x, t_start, t_end, nfe, eta=0.0, s_noise=1.0, noise_sampler=None):
-        noise_sampler = default_noise_sampler(x) if noise_sampler is None else noise_sampler
+        noise_sampler = _noise_sampler(x, self.extra_args, noise_sampler)
         if not t_end > t_start and eta:
             raise ValueError("eta must be 0 for reverse sampling")
         m = math.floor(nfe / 3) + 1
@@ -585,7 +597,7 @@ class DPMSolver:
 
     def dpm_solver_adaptive(self, x, t_start, t_end, order=3, rtol=0.05, atol=0.0078, h_init=0.05, pcoeff=0.0,
                             icoeff=1.0, dcoeff=0.0, accept_safety=0.81, eta=0.0, s_noise=1.0, noise_sampler=None):
-        noise_sampler = default_noise_sampler(x) if noise_sampler is None else noise_sampler
+        noise_sampler = _noise_sampler(x, self.extra_args, noise_sampler)
         if order not in {2, 3}:
             raise ValueError("order should be 2 or 3")
         forward = t_end > t_start

@@ -29,18 +29,20 @@ def prepare_noise(latent_image, seed, noise_inds=None):
 
 def sample(model, noise, steps, cfg, sampler_name, scheduler, positive, negative, latent_image, denoise=1.0,
            disable_noise=False, start_step=None, last_step=None, force_full_denoise=False, noise_mask=None,
-           sigmas=None, callback=None, disable_pbar=False, seed=None):
+           sigmas=None, callback=None, disable_pbar=False, seed=None, noise_inds=None):
+    """``noise_inds``: the global batch index of every latent (default 0..B-1) — keys the per-step
+    ancestral/SDE noise so it does not depend on how a batch is split (``sampling/rng.py``)."""
     ks = samplers.KSampler(model, steps=steps, device=model.load_device, sampler=sampler_name, scheduler=scheduler,
                            denoise=denoise, model_options=model.model_options)
     out = ks.sample(noise, positive, negative, cfg=cfg, latent_image=latent_image, start_step=start_step,
                     last_step=last_step, force_full_denoise=force_full_denoise, denoise_mask=noise_mask, sigmas=sigmas,
-                    callback=callback, disable_pbar=disable_pbar, seed=seed)
+                    callback=callback, disable_pbar=disable_pbar, seed=seed, noise_inds=noise_inds)
     return out.to(dm.intermediate_device())
 
 
 def sample_custom(model, noise, cfg, sampler, sigmas, positive, negative, latent_image, noise_mask=None,
-                  callback=None, disable_pbar=False, seed=None):
+                  callback=None, disable_pbar=False, seed=None, noise_inds=None):
     out = samplers.sample(model, noise, positive, negative, cfg, model.load_device, sampler, sigmas,
                           model_options=model.model_options, latent_image=latent_image, denoise_mask=noise_mask,
-                          callback=callback, disable_pbar=disable_pbar, seed=seed)
+                          callback=callback, disable_pbar=disable_pbar, seed=seed, noise_inds=noise_inds)
     return out.to(dm.intermediate_device())

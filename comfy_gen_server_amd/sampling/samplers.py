@@ -256,7 +256,7 @@ class KSamplerX0Inpaint:
         self.noise = None
         self.latent_image = None
 
-    def __call__(self, x, sigma, denoise_mask=None, model_options=None, seed=None):
+    def __call__(self, x, sigma, denoise_mask=None, model_options=None, seed=None, noise_inds=None):
         model_options = model_options or {}
         if denoise_mask is not None:
             if "denoise_mask_function" in model_options:
@@ -530,6 +530,8 @@ class CFGGuider:
             latent_image = self.inner_model.process_latent_in(latent_image)
         self.conds = process_conds(self.inner_model, noise, self.conds, device, latent_image, denoise_mask, seed)
         extra_args = {"model_options": self.model_options, "seed": seed}
+        if getattr(self, "noise_inds", None) is not None:
+            extra_args["noise_inds"] = list(self.noise_inds)
         samples = sampler.sample(self, sigmas, extra_args, callback, noise, latent_image, denoise_mask, disable_pbar)
         return self.inner_model.process_latent_out(samples.to(torch.float32))
 
@@ -555,10 +557,11 @@ class CFGGuider:
 
 
 def sample(model, noise, positive, negative, cfg, device, sampler, sigmas, model_options=None, latent_image=None,
-           denoise_mask=None, callback=None, disable_pbar=False, seed=None):
+           denoise_mask=None, callback=None, disable_pbar=False, seed=None, noise_inds=None):
     g = CFGGuider(model)
     g.set_conds(positive, negative)
     g.set_cfg(cfg)
+    g.noise_inds = noise_inds
     return g.sample(noise, latent_image, sampler, sigmas, denoise_mask, callback, disable_pbar, seed)
 
 
@@ -596,7 +599,8 @@ class KSampler:
             self.sigmas = self.calculate_sigmas(new_steps).to(self.device)[-(steps + 1):]
 
     def sample(self, noise, positive, negative, cfg, latent_image=None, start_step=None, last_step=None,
-               force_full_denoise=False, denoise_mask=None, sigmas=None, callback=None, disable_pbar=False, seed=None):
+               force_full_denoise=False, denoise_mask=None, sigmas=None, callback=None, disable_pbar=False, seed=None,
+               noise_inds=None):
         if sigmas is None:
             sigmas = self.sigmas
         if last_step is not None and last_step < len(sigmas) - 1:
@@ -610,4 +614,4 @@ class KSampler:
                 return latent_image if latent_image is not None else torch.zeros_like(noise)
         return sample(self.model, noise, positive, negative, cfg, self.device, sampler_object(self.sampler), sigmas,
                       self.model_options, latent_image=latent_image, denoise_mask=denoise_mask, callback=callback,
-                      disable_pbar=disable_pbar, seed=seed)
+                      disable_pbar=disable_pbar, seed=seed, noise_inds=noise_inds)

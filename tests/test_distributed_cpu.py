@@ -181,3 +181,92 @@ def test_dp_rank_failure_recovery(tmp_path):
     assert rec.shape == full.shape == (5, 64, 64, 3)
     d = (rec.int() - full.int()).abs()       # batch-size-dependent fp32 reduction order only
     assert d.max() <= 2 and d.float().mean() < 0.25, (d.max(), d.float().mean())
+
+
+def test_bench_spawns_ranks_without_launcher():
+    """``bench.py --gpus 2`` with no torchrun: the parent (which never imports torch) starts the two
+    rank processes itself; the JSON line reports the communicator's world size and backend."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0", "--cpu",
+           "--family", "tiny", "--res", "64", "--sampler-steps", "2", "--batch-per-gpu", "1"]
+    env = _env()
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["ranks"] == 2 and res["backend"] == "gloo"
+    assert res["config"]["global_batch"] == 2 and "op_backends" in res
+
+
+def test_bench_rejects_world_mismatch():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu", "--family", "tiny"]
+    env = dict(_env(), WORLD_SIZE="1", RANK="0")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_step_noise_is_keyed_by_global_index():
+    """Ancestral/SDE noise of image i depends on (seed, i, step) only: any rank split reproduces the
+    one-rank draw, and rank r's local image j does NOT reuse rank 0's image-j noise (the round-1 bug:
+    a per-rank generator seeded with the job seed)."""
+    from comfy_gen_server_amd import ops
+    shape = (6, 4, 8, 8)
+    for stream in (0, 5):
+        full = ops.philox_randn(shape, 77, list(range(6)), stream)
+        parts = [ops.philox_randn((2,) + shape[1:], 77, [2 * r, 2 * r + 1], stream) for r in range(3)]
+        assert torch.equal(torch.cat(parts), full)
+        assert (parts[1][0] - parts[0][0]).abs().mean() > 0.5
+    assert (ops.philox_randn(shape, 77, range(6), 0) - ops.philox_randn(shape, 77, range(6), 1)).abs().mean() > 0.5
+    # Brownian increments split the same way
+    bt = [ops.brownian_increment((2, 4, 4, 4), 3, [2 * r, 2 * r + 1], 0.0, 4.0, 1.0, 1.5, 1e-3, 24, 1.0)
+          for r in range(2)]
+    bf = ops.brownian_increment((4, 4, 4, 4), 3, [0, 1, 2, 3], 0.0, 4.0, 1.0, 1.5, 1e-3, 24, 1.0)
+    assert torch.equal(torch.cat(bt), bf)
+
+
+_EQ_WORKER = r'''
+import os, sys, torch
+sys.path.insert(0, os.environ["PYTHONPATH"])
+from comfy_gen_server_amd.parallel.comm import init_from_env
+from comfy_gen_server_amd.runtime import device as dm
+dm.set_cpu_mode(True)
+torch.set_num_threads(1)
+c = init_from_env(backend="gloo")
+from comfy_gen_server_amd.tools.synth import build_pipeline
+from comfy_gen_server_amd.parallel.dp import DataParallelGenerator, Job, generate_local
+with torch.inference_mode():
+    patcher, clip, vae = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=5)
+gen = DataParallelGenerator(patcher, clip, vae)
+gen.sync_weights()
+job = Job(batch=6, steps=int(os.environ["EQ_STEPS"]), width=64, height=64, seed=11,
+          sampler=os.environ["EQ_SAMPLER"])
+off, n = gen._shard(job, c.rank)
+with torch.inference_mode():
+    lat = generate_local(patcher, clip, vae, job, off, n, decode=False).contiguous()
+allv = c.all_gather(lat)
+if c.rank == 0:
+    torch.save(allv, os.path.join(os.environ["CGS_TEST_OUT"], f"lat_ws{c.world}.pt"))
+c.shutdown()
+'''
+
+
+@pytest.mark.parametrize("sampler", ["euler_ancestral", "dpmpp_2m_sde"])
+def test_dp_ws3_equals_ws1(tmp_path, sampler):
+    """A 3-rank data-parallel run of a 6-image batch with a stochastic sampler (8 steps) gives the
+    same latents as the 1-rank run of the whole batch (reference semantics: independent per-image
+    noise, comfy/k_diffusion/sampling.py:60-61, made split-invariant by keying on the global index)."""
+    script = tmp_path / "eq_worker.py"
+    script.write_text(_EQ_WORKER)
+    env = dict(_env(), CGS_TEST_OUT=str(tmp_path), EQ_STEPS="8", EQ_SAMPLER=sampler, OMP_NUM_THREADS="1")
+    for ws in (1, 3):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ws}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script)]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+    a = torch.load(tmp_path / "lat_ws1.pt", weights_only=True)
+    b = torch.load(tmp_path / "lat_ws3.pt", weights_only=True)
+    assert a.shape == b.shape == (6, 4, 8, 8)
+    assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), (a - b).abs().max()
+    # distinct images really got distinct noise (no rank-correlated images)
+    assert (b[2] - b[0]).abs().mean() > 0.05 and (b[4] - b[0]).abs().mean() > 0.05
