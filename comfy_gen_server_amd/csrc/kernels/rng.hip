@@ -165,6 +165,64 @@ __global__ void brownian_increment_kernel(float* __restrict__ out, int B, long l
   }
 }
 
+
+// ------------------------------------------------------------------ device-parameterised sampler step (K16)
+// One kernel = CFG combine + Euler / Euler-ancestral update + in-register noise, with every per-step
+// scalar read from device memory, so one captured hipGraph serves every step of every job:
+//   params[step * stride + 0..3] = sigma, sigma_down, sigma_up, s_noise   (host-built table per job)
+//   meta[0] = step, meta[1] = seed, meta[2] = global index of image 0     (meta[0] advanced in-graph)
+//   den = u + (c - u) * cfg  (u == nullptr: den = c) ; x += (x - den)/sigma * (sigma_down - sigma)
+//   if sigma_up > 0: x += N(seed, image, stream = step) * sigma_up * s_noise ; den_out = den (optional)
+__global__ void sampler_step_dev_kernel(float* __restrict__ x, const float* __restrict__ c, const float* __restrict__ u,
+                                        float* __restrict__ den_out, int B, long long n, float cfg,
+                                        const float* __restrict__ params, int stride,
+                                        const long long* __restrict__ meta) {
+  const long long step = meta[0];
+  const uint64_t seed = (uint64_t)meta[1];
+  const long long index0 = meta[2];
+  const float* pr = params + step * stride;
+  const float sigma = pr[0], sdown = pr[1], sup = pr[2] * pr[3];
+  const float inv_sigma = 1.0f / sigma, dt = sdown - sigma;
+  const long long groups = n >> 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)B * groups;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / groups);
+    const long long g = i - (long long)b * groups;
+    float4 xv = reinterpret_cast<float4*>(x)[i];
+    float4 dv = reinterpret_cast<const float4*>(c)[i];
+    if (u) {
+      const float4 uv = reinterpret_cast<const float4*>(u)[i];
+      dv.x = uv.x + (dv.x - uv.x) * cfg;
+      dv.y = uv.y + (dv.y - uv.y) * cfg;
+      dv.z = uv.z + (dv.z - uv.z) * cfg;
+      dv.w = uv.w + (dv.w - uv.w) * cfg;
+    }
+    if (den_out) reinterpret_cast<float4*>(den_out)[i] = dv;
+    xv.x = fmaf((xv.x - dv.x) * inv_sigma, dt, xv.x);
+    xv.y = fmaf((xv.y - dv.y) * inv_sigma, dt, xv.y);
+    xv.z = fmaf((xv.z - dv.z) * inv_sigma, dt, xv.z);
+    xv.w = fmaf((xv.w - dv.w) * inv_sigma, dt, xv.w);
+    if (sup > 0.0f) {
+      const float4 z = normal4(image_key(seed, (uint64_t)(index0 + b)), (uint64_t)g, (uint64_t)step);
+      xv.x = fmaf(z.x, sup, xv.x);
+      xv.y = fmaf(z.y, sup, xv.y);
+      xv.z = fmaf(z.z, sup, xv.z);
+      xv.w = fmaf(z.w, sup, xv.w);
+    }
+    reinterpret_cast<float4*>(x)[i] = xv;
+  }
+}
+
+// out[0..B) = params[step * stride + col] (the per-image sigma vector the model is called with)
+__global__ void step_param_kernel(float* __restrict__ out, int B, const float* __restrict__ params, int stride, int col,
+                                  const long long* __restrict__ meta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) out[i] = params[meta[0] * stride + col];
+}
+
+__global__ void step_advance_kernel(long long* meta) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) meta[0] += 1;
+}
 }  // namespace
 
 CGS_EXPORT int cgs_philox_randn(void* out, int B, long long n, unsigned long long seed, long long index0,
@@ -198,5 +256,27 @@ CGS_EXPORT int cgs_brownian_increment(void* out, int B, long long n, unsigned lo
   if (n % 4) return (int)hipErrorInvalidValue;
   brownian_increment_kernel<<<rng_blocks((long long)B * (n / 4)), 256, 0, s>>>(
       (float*)out, B, n, seed, index0, t0, t1, ta, tb, tol, max_depth, scale);
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_sampler_step_dev(void* x, const void* cond_den, const void* uncond_den, void* den_out, int B,
+                                    long long n, float cfg, const void* params, int stride, const void* meta,
+                                    hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  sampler_step_dev_kernel<<<rng_blocks((long long)B * (n / 4)), 256, 0, s>>>(
+      (float*)x, (const float*)cond_den, (const float*)uncond_den, (float*)den_out, B, n, cfg, (const float*)params,
+      stride, (const long long*)meta);
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_step_param(void* out, int B, const void* params, int stride, int col, const void* meta,
+                              hipStream_t s) {
+  step_param_kernel<<<(B + 63) / 64, 64, 0, s>>>((float*)out, B, (const float*)params, stride, col,
+                                                 (const long long*)meta);
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_step_advance(void* meta, hipStream_t s) {
+  step_advance_kernel<<<1, 64, 0, s>>>((long long*)meta);
   return (int)hipGetLastError();
 }

@@ -10,9 +10,16 @@ Parity: the reference picks one attention backend globally at import time
 (``comfy/model_management.py:132-202``, ``attention.py:352-368``); here the choice is per shape and
 measured, like MIOpen's find mode.
 
+A measured table for MI355X ships with the package (``data/tune_mi355x.json``) and is loaded by
+default, so a fresh box runs the recorded choices instead of re-tuning inside the first job (and
+two boxes cannot drift apart through different timing-noise picks). Keys missing from it are
+still tuned on first use.
+
 Env:
   CGS_AUTOTUNE=0          disable (always the first/default candidate: the HIP kernel)
-  CGS_TUNE_FILE=path      persist choices as JSON (loaded at first use, rewritten on new entries)
+  CGS_TUNE_FILE=path      persist choices as JSON (loaded after the packaged table, rewritten on new
+                          entries; the packaged table itself is never written)
+  CGS_TUNE_DEFAULT=0      do not load the packaged table
   CGS_TUNE_REPS=n         timed repetitions per candidate (default 3)
 """
 from __future__ import annotations
@@ -23,6 +30,8 @@ import threading
 
 import torch
 
+DEFAULT_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data",
+                             "tune_mi355x.json")
 _cache: dict[str, str] = {}
 _lock = threading.Lock()
 _loaded = False
@@ -42,13 +51,19 @@ def _load():
     if _loaded:
         return
     _loaded = True
-    path = os.environ.get("CGS_TUNE_FILE")
-    if path and os.path.exists(path):
+    paths = []
+    if os.environ.get("CGS_TUNE_DEFAULT", "1") != "0":
+        paths.append(DEFAULT_TABLE)
+    if os.environ.get("CGS_TUNE_FILE"):
+        paths.append(os.environ["CGS_TUNE_FILE"])
+    for path in paths:
+        if not os.path.exists(path):
+            continue
         try:
             with open(path) as f:
                 data = json.load(f)
             if isinstance(data, dict):
-                _cache.update({str(k): str(v) for k, v in data.items()})
+                _cache.update({str(k): str(v) for k, v in data.items() if not str(k).startswith("_")})
         except (OSError, ValueError):
             pass
 

@@ -772,3 +772,29 @@ def attention_with_probs(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, head
     p = softmax_rows(torch.bmm(qh, kh.transpose(1, 2)), d ** -0.5)
     o = torch.bmm(p, vh).reshape(b, heads, sq, d).permute(0, 2, 1, 3).reshape(b, sq, hd)
     return o.to(q.dtype), p
+
+
+# ----------------------------------------------------------------------------------------------
+# Device-parameterised sampler step (rng.hip): the per-step scalars live in a device table and a
+# device step counter, so one captured graph is replayed for every step (sampling/step_graph.py)
+# ----------------------------------------------------------------------------------------------
+def step_param(out: torch.Tensor, params: torch.Tensor, meta: torch.Tensor, col: int = 0):
+    """out[:] = params[meta[0], col] (fp32 device vector)."""
+    _check(_lib().cgs_step_param(out.data_ptr(), out.numel(), params.data_ptr(), params.shape[1], col,
+                                 meta.data_ptr(), _stream()), "cgs_step_param")
+    return out
+
+
+def sampler_step_dev(x: torch.Tensor, cond_den: torch.Tensor, uncond_den: torch.Tensor | None,
+                     den_out: torch.Tensor | None, cfg: float, params: torch.Tensor, meta: torch.Tensor):
+    """In place on ``x``: CFG combine + Euler(-ancestral) update + in-register noise, scalars from
+    ``params[meta[0]] = (sigma, sigma_down, sigma_up, s_noise)``, seed/index0 from ``meta[1:3]``."""
+    count("euler", "hip")
+    _check(_lib().cgs_sampler_step_dev(x.data_ptr(), cond_den.data_ptr(), _ptr(uncond_den), _ptr(den_out),
+                                       int(x.shape[0]), _numel1(x.shape), float(cfg), params.data_ptr(),
+                                       params.shape[1], meta.data_ptr(), _stream()), "cgs_sampler_step_dev")
+    return x
+
+
+def step_advance(meta: torch.Tensor):
+    _check(_lib().cgs_step_advance(meta.data_ptr(), _stream()), "cgs_step_advance")

@@ -25,6 +25,7 @@ import torch
 from .. import ops
 from .brownian import BrownianTreeNoiseSampler
 from .rng import StepNoise
+from . import step_graph
 
 
 def _f(sigmas):
@@ -82,6 +83,10 @@ def _brownian(x, extra_args, sigma_min, sigma_max, cpu=False):
 def sample_euler(model, x, sigmas, extra_args=None, callback=None, disable=None, s_churn=0.0, s_tmin=0.0,
                  s_tmax=float("inf"), s_noise=1.0):
     extra_args = {} if extra_args is None else extra_args
+    if s_churn == 0:
+        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "euler")
+        if r is not None:
+            return r
     s = _f(sigmas)
     s_in = _s_in(x)
     n = len(s) - 1
@@ -101,6 +106,10 @@ def sample_euler(model, x, sigmas, extra_args=None, callback=None, disable=None,
 def sample_euler_ancestral(model, x, sigmas, extra_args=None, callback=None, disable=None, eta=1.0, s_noise=1.0,
                            noise_sampler=None):
     extra_args = {} if extra_args is None else extra_args
+    if noise_sampler is None:
+        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "euler_ancestral", eta, s_noise)
+        if r is not None:
+            return r
     ns = _noise_sampler(x, extra_args, noise_sampler)
     s = _f(sigmas)
     s_in = _s_in(x)
@@ -175,6 +184,10 @@ def sample_dpm_2(model, x, sigmas, extra_args=None, callback=None, disable=None,
 def sample_dpm_2_ancestral(model, x, sigmas, extra_args=None, callback=None, disable=None, eta=1.0, s_noise=1.0,
                            noise_sampler=None):
     extra_args = {} if extra_args is None else extra_args
+    if noise_sampler is None:
+        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "euler_ancestral", eta, s_noise)
+        if r is not None:
+            return r
     ns = _noise_sampler(x, extra_args, noise_sampler)
     s = _f(sigmas)
     s_in = _s_in(x)
@@ -235,6 +248,10 @@ def sample_lms(model, x, sigmas, extra_args=None, callback=None, disable=None, o
 def sample_dpmpp_2s_ancestral(model, x, sigmas, extra_args=None, callback=None, disable=None, eta=1.0, s_noise=1.0,
                               noise_sampler=None):
     extra_args = {} if extra_args is None else extra_args
+    if noise_sampler is None:
+        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "euler_ancestral", eta, s_noise)
+        if r is not None:
+            return r
     ns = _noise_sampler(x, extra_args, noise_sampler)
     s = _f(sigmas)
     s_in = _s_in(x)

@@ -1,0 +1,191 @@
+"""One hipGraph per sampler step: UNet(cond ‖ uncond) + CFG combine + Euler(-a) update + noise.
+
+The reference runs the k-diffusion loop in Python, one op at a time
+(``comfy/k_diffusion/sampling.py:148-164`` -> ``comfy/samplers.py:234-255`` -> ``model_base.py:74-98``).
+Here the whole step body is captured ONCE per plan into a ``torch.cuda.CUDAGraph`` and replayed
+for every step of every job with that plan:
+
+  * every per-step scalar lives on the device: a host-built table ``params[step] = (sigma,
+    sigma_down, sigma_up, s_noise)`` and ``meta = (step, seed, index0)``; the graph's first kernel
+    broadcasts ``sigma`` into the model's sigma vector, its last kernel advances ``meta[0]``;
+  * the model sees sigma as a device tensor (c_in scaling, sigma -> timestep, calculate_denoised
+    are device ops), so nothing in the forward depends on host values;
+  * CFG combine, the Euler / Euler-ancestral update and the ancestral noise (counter-based, keyed
+    by (seed, global image index, step) — ``rng.py``) are ONE kernel (``cgs_sampler_step_dev``).
+
+A job then costs: copy x and the conditioning into the plan's static buffers, one 16-B-per-step
+parameter upload, and ``steps`` graph launches — no per-step Python op dispatch, no host gaps.
+
+Eligible (else the eager loop runs): device tensors, Euler / Euler-a (no churn), a seed and
+contiguous global image indices, a plain ``CFGGuider`` with one full-frame cond and uncond entry
+(no areas / masks / gligen / timestep ranges / ControlNet), no denoise mask, no sampler cfg hooks or
+model wrappers, no transformer patches. ``CGS_GRAPHS=0`` disables it.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+
+import torch
+
+from .. import ops
+from ..runtime import graphs
+from . import rng
+
+_lock = threading.Lock()
+CAPACITY = 1024          # steps per parameter table
+stats = {"capture": 0, "replay": 0, "jobs": 0}
+
+
+class _Plan:
+    __slots__ = ("graph", "x", "params", "meta", "sig", "den", "cond", "pool")
+
+
+def _ancestral(s0, s1, eta):
+    from .k_samplers import get_ancestral_step
+    return get_ancestral_step(s0, s1, eta=eta)
+
+
+def _eligible(mk, x, extra_args):
+    from .samplers import CFGGuider, KSamplerX0Inpaint, _simple_conds
+    if not graphs.enabled() or not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous():
+        return None
+    if x[0].numel() % 4 or not isinstance(mk, KSamplerX0Inpaint) or extra_args.get("denoise_mask") is not None:
+        return None
+    if extra_args.get("seed") is None:
+        return None
+    inds = extra_args.get("noise_inds") or list(range(x.shape[0]))
+    index0, contiguous = rng.contiguous_inds(inds)
+    if not contiguous or len(inds) != x.shape[0]:
+        return None
+    guider = mk.inner_model
+    if type(guider) is not CFGGuider:
+        return None
+    mo = extra_args.get("model_options") or {}
+    if any(k in mo for k in ("sampler_cfg_function", "sampler_post_cfg_function", "model_function_wrapper",
+                             "denoise_mask_function")):
+        return None
+    to = mo.get("transformer_options", {})
+    if to.get("patches") or to.get("patches_replace"):
+        return None
+    pos, neg = guider.conds.get("positive"), guider.conds.get("negative")
+    use_uncond = not (abs(guider.cfg - 1.0) < 1e-9 and not mo.get("disable_cfg1_optimization", False))
+    lists = [pos, neg] if use_uncond else [pos]
+    if any(cl is None or len(cl) != 1 for cl in lists) or not _simple_conds(lists):
+        return None
+    if any(cl[0].get("control") is not None or cl[0].get("gligen") is not None for cl in lists):
+        return None
+    return guider, lists, use_uncond, index0, mo
+
+
+def _conditioning(guider, lists, x, sigma0):
+    from .samplers import can_concat_cond, cond_cat, get_area_and_mult
+    sig = torch.full((x.shape[0],), sigma0, device=x.device, dtype=torch.float32)
+    runs = [get_area_and_mult(cl[0], x, sig, need_mult=False) for cl in lists]
+    if len(runs) == 2 and not can_concat_cond(runs[0], runs[1]):
+        return None
+    return cond_cat([r.conditioning for r in runs])
+
+
+def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0, s_noise: float = 1.0):
+    """Run the whole sampling loop from graph replays; None when not eligible (caller runs eager)."""
+    el = _eligible(mk, x, extra_args)
+    if el is None:
+        return None
+    guider, lists, use_uncond, index0, mo = el
+    s = [float(v) for v in sigmas.detach().cpu()]
+    n = len(s) - 1
+    if n < 1 or n > CAPACITY:
+        return None
+    cond = _conditioning(guider, lists, x, s[0])
+    if cond is None or any(not isinstance(v, torch.Tensor) or not v.is_cuda for v in cond.values()):
+        return None
+    model = guider.inner_model
+    from ..models import layers
+    key = (layers.WEIGHTS_EPOCH, tuple(x.shape), use_uncond, float(guider.cfg),
+           tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in cond.items())))
+    plans = model.__dict__.setdefault("_step_graph_plans", {})
+    plan = plans.get(key)
+    if plan is None:
+        plan = _capture(model, x, cond, use_uncond, float(guider.cfg), mo)
+        if plan is None:
+            return None
+        with _lock:
+            for k in [k for k in plans if k[0] != layers.WEIGHTS_EPOCH]:
+                del plans[k]
+            plans[key] = plan
+    # per-job inputs
+    rows = []
+    for i in range(n):
+        if kind == "euler_ancestral":
+            down, up = _ancestral(s[i], s[i + 1], eta)
+            if s[i + 1] <= 0:
+                up = 0.0
+        else:
+            down, up = s[i + 1], 0.0
+        rows.append((s[i], down, up, s_noise))
+    plan.params[:n].copy_(torch.tensor(rows, dtype=torch.float32))
+    plan.meta.copy_(torch.tensor([0, int(extra_args["seed"]) & 0x7FFFFFFFFFFFFFFF, index0], dtype=torch.int64))
+    plan.x.copy_(x)
+    for k, v in cond.items():
+        plan.cond[k].copy_(v)
+    stats["jobs"] += 1
+    for i in range(n):
+        plan.graph.replay()
+        stats["replay"] += 1
+        if callback is not None:
+            callback({"x": plan.x.clone(), "i": i, "sigma": s[i], "sigma_hat": s[i], "denoised": plan.den.clone()})
+    return plan.x.clone()
+
+
+def _capture(model, x, cond, use_uncond, cfg, mo):
+    p = _Plan()
+    dev = x.device
+    p.x = x.detach().clone()
+    p.params = torch.zeros((CAPACITY, 4), device=dev, dtype=torch.float32)
+    p.params[:, 0] = 1.0
+    p.meta = torch.zeros(3, device=dev, dtype=torch.int64)
+    p.sig = torch.empty(x.shape[0], device=dev, dtype=torch.float32)
+    p.den = torch.empty_like(p.x)
+    p.cond = {k: v.detach().clone() for k, v in cond.items()}
+    to = dict(mo.get("transformer_options", {}))
+    to["cond_or_uncond"] = [0, 1] if use_uncond else [0]
+
+    def body():
+        ops.step_param(p.sig, p.params, p.meta, 0)
+        if use_uncond:
+            xin, tin = torch.cat([p.x, p.x]), torch.cat([p.sig, p.sig])
+        else:
+            xin, tin = p.x, p.sig
+        t = dict(to)
+        t["sigmas"] = p.sig
+        out = model.apply_model(xin, tin, transformer_options=t, **p.cond)
+        if use_uncond:
+            oc, ou = out.chunk(2)
+            ops.sampler_step_dev(p.x, oc.contiguous(), ou.contiguous(), p.den, cfg, p.params, p.meta)
+        else:
+            ops.sampler_step_dev(p.x, out.contiguous(), None, p.den, 1.0, p.params, p.meta)
+        ops.step_advance(p.meta)
+
+    g = torch.cuda.CUDAGraph()
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            body()                      # warm-up: autotune keys, derived weight layouts, lazy attrs
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        p.pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=p.pool, stream=side):
+            body()
+        torch.cuda.synchronize()
+    except Exception as e:  # capture-unsafe op in the step: this plan stays eager
+        logging.warning("step hipGraph capture failed (%s); sampling stays eager", e)
+        try:
+            torch.cuda.synchronize()
+        except Exception:
+            pass
+        return None
+    p.graph = g
+    stats["capture"] += 1
+    return p

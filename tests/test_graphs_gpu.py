@@ -70,3 +70,29 @@ def test_graphs_cpu_is_eager():
         b = runner(x, t, context=ctx, y=y, transformer_options={})
     assert runner.stats == {"eager": 2, "capture": 0, "replay": 0}
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampler", ["euler_ancestral", "euler"])
+def test_step_graph_matches_eager_loop(cuda, monkeypatch, sampler):
+    """One captured graph per sampler step (UNet(cond||uncond) + CFG + Euler(-a) + in-register noise,
+    every scalar from a device table) reproduces the eager Python loop, for two jobs through the
+    same plan (second job = pure replay with a new seed, prompt latents and global image offset)."""
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    from comfy_gen_server_amd.parallel.dp import Job, generate_local
+    from comfy_gen_server_amd.sampling import step_graph
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_GRAPHS", mode)
+            outs = []
+            for seed, off in ((5, 0), (9, 3)):
+                job = Job(batch=3, steps=6, cfg=6.0, sampler=sampler, width=64, height=64, seed=seed)
+                outs.append(generate_local(patcher, clip, vae, job, off, 3, decode=False).float())
+            res[mode] = outs
+        torch.cuda.synchronize()
+    assert step_graph.stats["capture"] >= 1 and step_graph.stats["replay"] >= 12
+    for a, b in zip(res["0"], res["1"]):
+        err = (a - b).abs().max().item()
+        assert err < 2e-2 * (a.abs().max().item() + 1), err
