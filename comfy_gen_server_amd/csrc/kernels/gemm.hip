@@ -14,6 +14,7 @@
 #include "mfma_core.h"
 #include "mfma_pp.h"
 #include "mfma_pp160.h"
+#include "mfma_ppk.h"
 
 #define G_BM 128
 #define G_BN 128
@@ -504,6 +505,59 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   return (int)hipGetLastError();
 }
 
+// Dense A loader with 32-bit byte offsets from one uniform base (global_load_lds saddr + voffset form:
+// one VGPR per slot instead of a 64-bit pointer pair -- the v7 kernel runs at the 256-VGPR cap).
+struct DenseA32 {
+  const unsigned char* A;
+  long long lda;
+  int M;
+  uint32_t off[4];
+  __device__ __forceinline__ void setup(int slot, int row) {
+    row = row < M ? row : M - 1;
+    off[slot] = (uint32_t)(((long long)row * lda + 8 * pp::src_chunk8(slot & 1)) * 2);
+  }
+  __device__ __forceinline__ const void* src(int slot, int k0) const { return A + (off[slot] + (uint32_t)(k0 * 2)); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// v7: persistent 256 x 256 x 64 ping-pong with cross-tile prefetch and a register epilogue (mfma_ppk.h)
+template <bool GG>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v7_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  DenseA32 al{reinterpret_cast<const unsigned char*>(A), lda, M, {}};
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
+  ppk::run<GG>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+}
+
+static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ppk::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + ppk::BN - 1) / ppk::BN;
+  const int tiles_m = (M + ppk::BM - 1) / ppk::BM;
+  const long long T = (long long)tiles_m * tiles_n;
+  const int grid = (int)(T < num_cus() ? T : num_cus());
+  if (epi & EPI_GEGLU)
+    gemm_bf16_nt_v7_kernel<true><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
+        alpha, tiles_m, tiles_n, g_tile_group);
+  else
+    gemm_bf16_nt_v7_kernel<false><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
+        alpha, tiles_m, tiles_n, g_tile_group);
+  return (int)hipGetLastError();
+}
+
 static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 waves), 4 = v3 (8 waves), 5 = v5 ping-pong
 
 CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -524,6 +578,9 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
                ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && !(epi & EPI_GEGLU) && ((uintptr_t)bias % 8 == 0))
     return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&
+      ((uintptr_t)bias % 8 == 0) && (long long)M * lda * 2 < (1ll << 32) && (long long)N * ldw * 2 < (1ll << 32))
+    return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && variant == 5)
     return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && (variant >= 3 || variant == -1)) {

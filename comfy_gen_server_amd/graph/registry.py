@@ -95,6 +95,8 @@ def execute_prestartup_scripts(custom_node_dirs=None):
 
 def load_custom_nodes(dirs=None):
     from ..utils import folder_paths
+    from .. import compat
+    compat.install()          # `import comfy.utils`, `folder_paths`, `nodes`, `server`, ... resolve to this engine
     base_names = set(NODE_CLASS_MAPPINGS.keys())
     dirs = dirs if dirs is not None else folder_paths.get_folder_paths("custom_nodes")
     times = []

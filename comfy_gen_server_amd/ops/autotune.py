@@ -93,16 +93,18 @@ def choose(key_parts, candidates, default: str | None = None) -> str:
 
     ``candidates``: list of (name, fn) where fn() runs the op once on the current stream.
     """
+    names = [n for n, _ in candidates]
+    if default is None:
+        default = names[0]
+    if not enabled():               # explicit opt-out: the default kernel, table entries included
+        return default
     key = _key(key_parts)
     with _lock:
         _load()
         hit = _cache.get(key)
-    names = [n for n, _ in candidates]
     if hit is not None and hit in names:
         return hit
-    if default is None:
-        default = names[0]
-    if not enabled() or len(candidates) == 1 or _capturing():
+    if len(candidates) == 1 or _capturing():
         return default
     reps = max(1, int(os.environ.get("CGS_TUNE_REPS", "3")))
     stream = torch.cuda.current_stream()

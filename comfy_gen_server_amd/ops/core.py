@@ -93,6 +93,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         if M * N * K >= (1 << 27):
             cands = []
             if K % 64 == 0 and N % 8 == 0:
+                if K >= 128:
+                    cands.append(("v7", lambda: run_hip(7)))
                 cands.append(("v5", lambda: run_hip(5)))
                 cands.append(("v6", lambda: run_hip(6)))
             if K % 32 == 0 and N % 8 == 0:
@@ -104,7 +106,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v6": 6, "v5": 5, "v4": 4}.get(choice, -2)
+        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N)
     count("gemm", "torch" if be == "torch" else "lib")
     if be == "torch":
@@ -171,11 +173,13 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
         if M * N2 * K >= (1 << 27) and K % 32 == 0:
             cands = []
             if K % 64 == 0:
+                if K >= 128:
+                    cands.append(("v7", lambda: run_hip(7)))
                 cands.append(("v5", lambda: run_hip(5)))
             cands.append(("v4", lambda: run_hip(4)))
             cands.append(("hip", lambda: run_hip(-1)))
             choice = autotune.choose(("gemm_geglu", M, N2, K, epi), cands, default="hip")
-        variant = {"v5": 5, "v4": 4}.get(choice, -2)
+        variant = {"v7": 7, "v5": 5, "v4": 4}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N2 // 2)
     count("gemm_geglu", be)
     # reference path expects the *interleaved* weight too, undo it

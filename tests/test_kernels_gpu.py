@@ -170,7 +170,7 @@ def test_attention_d64_variants(cuda, attn_variant, B, H, Sq, Sk, spike):
     assert _rel(o, ref) < 2e-2
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160", "v7ppk"])
 def gemm_variant(request):
     lib = _native.load_kernels()
     lib.cgs_gemm_set_variant(request.param)
@@ -370,3 +370,49 @@ def test_fp8_e4m3_decode_rule_is_exact():
     mag = torch.where(e > 0, ((e + 120) << 7) | (m << 4), (m.float() * 0.001953125).view(torch.int32) >> 16)
     nan = (idx & 0x7F) == 0x7F
     assert torch.equal((s | mag)[~nan], ref[~nan])
+
+
+# The SDXL bench shapes (UNet batch 16 at 1024^2): 64x64 tokens x 640 ch and 32x32 x 1280 ch.
+@pytest.mark.parametrize("M,N,K,epi", [(65536, 1920, 640, "none"), (65536, 640, 640, "bias_res"),
+                                       (16384, 3840, 1280, "none"), (16384, 1280, 1280, "bias_res"),
+                                       (16384, 1280, 5120, "bias_res"), (1232, 2560, 2048, "none")])
+@pytest.mark.parametrize("variant", [5, 6, 7])
+def test_gemm_bench_shapes(cuda, M, N, K, epi, variant):
+    lib = _native.load_kernels()
+    lib.cgs_gemm_set_variant(variant)
+    try:
+        torch.manual_seed(0)
+        a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+        b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
+        r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
+        y = ops.linear(a, w, b, residual=r)
+        ref = a.float() @ w.float().t()
+        if b is not None:
+            ref += b.float()
+        if r is not None:
+            ref += r.float()
+        assert ops.stats().get(("gemm", "hip"), 0) == 1
+        assert _rel(y, ref) < 1e-2
+    finally:
+        lib.cgs_gemm_set_variant(-1)
+
+
+@pytest.mark.parametrize("M,N2,K", [(65536, 5120, 640), (16384, 10240, 1280)])
+@pytest.mark.parametrize("variant", [5, 7])
+def test_gemm_geglu_bench_shapes(cuda, M, N2, K, variant):
+    lib = _native.load_kernels()
+    lib.cgs_gemm_set_variant(variant)
+    try:
+        torch.manual_seed(0)
+        a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+        w = (torch.randn(N2, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+        b = torch.randn(N2, device=cuda).to(torch.bfloat16)
+        y = ops.linear_geglu(a, core.geglu_interleave(w), core.geglu_interleave(b))
+        h = a.float() @ w.float().t() + b.float()
+        x1, g = h.chunk(2, dim=-1)
+        ref = x1 * F.gelu(g)
+        assert ops.stats().get(("gemm_geglu", "hip"), 0) == 1
+        assert _rel(y, ref) < 1e-2
+    finally:
+        lib.cgs_gemm_set_variant(-1)
