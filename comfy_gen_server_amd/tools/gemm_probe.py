@@ -22,9 +22,14 @@ def main(argv):
         iters = int(argv[6]) if len(argv) > 6 else 20
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(torch.bfloat16)
-        lib.cgs_gemm_set_variant(var)
         lib.cgs_set_tile_group(grp)
-        fn = lambda: ops.linear(a, w)  # noqa: E731
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        from comfy_gen_server_amd.ops import core
+
+        def fn():  # the kernel itself (no autotune table, no library candidate)
+            err = lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K, K, K, N, 0, 0,
+                                      1.0, var, core._stream())
+            assert err == 0, err
         flops = 2.0 * M * N * K
     else:
         N, Ci, H, W, Co = (int(v) for v in argv[1:6])
