@@ -18,6 +18,8 @@ import os
 
 import torch
 
+from ..runtime import device as dm
+
 from ..runtime.tokenizer import get_clip_tokenizer
 from .clip import CLIPTextModel, CLIP_L_CONFIG, CLIP_G_CONFIG, CLIP_H_CONFIG
 
@@ -299,15 +301,18 @@ class SDClipModel(torch.nn.Module):
         if has_w or sections == 0:
             rows.append(self.gen_empty_tokens(maxlen))
         out, pooled = self.encode(rows)
-        first_pooled = pooled[0:1].cpu()
+        # conditioning stays where node outputs live (the device: dm.intermediate_device) -- no
+        # D2H + H2D round trip per prompt encode before sampling
+        dev = dm.intermediate_device()
+        first_pooled = pooled[0:1].to(dev)
         if sections == 0:
-            return out[-1:].cpu(), first_pooled
+            return out[-1:].to(dev), first_pooled
         z = out[:sections]
         if has_w:
             wt = torch.tensor([[w for _, w in chunk] for chunk in pairs], dtype=z.dtype, device=z.device)
             z_empty = out[-1:]
             z = (z - z_empty) * wt[..., None] + z_empty
-        return z.reshape(1, -1, z.shape[-1]).cpu(), first_pooled
+        return z.reshape(1, -1, z.shape[-1]).to(dev), first_pooled
 
     def load_sd(self, sd):
         return self.transformer.load_state_dict(sd, strict=False)

@@ -25,6 +25,11 @@ EPI_RESIDUAL = 2
 EPI_GEGLU = 4
 EPI_SILU_IN = 8   # reserved
 
+# hipBLASLt (through ATen) as a GEMM autotune candidate: off unless explicitly requested -- the
+# hand-written MFMA kernels (v5/v6/v7) are the device GEMMs; profiles/r02_gemm_table_v7.md has the
+# per-shape comparison.
+_LIB_GEMM = os.environ.get("CGS_GEMM_LIB", "0") == "1"
+
 
 def _stream():
     return ctypes_stream(torch.cuda.current_stream())
@@ -54,8 +59,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
            residual: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ weight^T (+ bias) (+ residual). ``residual`` has y's shape (fused epilogue add).
 
-    Device path: the HIP GEMM family (v5 ping-pong 256x256x64, v3 8-wave 32x32 MFMA, v1 128x128),
-    the kernel picked per shape by ``ops.autotune`` among those and hipBLASLt (through ATen)."""
+    Device path: the HIP GEMM family (v7 persistent ping-pong 256x256x64 with a register epilogue,
+    v6 persistent 256x160, v5 ping-pong 256x256, v3 8-wave 32x32 MFMA, v1 128x128), the kernel picked
+    per shape by ``ops.autotune`` (hipBLASLt joins the candidates only with ``CGS_GEMM_LIB=1``)."""
     if weight.dtype == torch.float8_e4m3fn:
         return _linear_w8(x, weight, bias, residual)
     be = backend_for("gemm", x, "cgs_gemm_bf16")
@@ -100,7 +106,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             if K % 32 == 0 and N % 8 == 0:
                 cands.append(("v4", lambda: run_hip(4)))
             cands.append(("hip", lambda: run_hip(-1)))
-            cands.append(("lib", run_lib))
+            if _LIB_GEMM:     # vendor GEMM only as an explicit opt-in (CGS_GEMM_LIB=1)
+                cands.append(("lib", run_lib))
             choice = autotune.choose(("gemm", M, N, K, epi), cands, default="hip")
         if choice == "lib":
             count("gemm", "lib")
