@@ -91,6 +91,25 @@ def build_runtime(verbose=False):
     return so
 
 
+def build_sanitized(kinds: str, verbose=False):
+    """CPU sanitizer build of the host runtime as a standalone threaded stress binary
+    (csrc/runtime/tests/stress_main.cpp + every runtime source except the pybind module), e.g.
+    ``--sanitize=address,undefined`` or ``--sanitize=thread``. Returns the binary path."""
+    kinds = ",".join(k.strip() for k in kinds.split(",") if k.strip())
+    tag = kinds.replace(",", "_")
+    out_dir = os.path.join(ROOT, "build", "sanitize")
+    os.makedirs(out_dir, exist_ok=True)
+    srcs = [s for s in sorted(glob.glob(os.path.join(RDIR, "*.cpp"))) if not s.endswith("module.cpp")]
+    srcs.append(os.path.join(RDIR, "tests", "stress_main.cpp"))
+    exe = os.path.join(out_dir, f"runtime_stress_{tag}")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={kinds}",
+           "-fno-sanitize-recover=all", "-o", exe] + srcs + ["-lpthread"]
+    out = _run(cmd)
+    if verbose and out.strip():
+        print(out)
+    return exe
+
+
 def build_all(verbose=False):
     k = build_kernels(verbose)
     r = build_runtime(verbose)
@@ -98,5 +117,14 @@ def build_all(verbose=False):
 
 
 if __name__ == "__main__":
-    k, r = build_all(verbose="-v" in sys.argv)
-    print("built", k, r)
+    san = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--sanitize=")]
+    if san:
+        for kinds in san:
+            exe = build_sanitized(kinds, verbose="-v" in sys.argv)
+            print("built", exe)
+            r = subprocess.run([exe, os.path.join(ROOT, "build", "sanitize")])
+            if r.returncode != 0:
+                sys.exit(r.returncode)
+    else:
+        k, r = build_all(verbose="-v" in sys.argv)
+        print("built", k, r)

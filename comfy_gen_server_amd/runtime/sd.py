@@ -196,6 +196,25 @@ class VAE:
             memory_format=torch.channels_last if self.device.type == "cuda" else torch.contiguous_format)
 
     def decode(self, samples_in):
+        """Batched decode; on HBM exhaustion retry as the 3-pass tiled decode (reference
+        ``comfy/sd.py:300-302``). Fault site ``CGS_FAULT=oom:vae_decode`` exercises the fallback."""
+        try:
+            from ..utils.telemetry import maybe_fault
+            maybe_fault("vae", "vae_decode")
+            return self._decode_full(samples_in)
+        except torch.cuda.OutOfMemoryError:
+            logging.warning("Ran out of memory in regular VAE decoding; retrying with tiled VAE decoding.")
+            dm.soft_empty_cache(force=True)
+            return self.decode_tiled_(samples_in)
+
+    def decode_tiled_(self, samples, tile_x=64, tile_y=64, overlap=16):
+        """Three tilings with rotated aspect averaged (reference ``sd.py:261-286``): the seams of one
+        tiling fall inside the tiles of the others."""
+        return (self.decode_tiled(samples, tile_x // 2, tile_y * 2, overlap) +
+                self.decode_tiled(samples, tile_x * 2, tile_y // 2, overlap) +
+                self.decode_tiled(samples, tile_x, tile_y, overlap)) / 3.0
+
+    def _decode_full(self, samples_in):
         dm.load_model_gpu(self.patcher)
         out = []
         # the temporal decoder mixes across the frames of a decode call: decode a clip in one call
@@ -218,6 +237,23 @@ class VAE:
         return out.movedim(1, -1)
 
     def encode(self, pixel_samples):
+        """Batched encode with the OOM -> tiled fallback (reference ``comfy/sd.py:326-328``; fault site
+        ``CGS_FAULT=oom:vae_encode``)."""
+        try:
+            from ..utils.telemetry import maybe_fault
+            maybe_fault("vae", "vae_encode")
+            return self._encode_full(pixel_samples)
+        except torch.cuda.OutOfMemoryError:
+            logging.warning("Ran out of memory in regular VAE encoding; retrying with tiled VAE encoding.")
+            dm.soft_empty_cache(force=True)
+            return self.encode_tiled_(pixel_samples)
+
+    def encode_tiled_(self, pixel_samples, tile_x=512, tile_y=512, overlap=64):
+        return (self.encode_tiled(pixel_samples, tile_x, tile_y, overlap) +
+                self.encode_tiled(pixel_samples, tile_x * 2, tile_y // 2, overlap) +
+                self.encode_tiled(pixel_samples, tile_x // 2, tile_y * 2, overlap)) / 3.0
+
+    def _encode_full(self, pixel_samples):
         dm.load_model_gpu(self.patcher)
         px = pixel_samples.movedim(-1, 1)
         out = []

@@ -217,7 +217,7 @@ def maybe_fault(site: str, key: str):
         if site == "node" and kind == "node":
             _fired.add(item)
             raise InjectedFault(f"injected fault in node {key}")
-        if site == "node" and kind == "oom":
+        if site in ("node", "vae") and kind == "oom":
             _fired.add(item)
             raise torch.cuda.OutOfMemoryError(f"injected out-of-memory in node {key}")
         if site == "step" and kind == "step":

@@ -60,3 +60,27 @@ def test_json_logs(capsys):
     rec = logging.LogRecord("cgs", logging.INFO, __file__, 1, "hello %s", ("world",), None)
     d = json.loads(JsonFormatter().format(rec))
     assert d["msg"] == "hello world" and d["level"] == "INFO"
+
+
+@pytest.mark.parametrize("site", ["vae_decode", "vae_encode"])
+def test_vae_oom_falls_back_to_tiled(monkeypatch, caplog, site):
+    """An HBM OOM in the batched VAE pass retries as the 3-pass tiled pass (reference
+    comfy/sd.py:300-302 / 326-328), driven by the ``oom:vae_*`` fault site."""
+    import logging
+    import torch
+    from comfy_gen_server_amd.runtime import device as dm
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    from comfy_gen_server_amd.utils import telemetry
+    dm.set_cpu_mode(True)
+    _, _, vae = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=1, with_clip=False)
+    g = torch.Generator().manual_seed(0)
+    lat = torch.randn(1, 4, 8, 8, generator=g)
+    px = torch.rand(1, 64, 64, 3, generator=g)
+    ref = vae.decode(lat) if site == "vae_decode" else vae.encode(px)
+    monkeypatch.setenv("CGS_FAULT", f"oom:{site}")
+    telemetry._fired.clear()
+    with caplog.at_level(logging.WARNING):
+        out = vae.decode(lat) if site == "vae_decode" else vae.encode(px)
+    assert any("retrying with tiled" in r.message for r in caplog.records)
+    assert out.shape == ref.shape
+    assert (out - ref).abs().max().item() < 1e-3   # tiles cover the whole (small) input: same result
