@@ -184,10 +184,6 @@ def sample_dpm_2(model, x, sigmas, extra_args=None, callback=None, disable=None,
 def sample_dpm_2_ancestral(model, x, sigmas, extra_args=None, callback=None, disable=None, eta=1.0, s_noise=1.0,
                            noise_sampler=None):
     extra_args = {} if extra_args is None else extra_args
-    if noise_sampler is None:
-        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "euler_ancestral", eta, s_noise)
-        if r is not None:
-            return r
     ns = _noise_sampler(x, extra_args, noise_sampler)
     s = _f(sigmas)
     s_in = _s_in(x)
@@ -235,12 +231,9 @@ def sample_lms(model, x, sigmas, extra_args=None, callback=None, disable=None, o
         if len(ds) > order:
             ds.pop(0)
         _cb(callback, i, x, s[i], s[i], denoised)
-        if s[i + 1] == 0:
-            x = denoised
-        else:
-            cur = min(i + 1, order)
-            coeffs = [linear_multistep_coeff(cur, s, i, j) for j in range(cur)]
-            x = x + sum(c * d for c, d in zip(coeffs, reversed(ds)))
+        cur = min(i + 1, order)      # the last step integrates to sigma 0 too (sampling.py:282-284)
+        coeffs = [linear_multistep_coeff(cur, s, i, j) for j in range(cur)]
+        x = x + sum(c * d for c, d in zip(coeffs, reversed(ds)))
     return x
 
 
@@ -248,10 +241,6 @@ def sample_lms(model, x, sigmas, extra_args=None, callback=None, disable=None, o
 def sample_dpmpp_2s_ancestral(model, x, sigmas, extra_args=None, callback=None, disable=None, eta=1.0, s_noise=1.0,
                               noise_sampler=None):
     extra_args = {} if extra_args is None else extra_args
-    if noise_sampler is None:
-        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "euler_ancestral", eta, s_noise)
-        if r is not None:
-            return r
     ns = _noise_sampler(x, extra_args, noise_sampler)
     s = _f(sigmas)
     s_in = _s_in(x)
@@ -291,15 +280,15 @@ def sample_dpmpp_sde(model, x, sigmas, extra_args=None, callback=None, disable=N
             continue
         t, t_next = -math.log(s[i]), -math.log(s[i + 1])
         h = t_next - t
-        s_ = t + h * r
+        s_mid = t + h * r
         fac = 1 / (2 * r)
         sig = lambda tt: math.exp(-tt)  # noqa: E731
-        # step 1
-        sd, su = get_ancestral_step(sig(t), sig(s_), eta)
+        # step 1: ancestral step to the midpoint; the model is evaluated AT the midpoint
+        sd, su = get_ancestral_step(sig(t), sig(s_mid), eta)
         s_ = -math.log(sd)
         x2 = (sig(s_) / sig(t)) * x - math.expm1(t - s_) * denoised
-        x2 = x2 + ns(sig(t), sig(s_)) * s_noise * su
-        denoised2 = _model(model, x2, sig(s_), extra_args, s_in)
+        x2 = x2 + ns(sig(t), sig(s_mid)) * s_noise * su
+        denoised2 = _model(model, x2, sig(s_mid), extra_args, s_in)
         # step 2
         sd, su = get_ancestral_step(sig(t), sig(t_next), eta)
         t_next_ = -math.log(sd)

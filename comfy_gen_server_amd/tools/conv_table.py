@@ -1,0 +1,107 @@
+"""Per-shape conv table on the SDXL bench shapes (UNet batch 16 at 1024^2, VAE decode batch 8):
+every HIP conv variant vs MIOpen (F.conv2d, channels_last) in TF/s.
+
+python -m comfy_gen_server_amd.tools.conv_table [out.md] [--vae]
+"""
+from __future__ import annotations
+
+import math
+import sys
+
+import torch
+import torch.nn.functional as F
+
+UNET = [  # (name, N, H, W, Cin, Cout, k, stride)
+    ("L0 res 320", 16, 128, 128, 320, 320, 3, 1),
+    ("L0 out-res 960->320", 16, 128, 128, 960, 320, 3, 1),
+    ("L0 out-res 640->320", 16, 128, 128, 640, 320, 3, 1),
+    ("L0 down s2", 16, 128, 128, 320, 320, 3, 2),
+    ("L1 res 320->640", 16, 64, 64, 320, 640, 3, 1),
+    ("L1 res 640", 16, 64, 64, 640, 640, 3, 1),
+    ("L1 out-res 1920->640", 16, 64, 64, 1920, 640, 3, 1),
+    ("L1 out-res 1280->640", 16, 64, 64, 1280, 640, 3, 1),
+    ("L1 out-res 960->640", 16, 64, 64, 960, 640, 3, 1),
+    ("L1 down s2", 16, 64, 64, 640, 640, 3, 2),
+    ("L2 res 640->1280", 16, 32, 32, 640, 1280, 3, 1),
+    ("L2 res 1280", 16, 32, 32, 1280, 1280, 3, 1),
+    ("L2 out-res 2560->1280", 16, 32, 32, 2560, 1280, 3, 1),
+    ("L2 out-res 1920->1280", 16, 32, 32, 1920, 1280, 3, 1),
+    ("up conv 1280 @64", 16, 64, 64, 1280, 1280, 3, 1),
+    ("up conv 640 @128", 16, 128, 128, 640, 640, 3, 1),
+    ("skip 1x1 960->320", 16, 128, 128, 960, 320, 1, 1),
+]
+VAE = [
+    ("vae 512 @128", 8, 128, 128, 512, 512, 3, 1),
+    ("vae 512 @256", 8, 256, 256, 512, 512, 3, 1),
+    ("vae 512 @512", 8, 512, 512, 512, 512, 3, 1),
+    ("vae 512->256 @512", 8, 512, 512, 512, 256, 3, 1),
+    ("vae 256 @512", 8, 512, 512, 256, 256, 3, 1),
+    ("vae 256 @1024", 8, 1024, 1024, 256, 256, 3, 1),
+    ("vae 256->128 @1024", 8, 1024, 1024, 256, 128, 3, 1),
+    ("vae 128 @1024", 8, 1024, 1024, 128, 128, 3, 1),
+]
+VARIANTS = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7}
+
+
+def _time(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main(argv):
+    from comfy_gen_server_amd import _native
+    from comfy_gen_server_amd.ops import core
+    lib = _native.load_kernels()
+    dev = torch.device("cuda", 0)
+    shapes = UNET + (VAE if "--vae" in argv else [])
+    argv = [a for a in argv if a != "--vae"]
+    rows = ["| conv | N | HxW | Cin | Cout | k/s | " + " | ".join(f"{v} TF/s" for v in VARIANTS) + " | MIOpen TF/s |",
+            "|---|---:|---|---:|---:|---|" + "---:|" * (len(VARIANTS) + 1)]
+    for name, N, H, W, Cin, Cout, k, s in shapes:
+        p = k // 2
+        x = (torch.rand(N, Cin, H, W, device=dev) * 2 - 1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = ((torch.rand(Cout, Cin, k, k, device=dev) * 2 - 1) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
+        wn = w.permute(0, 2, 3, 1).contiguous()
+        b = torch.zeros(Cout, device=dev, dtype=torch.bfloat16)
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        out = torch.empty(N, Cout, Ho, Wo, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        flops = 2.0 * N * Ho * Wo * Cout * Cin * k * k
+        it = max(2, int(3e11 / flops))
+        ref = F.conv2d(x[:1].float(), w.float(), b.float(), s, p)
+        res = {}
+        for vn, v in VARIANTS.items():
+            def run(v=v):
+                return lib.cgs_conv2d_nhwc_v(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
+                                             out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0, v,
+                                             core._stream())
+            try:
+                if run() != 0:
+                    res[vn] = float("nan")
+                    continue
+                torch.cuda.synchronize()
+                err = ((out[:1].float() - ref).norm() / ref.norm()).item()
+                res[vn] = flops / _time(run, it) / 1e9 if err < 2e-2 else -1.0
+            except Exception:
+                res[vn] = float("nan")
+        ms = _time(lambda: F.conv2d(x, w, b, s, p), it)
+        res["miopen"] = flops / ms / 1e9
+        rows.append(f"| {name} | {N} | {H}x{W} | {Cin} | {Cout} | {k}/{s} | " +
+                    " | ".join("bad" if res[v] == -1.0 else f"{res[v]:.0f}" for v in VARIANTS) +
+                    f" | {res['miopen']:.0f} |")
+        print(rows[-1], flush=True)
+        del x, w, wn, out
+    text = "\n".join(rows)
+    if argv:
+        open(argv[0], "w").write(text + "\n")
+    print(text)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

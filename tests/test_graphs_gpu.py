@@ -96,3 +96,19 @@ def test_step_graph_matches_eager_loop(cuda, monkeypatch, sampler):
     for a, b in zip(res["0"], res["1"]):
         err = (a - b).abs().max().item()
         assert err < 2e-2 * (a.abs().max().item() + 1), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampler", ["dpm_2_ancestral", "dpmpp_2s_ancestral", "heun"])
+def test_step_graph_only_serves_euler_family(cuda, monkeypatch, sampler):
+    """The whole-step graph implements Euler / Euler-a only; other samplers must run their own loop."""
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    from comfy_gen_server_amd.parallel.dp import Job, generate_local
+    from comfy_gen_server_amd.sampling import step_graph
+    monkeypatch.setenv("CGS_GRAPHS", "1")
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        jobs = step_graph.stats["jobs"]
+        generate_local(patcher, clip, vae, Job(batch=2, steps=3, sampler=sampler, width=64, height=64, seed=1), 0, 2,
+                       decode=False)
+    assert step_graph.stats["jobs"] == jobs
