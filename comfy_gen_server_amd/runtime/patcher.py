@@ -38,15 +38,13 @@ def set_model_options_post_cfg_function(model_options, post_cfg_function, disabl
 
 
 def weight_decompose(dora_scale, weight, lora_diff, alpha, strength):
-    dora_scale = dora_scale.to(weight.device, weight.dtype)
-    lora_diff = lora_diff * alpha
-    wc = weight + lora_diff.to(weight.dtype)
+    """DoRA as the reference applies it (``comfy/model_patcher.py:10-19``, ``:353-355``): add the
+    strength-scaled low-rank delta, then rescale every input-column slice of the merged weight to the
+    learned magnitude ``dora_scale``."""
+    wc = weight + (strength * alpha) * lora_diff.to(weight.dtype)
     norm = wc.transpose(0, 1).reshape(wc.shape[1], -1).norm(dim=1, keepdim=True)
     norm = norm.reshape(wc.shape[1], *[1] * (wc.dim() - 1)).transpose(0, 1)
-    wc = wc * (dora_scale / norm).to(weight.dtype)
-    if strength != 1.0:
-        return weight + strength * (wc - weight)
-    return wc
+    return wc * (dora_scale.to(weight.device, weight.dtype) / norm)
 
 
 def _f(t, like):
@@ -102,8 +100,8 @@ def calculate_weight(patches, weight, key):
                     w2 = torch.einsum("i j k l, j r, i p -> p r k l", _f(t2, weight), _f(w2b, weight), _f(w2a, weight))
             else:
                 w2 = _f(w2, weight)
-            if weight.dim() == 4:
-                w2 = w2.unsqueeze(2).unsqueeze(2)
+            if w2.dim() == 4:      # conv LoKr: w1 [a, b] -> [a, b, 1, 1] so kron spans the taps of w2
+                w1 = w1.unsqueeze(2).unsqueeze(2)
             alpha = (alpha / dim) if (alpha is not None and dim is not None) else 1.0
             diff = torch.kron(w1, w2).reshape(weight.shape)
             weight = weight_decompose(dora, weight, diff, alpha, strength) if dora is not None \

@@ -183,3 +183,126 @@ def test_samplers_match_reference(tmp_path):
 
 def test_cond_batching_matches_reference(tmp_path):
     assert "cond ok" in _run(_COND, tmp_path)
+
+
+_TOK = r'''
+import os, tempfile
+import comfy.sd1_clip as R
+from comfy_gen_server_amd.models import text_encoders as O
+from safetensors.torch import save_file
+d = tempfile.mkdtemp()
+g = torch.Generator().manual_seed(3)
+save_file({"emb_params": torch.randn(3, 768, generator=g)}, os.path.join(d, "myemb.safetensors"))
+prompts = [
+    "a photo of a cat",
+    "a (photo:1.3) of a ((cat)), [dog] (nested (emphasis:0.5) here:1.2)",
+    "escaped \\(not weighted\\) text and (weighted \\) inside:1.1)",
+    "newline\nseparated   spaces,and,commas!! unicode: café üñîçødé",
+    " ".join(["word%d" % i for i in range(120)]),
+    "supercalifragilisticexpialidocious antidisestablishmentarianism " * 12,
+    "embedding:myemb, a painting (embedding:myemb:1.4) and embedding:missing_one",
+    "",
+    "(unclosed paren and: colon",
+]
+for kw in (dict(), dict(pad_with_end=False), dict(pad_to_max_length=False), dict(has_start_token=True, min_length=80)):
+    rt = R.SDTokenizer(embedding_directory=d, **kw)
+    ot = O.SDTokenizer(embedding_directory=d, **kw)
+    for p in prompts:
+        for wid in (False, True):
+            a = ot.tokenize_with_weights(p, return_word_ids=wid)
+            b = rt.tokenize_with_weights(p, return_word_ids=wid)
+            assert len(a) == len(b), (p, kw, len(a), len(b))
+            for ca, cb in zip(a, b):
+                assert len(ca) == len(cb), (p, kw, len(ca), len(cb))
+                for ta, tb in zip(ca, cb):
+                    assert len(ta) == len(tb)
+                    if isinstance(tb[0], torch.Tensor):
+                        assert isinstance(ta[0], torch.Tensor) and torch.allclose(ta[0].float(), tb[0].float()), p
+                    else:
+                        assert ta[0] == tb[0], (p, kw, ta, tb)
+                    assert abs(ta[1] - tb[1]) < 1e-6, (p, kw, ta, tb)
+                    if wid:
+                        assert ta[2] == tb[2], (p, kw, ta, tb)
+print("tokenizer ok")
+'''
+
+
+def test_tokenizer_emphasis_ti_chunking_match_reference(tmp_path):
+    """Prompt emphasis / escapes / 77-token chunking / long-word splitting / textual inversion /
+    word ids (comfy/sd1_clip.py:201-480) against the reference SDTokenizer (transformers CLIPTokenizer
+    on comfy/sd1_tokenizer) -- this engine uses its own byte-level BPE."""
+    assert "tokenizer ok" in _run(_TOK, tmp_path)
+
+
+_LORA = r'''
+import types, copy
+import comfy.lora as RL, comfy.model_patcher as RP, comfy.utils as RUt
+from comfy_gen_server_amd.runtime import lora as OL, patcher as OP
+from comfy_gen_server_amd.tools import synth
+g = torch.Generator().manual_seed(7)
+rn = lambda *s: torch.randn(*s, generator=g) * 0.1
+W = {"lin": rn(64, 48), "conv": rn(32, 16, 3, 3)}
+lora = {}
+to_load = {}
+def add(prefix, target, entries):
+    to_load[prefix] = target
+    for k, v in entries.items():
+        lora[prefix + "." + k] = v
+# Linear targets (out 64, in 48), rank 4
+add("l_lora", "lin.lora", {"lora_up.weight": rn(64, 4), "lora_down.weight": rn(4, 48), "alpha": torch.tensor(2.0)})
+add("l_dora", "lin.dora", {"lora_up.weight": rn(64, 4), "lora_down.weight": rn(4, 48), "alpha": torch.tensor(4.0),
+                           "dora_scale": rn(64, 1).abs() + 0.5})
+add("l_diffusers", "lin.diffusers", {"lora_linear_layer.up.weight": rn(64, 4), "lora_linear_layer.down.weight": rn(4, 48)})
+add("l_loha", "lin.loha", {"hada_w1_a": rn(64, 4), "hada_w1_b": rn(4, 48), "hada_w2_a": rn(64, 4), "hada_w2_b": rn(4, 48),
+                           "alpha": torch.tensor(3.0)})
+add("l_lokr", "lin.lokr", {"lokr_w1": rn(8, 6), "lokr_w2_a": rn(8, 2), "lokr_w2_b": rn(2, 8), "alpha": torch.tensor(1.0)})
+add("l_glora", "lin.glora", {"a1.weight": rn(4, 48), "a2.weight": rn(48, 4), "b1.weight": rn(4, 48), "b2.weight": rn(64, 4),
+                             "alpha": torch.tensor(2.0)})
+add("l_diff", "lin.diff", {"diff": rn(64, 48)})
+# Conv targets (32, 16, 3, 3): LoCon with mid, LoHa with Tucker cores, LoKr full
+add("c_locon", "conv.locon", {"lora_up.weight": rn(32, 4, 1, 1), "lora_down.weight": rn(4, 16, 1, 1),
+                              "lora_mid.weight": rn(4, 4, 3, 3), "alpha": torch.tensor(2.0)})
+add("c_lora", "conv.lora", {"lora_up.weight": rn(32, 4, 1, 1), "lora_down.weight": rn(4, 16, 3, 3)})
+add("c_loha", "conv.loha", {"hada_w1_a": rn(4, 32), "hada_w1_b": rn(4, 16), "hada_w2_a": rn(4, 32), "hada_w2_b": rn(4, 16),
+                            "hada_t1": rn(4, 4, 3, 3), "hada_t2": rn(4, 4, 3, 3), "alpha": torch.tensor(2.0)})
+add("c_lokr", "conv.lokr", {"lokr_w1": rn(4, 2), "lokr_w2": rn(8, 8, 3, 3)})
+pr = RL.load_lora(lora, to_load)
+po = OL.load_lora(lora, to_load)
+assert set(pr) == set(po), (set(pr) ^ set(po))
+fake = types.SimpleNamespace()
+fake.calculate_weight = lambda p, w, k: RP.ModelPatcher.calculate_weight(fake, p, w, k)
+for key in sorted(pr):
+    base = W[key.split(".")[0]]
+    assert pr[key][0] == po[key][0], key
+    for strength, smodel in ((1.0, 1.0), (0.6, 0.9)):
+        a = OP.calculate_weight([(strength, po[key], smodel)], base.clone(), key)
+        b = fake.calculate_weight([(strength, pr[key], smodel)], base.clone(), key)
+        close(a, b, 1e-5, key)
+# key maps: SDXL UNet (ldm + diffusers names) and SDXL CLIP-L/G
+unet_cfg = dict(synth.SDXL_UNET, num_head_channels=64)
+from comfy_gen_server_amd.models.unet import UNetModel
+with torch.device("meta"):
+    net = UNetModel(**unet_cfg, dtype=torch.float16, device=torch.device("meta"))
+keys = ["diffusion_model." + k for k in net.state_dict().keys()]
+fm = types.SimpleNamespace(state_dict=lambda: {k: None for k in keys},
+                           model_config=types.SimpleNamespace(unet_config=unet_cfg))
+ko = OL.model_lora_keys_unet(fm, {})
+kr = RL.model_lora_keys_unet(fm, {})
+assert ko == kr, (len(ko), len(kr), sorted(set(ko.items()) ^ set(kr.items()))[:5])
+from comfy_gen_server_amd.runtime import families
+ct = families.SDXL(dict(synth.SDXL_UNET)).clip_target()
+with torch.device("meta"):
+    cm = ct.stack(dtype=torch.float16, device=torch.device("meta"))
+ck = {k: None for k in cm.state_dict().keys()}
+cf = types.SimpleNamespace(state_dict=lambda: ck)
+co, cr = OL.model_lora_keys_clip(cf, {}), RL.model_lora_keys_clip(cf, {})
+assert co == cr and len(co) > 100, (len(co), len(cr))
+print("lora ok", len(ko), len(co))
+'''
+
+
+def test_lora_lycoris_patches_and_key_maps_match_reference(tmp_path):
+    """LoRA / LoCon (mid) / DoRA / diffusers / LoHa (+Tucker) / LoKr / GLoRA / diff patches parsed and
+    merged exactly like comfy/lora.py:14-166 + comfy/model_patcher.py:316-452; UNet (ldm + diffusers
+    names) and CLIP-L/G key maps equal to comfy/lora.py:169-241 on the SDXL architecture."""
+    assert "lora ok" in _run(_LORA, tmp_path)
