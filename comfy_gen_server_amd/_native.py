@@ -68,6 +68,8 @@ KERNEL_SIGNATURES = {
     # y = GN(x + pre_add) (+SiLU); NHWC layout, x [N, HW, C]; ws = torch-allocated workspace
     "cgs_groupnorm_nhwc_ws": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P],
     "cgs_groupnorm_workspace": [_I, _I, _I],
+    # GroupNorm over cat([x, x2], C) without materialising the concat (K14): x, x2, C1, y, ...
+    "cgs_groupnorm_nhwc_dual": [_P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P],
     # y = LN(x) over last dim; rows x C
     "cgs_layernorm": [_P, _P, _P, _P, _I, _I, _F, _I, _P],
     # flash attention forward (bf16): q,k,v,o + strides (elements) + shapes

@@ -18,6 +18,7 @@
 #include "mfma_core.h"
 #include "mfma_pp.h"
 #include "mfma_pp160.h"
+#include "mfma_ppk.h"
 
 #define EPI_BIAS 1
 #define EPI_RESIDUAL 2
@@ -340,6 +341,30 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   conv_nhwc_v6_kernel<<<grid, pq::THREADS, pq::LDS, stream>>>(a);
 }
 
+// v7: the persistent 256 x 256 ping-pong with cross-tile prefetch and register epilogue (mfma_ppk.h)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v7_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  ConvGatherA8 al;
+  al.a = &a;
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  ppk::run<false>(al, a.w, K, M, a.Cout, K, e, smem, (M + ppk::BM - 1) / ppk::BM, a.tiles_n, a.group_m);
+}
+
+static void conv_v7_go(ConvArgs& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = (a.Cout + ppk::BN - 1) / ppk::BN;
+  const long long T = (long long)((M + ppk::BM - 1) / ppk::BM) * a.tiles_n;
+  const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
+  conv_nhwc_v7_kernel<<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+}
+
 static int g_conv_group = 8;
 CGS_EXPORT void cgs_conv_set_tile_group(int g) { g_conv_group = g < 1 ? 1 : g; }
 static int g_conv_variant = -1;   // -1 auto (v3/8 waves where legal), 2 = v2 only, 3 = v3/4 waves, 4 = v3/8 waves
@@ -349,6 +374,11 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
   a.group_m = g_conv_group;
   if (variant == 5 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0)) {
     conv_v5_go(a, stream);
+    return (int)hipGetLastError();
+  }
+  if (variant == 7 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
+      ((uintptr_t)a.bias % 8) == 0 && (long long)a.Cout * a.kh * a.kw * a.Cin * 2 < (1ll << 32)) {
+    conv_v7_go(a, stream);
     return (int)hipGetLastError();
   }
   if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&

@@ -22,8 +22,17 @@ static inline int gn_pix_per_block(int N, int HW) {
   return ppb;
 }
 
+// Dual-source rows (K14: the UNet decoder's torch.cat([h, skip], 1) is never materialised): channel
+// c < C1 of pixel `pix` lives in x (rows of C1), channel c >= C1 in x2 (rows of C - C1). Single-source
+// calls pass C1 = C. C1 % 8 == 0, so an 8-channel vector never straddles the two sources.
+__device__ __forceinline__ const u16* gn_src(const u16* __restrict__ x, const u16* __restrict__ x2, int C, int C1,
+                                             size_t pix, int c) {
+  return c < C1 ? x + pix * C1 + c : x2 + pix * (size_t)(C - C1) + (c - C1);
+}
+
 template <int DT, int KM>
-__global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, float* __restrict__ part,
+__global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, const u16* __restrict__ x2,
+                                                               int C1, float* __restrict__ part,
                                                                int HW, int C, int ppb, int nb, int CS) {
   // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget).
   // KM = 16-byte chunk rounds per lane (ceil(CS / 512)); each wave keeps GN_UNROLL rows of loads in
@@ -37,14 +46,14 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nchunk = CS >> 3;
-  const u16* xn = x + (size_t)n * HW * C + c0;
+  const size_t pix0 = (size_t)n * HW;
   // shift = the block's first pixel (shared by all 4 waves): keeps the shifted sums well conditioned
   float s1[KM][8], s2[KM][8], sh[KM][8];
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     int ch = lane + 64 * k;
     s16x8 v = {};
-    if (ch < nchunk && p0 < p1) v = *reinterpret_cast<const s16x8*>(xn + (size_t)p0 * C + ch * 8);
+    if (ch < nchunk && p0 < p1) v = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, pix0 + p0, c0 + ch * 8));
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sh[k][j] = cvt_in<DT>((u16)v[j]); s1[k][j] = 0.f; s2[k][j] = 0.f; }
   }
@@ -57,7 +66,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         int ch = lane + 64 * k;
-        if (pu < p1 && ch < nchunk) buf[u][k] = *reinterpret_cast<const s16x8*>(xn + (size_t)pu * C + ch * 8);
+        if (pu < p1 && ch < nchunk) buf[u][k] = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, pix0 + pu, c0 + ch * 8));
       }
     }
 #pragma unroll
@@ -182,7 +191,8 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
 }
 
 template <int DT, bool SILU>
-__global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y,
+__global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ x2, int C1,
+                                                      u16* __restrict__ y,
                                                       const float* __restrict__ ab, int rows_total, int rows_per_iter,
                                                       int HW, int C) {
   // The grid stride is a whole number of rows, so every thread keeps ONE 8-channel chunk for its whole
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x
       }
     }
     const size_t i = (size_t)row * cpr + ch;
-    s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
+    s16x8 v = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, (size_t)row, ch * 8));
     s16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -226,12 +236,12 @@ CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
 
 // x, y: [N, HW, C] (NHWC); gamma/beta [C] in the activation dtype; pre_add [N, C] (act dtype) or null.
 // ws: workspace of cgs_groupnorm_workspace() bytes (torch-allocated so it is graph-capturable).
-CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,
-                                     void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
-                                     hipStream_t stream) {
+static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const void* gamma, const void* beta,
+                          const void* pre_add, void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
+                          hipStream_t stream) {
   // channel slices of <= 2048 (the per-lane register budget of gn_partial), equal and 8-aligned
   const int ns = (C + 2047) / 2048;
-  if (C % 8 || C % G || C % (8 * ns) || C > 8192) return (int)hipErrorInvalidValue;
+  if (C % 8 || C % G || C % (8 * ns) || C > 8192 || C1 % 8 || C1 > C) return (int)hipErrorInvalidValue;
   const int CS = C / ns;
   int ppb = gn_pix_per_block(N, HW);
   int nb = (HW + ppb - 1) / ppb;
@@ -241,9 +251,9 @@ CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, 
   const int km = (CS / 8 + 63) / 64;  // 1..4
 #define CGS_GN_PARTIAL(KMV)                                                                                     \
   if (dtype == CGS_BF16)                                                                                        \
-    gn_partial_kernel<CGS_BF16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb, CS); \
+    gn_partial_kernel<CGS_BF16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS); \
   else                                                                                                          \
-    gn_partial_kernel<CGS_F16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, part, HW, C, ppb, nb, CS);
+    gn_partial_kernel<CGS_F16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS);
   if (km == 1) { CGS_GN_PARTIAL(1) } else if (km == 2) { CGS_GN_PARTIAL(2) } else if (km == 3) { CGS_GN_PARTIAL(3) } else { CGS_GN_PARTIAL(4) }
 #undef CGS_GN_PARTIAL
   gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
@@ -257,13 +267,26 @@ CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, 
   int rows_per_iter = (blocks * 256) / cpr;  // cpr <= 1024 <= blocks * 256 whenever chunks >= cpr
   if (rows_per_iter < 1) rows_per_iter = 1, blocks = (cpr + 255) / 256;
   if (dtype == CGS_BF16) {
-    if (silu) gn_apply_kernel<CGS_BF16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
-    else gn_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
+    if (silu) gn_apply_kernel<CGS_BF16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)x2, C1, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
+    else gn_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)x2, C1, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
   } else {
-    if (silu) gn_apply_kernel<CGS_F16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
-    else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
+    if (silu) gn_apply_kernel<CGS_F16, true><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)x2, C1, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
+    else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)x2, C1, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
   }
   return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,
+                                     void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
+                                     hipStream_t stream) {
+  return groupnorm_impl(x, nullptr, C, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream);
+}
+
+// GroupNorm over the channel concat of x ([N, HW, C1]) and x2 ([N, HW, C - C1]) without materialising it.
+CGS_EXPORT int cgs_groupnorm_nhwc_dual(const void* x, const void* x2, int C1, void* y, const void* gamma,
+                                       const void* beta, const void* pre_add, void* ws, int N, int HW, int C, int G,
+                                       float eps, int silu, int dtype, hipStream_t stream) {
+  return groupnorm_impl(x, x2, C1, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -92,9 +92,15 @@ class Conv2d(nn.Module, DerivedMixin):
     def weight_nhwc(self):
         return self._derived_get("w_nhwc", lambda: self.weight.permute(0, 2, 3, 1).contiguous())
 
-    def forward(self, x, residual=None, upsample2x=False):
+    def forward(self, x, residual=None, upsample2x=False, x2=None):
+        """``x2``: convolve cat([x, x2], 1) without materialising the concat (K14)."""
         w, b = self.weight, self.bias
         wn = None
+        if x2 is not None:
+            if x.is_cuda and self.groups == 1 and w.dtype == x.dtype and w.device == x.device:
+                return ops.conv2d(x, w, b, self.stride, self.padding, residual=residual,
+                                  weight_nhwc=self.weight_nhwc(), groups=self.groups, x2=x2)
+            x = torch.cat([x, x2], dim=1)
         if w.dtype != x.dtype or w.device != x.device:
             w = w.to(device=x.device, dtype=x.dtype)
             b = None if b is None else b.to(device=x.device, dtype=x.dtype)
@@ -185,12 +191,12 @@ class GroupNorm(nn.Module):
             self.register_parameter("weight", None)
             self.register_parameter("bias", None)
 
-    def forward(self, x, silu=False):
+    def forward(self, x, silu=False, x2=None):
         w, b = self.weight, self.bias
         if w is not None and (w.dtype != x.dtype or w.device != x.device):
             w = w.to(device=x.device, dtype=x.dtype)
             b = b.to(device=x.device, dtype=x.dtype)
-        return ops.group_norm(x, self.num_groups, w, b, self.eps, silu=silu)
+        return ops.group_norm(x, self.num_groups, w, b, self.eps, silu=silu, x2=x2)
 
 
 class LayerNorm(nn.Module):

@@ -27,6 +27,24 @@ from .attention import BasicTransformerBlock, SpatialTransformer, _Seq
 from .layers import Conv2d, Conv3d, GroupNorm, Linear
 
 
+class SkipCat:
+    """``torch.cat([h, skip], 1)`` of the UNet decoder kept as its two halves (K14): the output
+    ResBlock's GroupNorm and 1x1 skip conv read the channel concat straight from both tensors, so the
+    concat (openaimodel.py:879) is never written. Anything else materialises it."""
+    __slots__ = ("a", "b")
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    @property
+    def shape(self):
+        return torch.Size((self.a.shape[0], self.a.shape[1] + self.b.shape[1]) + tuple(self.a.shape[2:]))
+
+    def materialize(self):
+        h = torch.cat([self.a, self.b], dim=1)
+        return h.contiguous(memory_format=torch.channels_last) if h.is_cuda else h
+
+
 class ResBlock(nn.Module):
     def __init__(self, channels, emb_channels, out_channels=None, dtype=None, device=None,
                  kernel_size=3, skip_t_emb=False):
@@ -48,14 +66,23 @@ class ResBlock(nn.Module):
             self.skip_connection = Conv2d(channels, out_channels, 1, dtype=dtype, device=device)
 
     def forward(self, x, emb_silu, transformer_options=None):
+        if isinstance(x, SkipCat):
+            if isinstance(self.skip_connection, nn.Identity):
+                x = x.materialize()
+            else:
+                h = self.in_layers[2](self.in_layers[0](x.a, silu=True, x2=x.b))
+                return self._out(h, emb_silu, self.skip_connection(x.a, x2=x.b))
         h = self.in_layers[0](x, silu=True)
         h = self.in_layers[2](h)
+        skip = x if isinstance(self.skip_connection, nn.Identity) else None
+        return self._out(h, emb_silu, skip if skip is not None else self.skip_connection(x))
+
+    def _out(self, h, emb_silu, skip):
         pre = None
         if not self.skip_t_emb and emb_silu is not None:
             pre = self.emb_layers[1](emb_silu).to(h.dtype)          # [B, C]
         h = ops.group_norm(h, 32, self.out_layers[0].weight, self.out_layers[0].bias,
                            self.out_layers[0].eps, silu=True, pre_add=pre)
-        skip = x if isinstance(self.skip_connection, nn.Identity) else self.skip_connection(x)
         return self.out_layers[3](h, residual=skip)
 
 
@@ -159,6 +186,8 @@ class TimestepEmbedSequential(nn.ModuleList):
     def forward(self, x, emb_silu, context, transformer_options, output_shape=None, time_context=None,
                 num_video_frames=None, image_only_indicator=None):
         for layer in self:
+            if isinstance(x, SkipCat) and not (isinstance(layer, ResBlock) and not isinstance(layer, VideoResBlock)):
+                x = x.materialize()
             if isinstance(layer, VideoResBlock):
                 x = layer(x, emb_silu, transformer_options, num_video_frames, image_only_indicator)
             elif isinstance(layer, ResBlock):
@@ -436,9 +465,12 @@ class UNetModel(nn.Module):
             hsp = _apply_control(hsp, control, "output")
             for p in patches.get("output_block_patch", []):
                 h, hsp = p(h, hsp, to)
-            h = torch.cat([h, hsp], dim=1)
-            if x.is_cuda:
-                h = h.contiguous(memory_format=torch.channels_last)
+            if x.is_cuda and h.shape[1] % 64 == 0 and hsp.shape[1] % 64 == 0 and h.dtype == hsp.dtype:
+                h = SkipCat(h, hsp)          # consumed by the block's ResBlock without a concat
+            else:
+                h = torch.cat([h, hsp], dim=1)
+                if x.is_cuda:
+                    h = h.contiguous(memory_format=torch.channels_last)
             out_shape = hs[-1].shape if hs else None
             h = mod(h, emb_silu, context, to, output_shape=out_shape, **vk)
         h = self.out[0](h, silu=True)

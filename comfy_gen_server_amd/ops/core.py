@@ -324,35 +324,50 @@ def attention_reference(q, k, v, heads, mask=None, causal=False, key_padding=Non
 # Normalisation
 # ----------------------------------------------------------------------------------------------
 def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: torch.Tensor | None,
-               eps: float, silu: bool = False, pre_add: torch.Tensor | None = None) -> torch.Tensor:
+               eps: float, silu: bool = False, pre_add: torch.Tensor | None = None,
+               x2: torch.Tensor | None = None) -> torch.Tensor:
     """GroupNorm (+ fused SiLU) over a 4-D image tensor (K06).
 
     ``pre_add`` ([N, C]) is added per (sample, channel) BEFORE normalising — this is how the
     ResBlock timestep-embedding add (openaimodel.py:245-264) is fused into the GroupNorm kernel.
+    ``x2``: normalise ``cat([x, x2], 1)`` without materialising the concat (K14, the UNet decoder's
+    skip connection, openaimodel.py:879); the kernel reads each 8-channel vector from its source.
     """
     be = backend_for("groupnorm", x, "cgs_groupnorm_nhwc_ws")
+    Ct = x.shape[1] + (0 if x2 is None else x2.shape[1])
     if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16) and \
-            weight is not None and x.shape[1] % 8 == 0 and x.shape[1] % groups == 0 and x.shape[1] <= 8192 and \
-            x.shape[1] % (8 * ((x.shape[1] + 2047) // 2048)) == 0:
+            weight is not None and Ct % 8 == 0 and Ct % groups == 0 and Ct <= 8192 and \
+            Ct % (8 * ((Ct + 2047) // 2048)) == 0 and x.shape[1] % 8 == 0 and \
+            (x2 is None or (x2.dtype == x.dtype and x2.shape[0] == x.shape[0] and x2.shape[2:] == x.shape[2:])):
         count("groupnorm", "hip")
-        N, C, H, W = x.shape
+        N, C1, H, W = x.shape
+        C = Ct
         # the kernel reads gamma/beta in the activation dtype: cast fp8 / offloaded / mixed-dtype params
         if weight.dtype != x.dtype or weight.device != x.device or not weight.is_contiguous():
             weight = weight.to(device=x.device, dtype=x.dtype).contiguous()
         if bias is not None and (bias.dtype != x.dtype or bias.device != x.device or not bias.is_contiguous()):
             bias = bias.to(device=x.device, dtype=x.dtype).contiguous()
         xc = x.contiguous(memory_format=torch.channels_last)
-        y = torch.empty_like(xc, memory_format=torch.channels_last)
+        y = torch.empty((N, C, H, W), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
         pa = None
         if pre_add is not None:
             pa = pre_add.to(x.dtype).contiguous()
         wsb = int(_lib().cgs_groupnorm_workspace(N, H * W, C))
         ws = torch.empty((wsb + 3) // 4, device=x.device, dtype=torch.float32)
-        _check(_lib().cgs_groupnorm_nhwc_ws(xc.data_ptr(), y.data_ptr(), weight.data_ptr(),
-                                            _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups, float(eps),
-                                            1 if silu else 0, _DT[x.dtype], _stream()),
-               "cgs_groupnorm_nhwc_ws")
+        if x2 is None:
+            _check(_lib().cgs_groupnorm_nhwc_ws(xc.data_ptr(), y.data_ptr(), weight.data_ptr(),
+                                                _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups, float(eps),
+                                                1 if silu else 0, _DT[x.dtype], _stream()),
+                   "cgs_groupnorm_nhwc_ws")
+        else:
+            x2c = x2.contiguous(memory_format=torch.channels_last)
+            _check(_lib().cgs_groupnorm_nhwc_dual(xc.data_ptr(), x2c.data_ptr(), C1, y.data_ptr(), weight.data_ptr(),
+                                                  _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups,
+                                                  float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
+                   "cgs_groupnorm_nhwc_dual")
         return y
+    if x2 is not None:
+        x = torch.cat([x, x2], dim=1)
     count("groupnorm", "torch" if x.device.type == "cpu" else "lib")
     if pre_add is not None:
         x = x + pre_add.to(x.dtype)[:, :, None, None]
@@ -385,21 +400,30 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor 
 # ----------------------------------------------------------------------------------------------
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
            residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
-           groups: int = 1, upsample2x: bool = False) -> torch.Tensor:
+           groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
     """2-D convolution (K09/K10/K12). Device path: implicit-GEMM NHWC kernel on MFMA
     (csrc/kernels/conv.hip) with fused bias + residual epilogue; ``weight_nhwc`` = weight permuted
     to [Cout, kh, kw, Cin]. ``upsample2x`` reads the input through a nearest-2x upsample inside the
-    kernel (openaimodel.py Upsample: interpolate + conv) so the 4x tensor is never written."""
+    kernel (openaimodel.py Upsample: interpolate + conv) so the 4x tensor is never written.
+    ``x2``: convolve ``cat([x, x2], 1)`` with the concat never materialised (K14; the kernel's A-loader
+    picks the source per 64-channel K step, so both channel counts must be multiples of 64)."""
     if isinstance(stride, (tuple, list)):
         stride = stride[0]
     if isinstance(padding, (tuple, list)):
         padding = padding[0]
     be = backend_for("conv", x, "cgs_conv2d_nhwc")
     Cout, Cin_g, kh, kw = weight.shape
+    dual_ok = x2 is None or (x.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0 and x2.dtype == x.dtype
+                             and not upsample2x and Cout % 8 == 0)
+    if x2 is not None and (be != "hip" or not dual_ok):
+        x = torch.cat([x, x2], dim=1)
+        x2 = None
     if (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
             and x.dim() == 4 and x.shape[1] % 32 == 0 and (Cout % 8 == 0 or x.shape[1] % 64 == 0)):
         count("conv", "hip")
-        N, Cin, H, W = x.shape
+        N, C1, H, W = x.shape
+        Cin = C1 + (0 if x2 is None else x2.shape[1])
+        x2c = None if x2 is None else x2.contiguous(memory_format=torch.channels_last)
         Hl, Wl = (2 * H, 2 * W) if upsample2x else (H, W)
         Ho = (Hl + 2 * padding - kh) // stride + 1
         Wo = (Wl + 2 * padding - kw) // stride + 1
@@ -414,7 +438,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         def run(variant):
             out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype,
                               memory_format=torch.channels_last)
-            _check(_lib().cgs_conv2d_nhwc_v(xc.data_ptr(), None, Cin, weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
+            _check(_lib().cgs_conv2d_nhwc_v(xc.data_ptr(), _ptr(x2c), C1, weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
                                             out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding, Ho, Wo,
                                             flags, variant, _stream()), "cgs_conv2d_nhwc")
             return out
@@ -424,10 +448,11 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         if M * Cout * Cin * kh * kw >= (1 << 27):
             cands = [("v4", lambda: run(4))]
             if Cin % 64 == 0:
-                cands += [("v5", lambda: run(5)), ("v6", lambda: run(6)), ("v2", lambda: run(2))]
-            choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None)),
-                                     cands, default="auto")
-            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "auto": -2}[choice]
+                cands += [("v7", lambda: run(7)), ("v5", lambda: run(5)), ("v6", lambda: run(6)),
+                          ("v2", lambda: run(2))]
+            choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None))
+                                     + ((("dual", C1),) if x2c is not None else ()), cands, default="auto")
+            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7, "auto": -2}[choice]
         return run(variant)
     if upsample2x:
         x = upsample_nearest2x(x)

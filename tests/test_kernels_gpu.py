@@ -237,7 +237,7 @@ def test_elementwise(cuda):
     assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
 
 
-@pytest.fixture(params=[2, 3, 4, 5, 6], ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160"])
+@pytest.fixture(params=[2, 3, 4, 5, 6, 7], ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160", "cv7ppk"])
 def conv_variant(request):
     lib = _native.load_kernels()
     lib.cgs_conv_set_variant(request.param)
@@ -416,3 +416,54 @@ def test_gemm_geglu_bench_shapes(cuda, M, N2, K, variant):
         assert _rel(y, ref) < 1e-2
     finally:
         lib.cgs_gemm_set_variant(-1)
+
+
+@pytest.mark.parametrize("N,C1,C2,H,W", [(2, 1280, 1280, 16, 16), (2, 1280, 640, 16, 16), (1, 640, 320, 32, 24),
+                                         (3, 320, 320, 8, 8)])
+def test_groupnorm_dual_source(cuda, N, C1, C2, H, W):
+    """GroupNorm of cat([a, b], 1) read from both tensors (K14), groups straddling the seam included."""
+    torch.manual_seed(0)
+    a = (torch.randn(N, C1, H, W, device=cuda) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = (torch.randn(N, C2, H, W, device=cuda) - 1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(C1 + C2, device=cuda).to(torch.bfloat16)
+    bb = torch.randn(C1 + C2, device=cuda).to(torch.bfloat16)
+    y = ops.group_norm(a, 32, w, bb, 1e-5, silu=True, x2=b)
+    ref = F.silu(F.group_norm(torch.cat([a, b], 1).float(), 32, w.float(), bb.float(), 1e-5))
+    assert ops.stats().get(("groupnorm", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("C1,C2,Cout,k", [(1280, 1280, 1280, 3), (1280, 640, 640, 1), (640, 320, 320, 3), (320, 320, 320, 1)])
+def test_conv_dual_source(cuda, C1, C2, Cout, k, conv_variant):
+    torch.manual_seed(0)
+    a = torch.randn(2, C1, 16, 16, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(2, C2, 16, 16, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C1 + C2, k, k, device=cuda) / math.sqrt((C1 + C2) * k * k)).to(torch.bfloat16)
+    bias = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    y = ops.conv2d(a, w, bias, 1, k // 2, weight_nhwc=w.permute(0, 2, 3, 1).contiguous(), x2=b)
+    ref = F.conv2d(torch.cat([a, b], 1).float(), w.float(), bias.float(), 1, k // 2)
+    assert ops.stats().get(("conv", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+
+
+def test_unet_skip_concat_never_materialised(cuda):
+    """The decoder ResBlocks consume the skip concat as two tensors (SkipCat): the device forward
+    matches the fp32 CPU forward of the same weights (which concatenates)."""
+    import copy
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    from comfy_gen_server_amd.models.unet import UNetModel
+    cfg = dict(in_channels=4, model_channels=128, out_channels=4, num_res_blocks=[1, 1], channel_mult=[1, 2],
+               transformer_depth=[0, 1], transformer_depth_output=[0, 0, 1, 1], transformer_depth_middle=1,
+               num_heads=-1, num_head_channels=64, use_linear_in_transformer=True, context_dim=128)
+    with torch.inference_mode():
+        m = UNetModel(**cfg, dtype=torch.bfloat16, device=cuda)
+        init_random_fast_(m, seed=4)
+        cpu = copy.deepcopy(m).float().cpu()
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(2, 4, 16, 16, generator=g)
+        t = torch.tensor([700.0, 30.0])
+        c = torch.randn(2, 12, 128, generator=g)
+        yd = m(x.to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last), t.to(cuda),
+               context=c.to(cuda, torch.bfloat16), transformer_options={})
+        yc = cpu(x, t, context=c, transformer_options={})
+    assert _rel(yd.float().cpu(), yc) < 3e-2
