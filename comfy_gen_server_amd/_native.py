@@ -125,6 +125,7 @@ KERNEL_SIGNATURES = {
     "cgs_sampler_step_dev": [_P, _P, _P, _P, _I, _L, _F, _P, _I, _P, _P],
     "cgs_step_param": [_P, _I, _P, _I, _I, _P, _P],
     "cgs_step_advance": [_P, _P],
+    "cgs_vae_out_u8": [_P, _P, _L, _P],                                # bf16 NHWC -> uint8 image (K23)
     "cgs_conv2d_nhwc_ex": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
 }
 

@@ -322,3 +322,37 @@ CGS_EXPORT int cgs_softmax_rows(const void* x, float* y, long long rows, int col
   CGS_DISPATCH_DT(dtype, softmax_rows_kernel, <<<(unsigned)blocks, 256, 0, stream>>>(x, y, rows, cols, scale));
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- K23: VAE output -> uint8 image
+// The decoder's conv_out output (bf16, NHWC with C channels) straight to the uint8 HWC image the
+// server encodes: v = clamp((x + 1) / 2, 0, 1); u8 = (uint8)(v * 255 + 0.5). One pass replaces the
+// fp32 upcast, process_output, the NCHW->NHWC move and the uint8 conversion (sd.py VAE.decode +
+// SaveImage's 255 scaling).
+__global__ void vae_out_u8_kernel(const u16* __restrict__ x, uint8_t* __restrict__ y, long long n) {
+  const long long n8 = n >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
+    uint2 o;
+    uint32_t w[2] = {0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = fminf(fmaxf((bf2f((u16)v[j]) + 1.0f) * 0.5f, 0.0f), 1.0f);
+      w[j >> 2] |= (uint32_t)(f * 255.0f + 0.5f) << (8 * (j & 3));
+    }
+    o.x = w[0];
+    o.y = w[1];
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+  for (long long t = (n8 << 3) + blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n;
+       t += (long long)gridDim.x * blockDim.x) {
+    const float f = fminf(fmaxf((bf2f(x[t]) + 1.0f) * 0.5f, 0.0f), 1.0f);
+    y[t] = (uint8_t)(f * 255.0f + 0.5f);
+  }
+}
+
+CGS_EXPORT int cgs_vae_out_u8(const void* x, void* y, long long n, hipStream_t stream) {
+  long long b = (n / 8 + 255) / 256;
+  const int blocks = (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+  vae_out_u8_kernel<<<blocks, 256, 0, stream>>>((const u16*)x, (uint8_t*)y, n);
+  return (int)hipGetLastError();
+}

@@ -27,6 +27,11 @@ from .attention import BasicTransformerBlock, SpatialTransformer, _Seq
 from .layers import Conv2d, Conv3d, GroupNorm, Linear
 
 
+def _SKIPCAT():
+    import os
+    return os.environ.get("CGS_SKIPCAT", "1") != "0"
+
+
 class SkipCat:
     """``torch.cat([h, skip], 1)`` of the UNet decoder kept as its two halves (K14): the output
     ResBlock's GroupNorm and 1x1 skip conv read the channel concat straight from both tensors, so the
@@ -465,7 +470,7 @@ class UNetModel(nn.Module):
             hsp = _apply_control(hsp, control, "output")
             for p in patches.get("output_block_patch", []):
                 h, hsp = p(h, hsp, to)
-            if x.is_cuda and h.shape[1] % 64 == 0 and hsp.shape[1] % 64 == 0 and h.dtype == hsp.dtype:
+            if x.is_cuda and _SKIPCAT() and h.shape[1] % 64 == 0 and hsp.shape[1] % 64 == 0 and h.dtype == hsp.dtype:
                 h = SkipCat(h, hsp)          # consumed by the block's ResBlock without a concat
             else:
                 h = torch.cat([h, hsp], dim=1)

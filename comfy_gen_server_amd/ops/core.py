@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from .. import _native
 from . import autotune
-from .dispatch import backend_for, count
+from .dispatch import backend_for, count, vendor_fallback
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
@@ -110,12 +110,15 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
                 cands.append(("lib", run_lib))
             choice = autotune.choose(("gemm", M, N, K, epi), cands, default="hip")
         if choice == "lib":
-            count("gemm", "lib")
+            count("gemm", "lib")     # explicit opt-in (CGS_GEMM_LIB=1)
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
         variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N)
-    count("gemm", "torch" if be == "torch" else "lib")
+    if be == "torch":
+        count("gemm", "torch")
+    else:
+        vendor_fallback("gemm", f"dtype {x.dtype}/{weight.dtype}, K={x.shape[-1]}")
     if be == "torch":
         y = F.linear(x.float(), weight.float(), None if bias is None else bias.float())
         if residual is not None:
@@ -276,10 +279,12 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
             return _sdpa(q, k, v, heads, causal)
         count("attention", "hip")
         return run_hip()
-    if q.device.type != "cpu" and mask is None and key_padding is None:
-        count("attention", "lib")
-        return _sdpa(q, k, v, heads, causal)
-    count("attention", "torch" if q.device.type == "cpu" else "lib")
+    if q.device.type != "cpu":
+        vendor_fallback("attention", f"dtype {q.dtype}, head dim {D}, mask={mask is not None}")
+        if mask is None and key_padding is None:
+            return _sdpa(q, k, v, heads, causal)
+    else:
+        count("attention", "torch")
     return attention_reference(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
 
 
@@ -368,7 +373,10 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
         return y
     if x2 is not None:
         x = torch.cat([x, x2], dim=1)
-    count("groupnorm", "torch" if x.device.type == "cpu" else "lib")
+    if x.device.type == "cpu":
+        count("groupnorm", "torch")
+    else:
+        vendor_fallback("groupnorm", f"dtype {x.dtype}, C={Ct}, groups={groups}")
     if pre_add is not None:
         x = x + pre_add.to(x.dtype)[:, :, None, None]
     y = F.group_norm(x.float(), groups, None if weight is None else weight.to(x.device, torch.float32),
@@ -390,7 +398,10 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor 
         _check(_lib().cgs_layernorm(xc.data_ptr(), y.data_ptr(), _ptr(weight), _ptr(bias),
                                     rows, C, float(eps), _DT[x.dtype], _stream()), "cgs_layernorm")
         return y
-    count("layernorm", "torch" if x.device.type == "cpu" else "lib")
+    if x.device.type == "cpu":
+        count("layernorm", "torch")
+    else:
+        vendor_fallback("layernorm", f"dtype {x.dtype}, C={C}")
     return F.layer_norm(x.float(), (C,), None if weight is None else weight.float(),
                         None if bias is None else bias.float(), eps).to(x.dtype)
 
@@ -463,7 +474,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         if residual is not None:
             y = y + residual.float()
         return y.to(x.dtype)
-    count("conv", "lib")
+    vendor_fallback("conv", f"dtype {x.dtype}, groups={groups}, Cin={x.shape[1]}, Cout={Cout}")
     y = F.conv2d(x, weight, bias, stride, padding, groups=groups)
     if residual is not None:
         y = y + residual
@@ -834,3 +845,18 @@ def sampler_step_dev(x: torch.Tensor, cond_den: torch.Tensor, uncond_den: torch.
 
 def step_advance(meta: torch.Tensor):
     _check(_lib().cgs_step_advance(meta.data_ptr(), _stream()), "cgs_step_advance")
+
+
+def vae_out_u8(x: torch.Tensor) -> torch.Tensor:
+    """VAE decoder output [N, C, H, W] (NHWC in memory) -> uint8 [N, H, W, C]:
+    (clamp((x + 1) / 2, 0, 1) * 255 + 0.5).to(uint8) in one pass on the device (K23)."""
+    be = backend_for("vae_u8", x, "cgs_vae_out_u8")
+    N, C, H, W = x.shape
+    if be == "hip" and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last):
+        count("vae_u8", "hip")
+        y = torch.empty((N, H, W, C), device=x.device, dtype=torch.uint8)
+        _check(_lib().cgs_vae_out_u8(x.data_ptr(), y.data_ptr(), x.numel(), _stream()), "cgs_vae_out_u8")
+        return y
+    count("vae_u8", "torch")
+    v = torch.clamp((x.float() + 1.0) / 2.0, 0.0, 1.0).movedim(1, -1)
+    return (v * 255.0 + 0.5).to(torch.uint8)

@@ -64,6 +64,28 @@ def backend_for(op: str, t: torch.Tensor, kernel: str | None = None) -> str:
     return b
 
 
+class VendorFallbackError(RuntimeError):
+    pass
+
+
+_warned: set = set()
+
+
+def vendor_fallback(op: str, detail: str):
+    """A device call of ``op`` is about to leave the hand-written kernels for a vendor library /
+    ATen (SDPA, MIOpen, hipBLASLt, ...). Loud by design: logs once per (op, reason) and counts
+    ``(op, "lib")``; with ``CGS_STRICT_NATIVE=1`` it raises instead (the GPU test tier and the
+    flagship smoke run also assert zero ``lib`` calls on their paths)."""
+    import logging
+    if os.environ.get("CGS_STRICT_NATIVE", "0") == "1":
+        raise VendorFallbackError(f"{op}: {detail} has no HIP kernel path (CGS_STRICT_NATIVE=1)")
+    key = (op, detail)
+    if key not in _warned:
+        _warned.add(key)
+        logging.warning("vendor fallback: %s (%s) runs through the vendor library, not a HIP kernel", op, detail)
+    count(op, "lib")
+
+
 def count(op: str, backend: str):
     with _stats_lock:
         _stats[(op, backend)] += 1

@@ -86,6 +86,8 @@ def generate_local(patcher, clip, vae, job: Job, index_offset: int, local_batch:
     if not decode:
         return samples
     with _stage("vae"):
+        if decode == "uint8":
+            return vae.decode_uint8(samples)
         return vae.decode(samples)
 
 
@@ -129,13 +131,12 @@ class DataParallelGenerator:
             # degraded (after a rank failure): rank 0 alone serves whole jobs; other survivors idle
             if c.rank != 0:
                 return None
-            return to_uint8(generate_local(self.patcher, self.clip, self.vae, job, 0, job.batch))
+            return generate_local(self.patcher, self.clip, self.vae, job, 0, job.batch, decode="uint8")
         job = c.broadcast_object(job)
         per = job.batch // c.world
         rem = job.batch % c.world
         offset, local = self._shard(job, c.rank)
-        imgs = generate_local(self.patcher, self.clip, self.vae, job, offset, local)
-        u8 = to_uint8(imgs)
+        u8 = generate_local(self.patcher, self.clip, self.vae, job, offset, local, decode="uint8")
         if gather and c.enabled and fault_tolerant:
             c.heartbeat_fault_site()
             rid, dead = c.liveness_round(float(os.environ.get("CGS_DP_LIVENESS_TIMEOUT", "30")))
@@ -171,7 +172,7 @@ class DataParallelGenerator:
         for r in range(1, c.world):
             if r in dead:
                 off, n = self._shard(job, r)
-                parts[r] = to_uint8(generate_local(self.patcher, self.clip, self.vae, job, off, n)).cpu()
+                parts[r] = generate_local(self.patcher, self.clip, self.vae, job, off, n, decode="uint8").cpu()
             else:
                 parts[r] = c.store_get_tensor(f"cgs/shard/{rid}/{r}")
         return torch.cat([parts[r] for r in range(c.world)])

@@ -123,6 +123,21 @@ def configure(**kw):
     _args.update({k: v for k, v in kw.items() if k in _args})
 
 
+def _fp16_on_device(what: str):
+    """fp16 requested for a device model. The hand-written MI355X kernels are bf16 (same MFMA rate,
+    wider exponent); fp16 would route every op through the vendor libraries. So fp16 requests run the
+    bf16 HIP path unless ``CGS_ALLOW_LIB=1`` asks for real fp16 through the libraries."""
+    import os
+    if os.environ.get("CGS_ALLOW_LIB", "0") == "1":
+        return torch.float16
+    key = "_fp16_warned_" + what
+    if not _args.get(key):
+        _args[key] = True
+        logging.warning("%s: fp16 requested; MI355X kernels run bf16 (set CGS_ALLOW_LIB=1 for fp16 through "
+                        "the vendor libraries)", what)
+    return torch.bfloat16
+
+
 def unet_dtype(device=None, model_params=0, supported_dtypes=(torch.bfloat16, torch.float16, torch.float32)):
     device = device or get_torch_device()
     if _args["force_fp32"] or device.type == "cpu":
@@ -132,7 +147,8 @@ def unet_dtype(device=None, model_params=0, supported_dtypes=(torch.bfloat16, to
     if _args["fp8_e5m2_unet"]:
         return torch.float8_e5m2
     if _args["fp16_unet"] and torch.float16 in supported_dtypes:
-        return torch.float16
+        return _fp16_on_device("unet") if device.type == "cuda" and torch.bfloat16 in supported_dtypes \
+            else torch.float16
     if torch.bfloat16 in supported_dtypes:
         return torch.bfloat16
     return torch.float16 if torch.float16 in supported_dtypes else torch.float32
@@ -149,7 +165,7 @@ def text_encoder_dtype(device=None):
     if _args["fp32_text_enc"] or device.type == "cpu":
         return torch.float32
     if _args["fp16_text_enc"]:
-        return torch.float16
+        return _fp16_on_device("text encoder") if device.type == "cuda" else torch.float16
     return torch.bfloat16
 
 
@@ -158,7 +174,7 @@ def vae_dtype(device=None):
     if _args["fp32_vae"] or device.type == "cpu":
         return torch.float32
     if _args["fp16_vae"]:
-        return torch.float16
+        return _fp16_on_device("vae") if device.type == "cuda" else torch.float16
     return torch.bfloat16
 
 

@@ -17,6 +17,8 @@ import math
 
 import torch
 
+from .. import ops
+
 from . import device as dm
 from . import detection, families
 from .checkpoint import load_state_dict, save_state_dict, calculate_parameters, weight_dtype
@@ -213,6 +215,28 @@ class VAE:
         return (self.decode_tiled(samples, tile_x // 2, tile_y * 2, overlap) +
                 self.decode_tiled(samples, tile_x * 2, tile_y // 2, overlap) +
                 self.decode_tiled(samples, tile_x, tile_y, overlap)) / 3.0
+
+    def decode_uint8(self, samples_in):
+        """Decode straight to the uint8 [B, H, W, 3] image (server / DP gather format): the conv_out
+        output goes through one fused kernel (K23) instead of fp32 upcast + scaling + uint8 passes."""
+        if self.kind != "kl" or self.device.type != "cuda" or self.vae_dtype != torch.bfloat16:
+            px = self.decode(samples_in)
+            return (px.clamp(0, 1) * 255.0 + 0.5).to(torch.uint8)
+        try:
+            from ..utils.telemetry import maybe_fault
+            maybe_fault("vae", "vae_decode")
+            dm.load_model_gpu(self.patcher)
+            out = []
+            with torch.inference_mode():
+                for i in range(0, samples_in.shape[0], self.batch):
+                    img = self.first_stage_model.decode(self._mf(samples_in[i:i + self.batch]))
+                    out.append(ops.vae_out_u8(img.contiguous(memory_format=torch.channels_last)))
+            return torch.cat(out, 0)
+        except torch.cuda.OutOfMemoryError:
+            logging.warning("Ran out of memory in regular VAE decoding; retrying with tiled VAE decoding.")
+            dm.soft_empty_cache(force=True)
+            px = self.decode_tiled_(samples_in)
+            return (px.clamp(0, 1) * 255.0 + 0.5).to(torch.uint8)
 
     def _decode_full(self, samples_in):
         dm.load_model_gpu(self.patcher)

@@ -148,3 +148,15 @@ def test_attention_probs_cpu():
     q, k, v = (torch.randn(1, 16, 2 * 8) for _ in range(3))
     o, p = ops.attention_with_probs(q, k, v, 2)
     assert p.shape == (2, 16, 16) and torch.allclose(p.sum(-1), torch.ones(2, 16))
+
+
+def test_vae_out_u8_matches_reference(cuda):
+    """K23: the fused bf16 NHWC -> uint8 HWC kernel equals clamp((x+1)/2)*255+0.5 -> uint8."""
+    from comfy_gen_server_amd import ops
+    torch.manual_seed(0)
+    x = (torch.randn(2, 3, 37, 53, device=cuda) * 1.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ops.reset_stats()
+    y = ops.vae_out_u8(x)
+    ref = (torch.clamp((x.float() + 1.0) / 2.0, 0.0, 1.0).movedim(1, -1) * 255.0 + 0.5).to(torch.uint8)
+    assert ops.stats().get(("vae_u8", "hip"), 0) == 1
+    assert y.shape == (2, 37, 53, 3) and torch.equal(y, ref)
