@@ -150,6 +150,7 @@ def test_attention_probs_cpu():
     assert p.shape == (2, 16, 16) and torch.allclose(p.sum(-1), torch.ones(2, 16))
 
 
+@pytest.mark.gpu
 def test_vae_out_u8_matches_reference(cuda):
     """K23: the fused bf16 NHWC -> uint8 HWC kernel equals clamp((x+1)/2)*255+0.5 -> uint8."""
     from comfy_gen_server_amd import ops
