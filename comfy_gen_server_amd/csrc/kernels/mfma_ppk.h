@@ -246,7 +246,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
                 v0 += rv.x; v1 += rv.y; v2 += rv.z; v3 += rv.w;
               }
               const int col = ncw + nq * 32 + 16 * j + 4 * fq;
-              if (row < M && col < N)
+              // EXPERIMENT flag 64: store only one quadrant (timing probe of the store-drain cost)
+              if (row < M && col < N && (!(e.flags & 64) || (mq == 0 && nq == 0)))
                 *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pack4_bf16(v0, v1, v2, v3);
             }
         }
@@ -265,6 +266,10 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     }
   };
 
+  // EXPERIMENT flag 128: odd workgroups start ~half a tile later (store-burst desync probe)
+  if ((e.flags & 128) && (blockIdx.x & 1)) {
+    for (int t = 0; t < nk * 3000 / 8128 / 2 + 1; ++t) __builtin_amdgcn_s_sleep(127);
+  }
   // ---- prologue: A0 B0 B1 A1 of K-tile 0, A0 B0 B1 of K-tile 1 -> wait for A0(0), B0(0)
   int l = l0, m0, n0;
   coords(l, m0, n0);

@@ -97,8 +97,24 @@ class ControlBase:
     def _outside_window(self, t):
         if self.timestep_range is None:
             return False
-        s = float(t[0])
-        return s > self.timestep_range[0] or s < self.timestep_range[1]
+        from ..sampling.samplers import current_sigma
+        s = current_sigma.get()           # host copy published by the sampler: no D2H sync per step
+        s = float(t[0]) if s is None else s
+        return self.outside_window_at(s)
+
+    def outside_window_at(self, sigma: float) -> bool:
+        if self.timestep_range is None:
+            return False
+        return sigma > self.timestep_range[0] or sigma < self.timestep_range[1]
+
+    def prepare_hint(self, x_noisy, batched_number):
+        """The per-job hint tensor get_control() would build (resized, cast, batch-broadcast),
+        built eagerly so a captured step graph can take it as a static input."""
+        dtype = getattr(self, "manual_cast_dtype", None) or self.control_model.dtype
+        self._hint_for(x_noisy, dtype)
+        if x_noisy.shape[0] != self.cond_hint.shape[0]:
+            self.cond_hint = broadcast_image_to(self.cond_hint, x_noisy.shape[0], batched_number)
+        return self.cond_hint
 
     def control_merge(self, control_input, control_output, control_prev, output_dtype):
         out = {"input": [], "middle": [], "output": []}

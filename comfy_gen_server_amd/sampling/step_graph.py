@@ -16,10 +16,16 @@ for every step of every job with that plan:
 A job then costs: copy x and the conditioning into the plan's static buffers, one 16-B-per-step
 parameter upload, and ``steps`` graph launches — no per-step Python op dispatch, no host gaps.
 
+ControlNet (``comfy/controlnet.py:152``, chains included) runs inside the same captured step: its
+timestep window is evaluated on the host per step (one graph per distinct on/off pattern of the
+chain, usually one), the strength is part of the plan key, and the prepared hint is a static input
+refreshed per job.
+
 Eligible (else the eager loop runs): device tensors, Euler / Euler-a (no churn), a seed and
 contiguous global image indices, a plain ``CFGGuider`` with one full-frame cond and uncond entry
-(no areas / masks / gligen / timestep ranges / ControlNet), no denoise mask, no sampler cfg hooks or
-model wrappers, no transformer patches. ``CGS_GRAPHS=0`` disables it.
+sharing one ControlNet chain (or none) — no areas / masks / gligen / timestep ranges / T2I adapters,
+no denoise mask, no sampler cfg hooks or model wrappers, no transformer patches. ``CGS_GRAPHS=0``
+disables it.
 """
 from __future__ import annotations
 
@@ -38,7 +44,7 @@ stats = {"capture": 0, "replay": 0, "jobs": 0}
 
 
 class _Plan:
-    __slots__ = ("graph", "x", "params", "meta", "sig", "den", "cond", "pool")
+    __slots__ = ("graphs", "x", "params", "meta", "sig", "den", "cond", "hints", "pool")
 
 
 def _ancestral(s0, s1, eta):
@@ -73,9 +79,25 @@ def _eligible(mk, x, extra_args):
     lists = [pos, neg] if use_uncond else [pos]
     if any(cl is None or len(cl) != 1 for cl in lists) or not _simple_conds(lists):
         return None
-    if any(cl[0].get("control") is not None or cl[0].get("gligen") is not None for cl in lists):
+    if any(cl[0].get("gligen") is not None for cl in lists):
         return None
-    return guider, lists, use_uncond, index0, mo
+    ctrls = [cl[0].get("control") for cl in lists]
+    ctrl = ctrls[0]
+    if any(c is not ctrl for c in ctrls):       # cond and uncond must share the control (one batch)
+        return None
+    if ctrl is not None:
+        from ..runtime.controlnet import ControlNet
+        if any(type(cn) is not ControlNet and not issubclass(type(cn), ControlNet) for cn in _chain(ctrl)):
+            return None                          # T2I adapters / others: eager
+    return guider, lists, use_uncond, index0, mo, ctrl
+
+
+def _chain(ctrl):
+    out = []
+    while ctrl is not None:
+        out.append(ctrl)
+        ctrl = ctrl.previous_controlnet
+    return out
 
 
 def _conditioning(guider, lists, x, sigma0):
@@ -92,7 +114,7 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     el = _eligible(mk, x, extra_args)
     if el is None:
         return None
-    guider, lists, use_uncond, index0, mo = el
+    guider, lists, use_uncond, index0, mo, ctrl = el
     s = [float(v) for v in sigmas.detach().cpu()]
     n = len(s) - 1
     if n < 1 or n > CAPACITY:
@@ -101,19 +123,35 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     if cond is None or any(not isinstance(v, torch.Tensor) or not v.is_cuda for v in cond.values()):
         return None
     model = guider.inner_model
+    chain = _chain(ctrl)
+    batched = 2 if use_uncond else 1
+    # ControlNet: the per-step on/off window is decided on the HOST (one captured graph per distinct
+    # on/off pattern of the chain), the hint is a static input, strength is part of the plan key
+    patterns = [tuple(not cn.outside_window_at(s[i]) for cn in chain) for i in range(n)]
+    hints = []
+    if chain:
+        xin = torch.empty((x.shape[0] * batched,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        hints = [cn.prepare_hint(xin, batched) for cn in chain]
     from ..models import layers
     key = (layers.WEIGHTS_EPOCH, tuple(x.shape), use_uncond, float(guider.cfg),
-           tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in cond.items())))
+           tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in cond.items())),
+           tuple((id(cn.control_model), float(cn.strength), bool(cn.global_average_pooling), tuple(h.shape), h.dtype)
+                 for cn, h in zip(chain, hints)))
     plans = model.__dict__.setdefault("_step_graph_plans", {})
     plan = plans.get(key)
     if plan is None:
-        plan = _capture(model, x, cond, use_uncond, float(guider.cfg), mo)
-        if plan is None:
-            return None
+        plan = _new_plan(x, cond, hints)
         with _lock:
             for k in [k for k in plans if k[0] != layers.WEIGHTS_EPOCH]:
                 del plans[k]
             plans[key] = plan
+    for pat in sorted(set(patterns)):
+        if pat not in plan.graphs:
+            rep = s[patterns.index(pat)]
+            g = _capture(plan, model, chain, pat, rep, use_uncond, float(guider.cfg), mo)
+            if g is None:
+                return None
+            plan.graphs[pat] = g
     # per-job inputs
     rows = []
     for i in range(n):
@@ -129,16 +167,19 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     plan.x.copy_(x)
     for k, v in cond.items():
         plan.cond[k].copy_(v)
+    for dst, src in zip(plan.hints, hints):
+        if dst is not src:
+            dst.copy_(src)
     stats["jobs"] += 1
     for i in range(n):
-        plan.graph.replay()
+        plan.graphs[patterns[i]].replay()
         stats["replay"] += 1
         if callback is not None:
             callback({"x": plan.x.clone(), "i": i, "sigma": s[i], "sigma_hat": s[i], "denoised": plan.den.clone()})
     return plan.x.clone()
 
 
-def _capture(model, x, cond, use_uncond, cfg, mo):
+def _new_plan(x, cond, hints):
     p = _Plan()
     dev = x.device
     p.x = x.detach().clone()
@@ -148,8 +189,20 @@ def _capture(model, x, cond, use_uncond, cfg, mo):
     p.sig = torch.empty(x.shape[0], device=dev, dtype=torch.float32)
     p.den = torch.empty_like(p.x)
     p.cond = {k: v.detach().clone() for k, v in cond.items()}
+    p.hints = list(hints)           # the first job's prepared hint tensors become the static inputs
+    p.graphs = {}
+    p.pool = None
+    return p
+
+
+def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
+    """Capture the step body for one ControlNet on/off pattern (``rep_sigma``: a step's sigma with
+    that pattern, published as the host sigma while the body records)."""
+    from .samplers import current_sigma
     to = dict(mo.get("transformer_options", {}))
     to["cond_or_uncond"] = [0, 1] if use_uncond else [0]
+    for cn, h in zip(chain, p.hints):
+        cn.cond_hint = h            # get_control() then reads the plan's static hint
 
     def body():
         ops.step_param(p.sig, p.params, p.meta, 0)
@@ -159,7 +212,10 @@ def _capture(model, x, cond, use_uncond, cfg, mo):
             xin, tin = p.x, p.sig
         t = dict(to)
         t["sigmas"] = p.sig
-        out = model.apply_model(xin, tin, transformer_options=t, **p.cond)
+        control = None
+        if chain:
+            control = chain[0].get_control(xin, tin, p.cond, 2 if use_uncond else 1)
+        out = model.apply_model(xin, tin, control=control, transformer_options=t, **p.cond)
         if use_uncond:
             oc, ou = out.chunk(2)
             ops.sampler_step_dev(p.x, oc.contiguous(), ou.contiguous(), p.den, cfg, p.params, p.meta)
@@ -168,6 +224,8 @@ def _capture(model, x, cond, use_uncond, cfg, mo):
         ops.step_advance(p.meta)
 
     g = torch.cuda.CUDAGraph()
+    tok = current_sigma.set(float(rep_sigma))
+    saved_x, saved_meta = p.x.clone(), p.meta.clone()
     try:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -175,7 +233,8 @@ def _capture(model, x, cond, use_uncond, cfg, mo):
             body()                      # warm-up: autotune keys, derived weight layouts, lazy attrs
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        p.pool = torch.cuda.graph_pool_handle()
+        if p.pool is None:
+            p.pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=p.pool, stream=side):
             body()
         torch.cuda.synchronize()
@@ -186,6 +245,9 @@ def _capture(model, x, cond, use_uncond, cfg, mo):
         except Exception:
             pass
         return None
-    p.graph = g
+    finally:
+        current_sigma.reset(tok)
+        p.x.copy_(saved_x)
+        p.meta.copy_(saved_meta)
     stats["capture"] += 1
-    return p
+    return g

@@ -12,6 +12,15 @@ import torch
 SHAPES = [(16384, 3840, 1280), (16384, 1280, 5120), (65536, 1920, 640), (4096, 4096, 4096), (8192, 8192, 8192)]
 VARIANTS = [5, 6, 7]
 GROUPS = [1, 4, 8, 16]
+EPI = 0
+if "--quarter-stores" in sys.argv:   # v7 timing probe: epilogue stores 1/4 of the tile (flag 64)
+    EPI = 64
+if "--stagger" in sys.argv:          # v7 probe: odd workgroups start half a tile late (flag 128)
+    EPI |= 128
+if "--kseries" in sys.argv:        # per-tile fixed cost vs per-K-tile cost: 1024 tiles (4 rounds), K swept
+    SHAPES = [(16384, 4096, k) for k in (128, 256, 640, 1280, 2560, 5120)] + [(16384, 10240, 1280), (65536, 4096, 640)]
+    VARIANTS = [5, 7]
+    GROUPS = [8]
 
 
 def main(argv):
@@ -31,7 +40,7 @@ def main(argv):
                 for g in GROUPS:
                     lib.cgs_set_tile_group(g)
                     fn = lambda: lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K,  # noqa
-                                                     K, K, N, 0, 0, 1.0, v, core._stream())
+                                                     K, K, N, 0, EPI, 1.0, v, core._stream())
                     fn()
                     torch.cuda.synchronize()
                     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,6 +58,7 @@ def main(argv):
             print(rows[-1], flush=True)
         del a, w, out
     text = "\n".join(rows)
+    argv = [a for a in argv if not a.startswith("--")]
     if argv:
         open(argv[0], "w").write(text + "\n")
     print(text)

@@ -112,3 +112,50 @@ def test_step_graph_only_serves_euler_family(cuda, monkeypatch, sampler):
         generate_local(patcher, clip, vae, Job(batch=2, steps=3, sampler=sampler, width=64, height=64, seed=1), 0, 2,
                        decode=False)
     assert step_graph.stats["jobs"] == jobs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [(0.0, 1.0), (0.0, 0.5)])
+def test_step_graph_with_controlnet_matches_eager(cuda, monkeypatch, window):
+    """ControlNet inside the captured step (K15 path of the step graph): residual injection, strength
+    and a host-evaluated timestep window (two on/off patterns -> two graphs) reproduce the eager loop,
+    for two jobs with different hints through one plan."""
+    import copy
+    from comfy_gen_server_amd.graph import registry
+    from comfy_gen_server_amd.models.cldm import ControlNet as CN
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    from comfy_gen_server_amd.parallel.dp import encode_prompt
+    from comfy_gen_server_amd.runtime import controlnet as rcn
+    from comfy_gen_server_amd.sampling import sample as S, step_graph
+    from comfy_gen_server_amd.tools.synth import TINY_UNET, build_pipeline
+    registry.init_nodes(custom_nodes=False)
+    NM = registry.NODE_CLASS_MAPPINGS
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        cfg = copy.deepcopy(TINY_UNET)
+        cfg.update(num_heads=2, num_head_channels=-1)
+        cm = CN(hint_channels=3, dtype=torch.bfloat16, device=cuda, **cfg)
+        init_random_fast_(cm, seed=7)
+        pos = encode_prompt(clip, "a house", 64, 64)
+        neg = encode_prompt(clip, "blurry", 64, 64)
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_GRAPHS", mode)
+            outs = []
+            for j in range(2):
+                g = torch.Generator().manual_seed(j)
+                hint = torch.rand(1, 64, 64, 3, generator=g)
+                cnet = rcn.ControlNet(cm, load_device=cuda)
+                pc, nc = NM["ControlNetApplyAdvanced"]().apply_controlnet(pos, neg, cnet, hint, 0.8, window[0],
+                                                                          window[1])
+                latent = torch.zeros([2, 4, 8, 8])
+                noise = S.prepare_noise(latent, 5 + j)
+                outs.append(S.sample(patcher, noise, 6, 5.0, "euler_ancestral", "normal", pc, nc, latent,
+                                     seed=5 + j).float())
+            res[mode] = outs
+        torch.cuda.synchronize()
+    assert step_graph.stats["replay"] >= 12
+    for a, b in zip(res["0"], res["1"]):
+        err = (a - b).abs().max().item()
+        assert err < 2e-2 * (a.abs().max().item() + 1), err
+    assert (res["1"][0] - res["1"][1]).abs().max() > 1e-3     # different hints -> different images
