@@ -15,6 +15,8 @@ GROUPS = [1, 4, 8, 16]
 EPI = 0
 if "--quarter-stores" in sys.argv:   # v7 timing probe: epilogue stores 1/4 of the tile (flag 64)
     EPI = 64
+if "--nowait" in sys.argv:           # v7 probe: DMA waits ignore epilogue stores for 3 K-tiles (flag 256)
+    EPI |= 256
 if "--stagger" in sys.argv:          # v7 probe: odd workgroups start half a tile late (flag 128)
     EPI |= 128
 if "--kseries" in sys.argv:        # per-tile fixed cost vs per-K-tile cost: 1024 tiles (4 rounds), K swept

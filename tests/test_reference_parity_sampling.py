@@ -306,3 +306,90 @@ def test_lora_lycoris_patches_and_key_maps_match_reference(tmp_path):
     merged exactly like comfy/lora.py:14-166 + comfy/model_patcher.py:316-452; UNet (ldm + diffusers
     names) and CLIP-L/G key maps equal to comfy/lora.py:169-241 on the SDXL architecture."""
     assert "lora ok" in _run(_LORA, tmp_path)
+
+
+_DETECT = r'''
+import copy
+import comfy.model_detection as RD, comfy.supported_models as RSM
+from comfy_gen_server_amd.runtime import detection as OD
+from comfy_gen_server_amd.models.unet import UNetModel
+from comfy_gen_server_amd.tools import synth
+TEMPORAL = dict(use_temporal_resblock=True, use_temporal_attention=True, extra_ff_mix_layer=True,
+                use_spatial_context=True, merge_strategy="learned_with_images", merge_factor=0.0,
+                video_kernel_size=[3, 1, 1], channel_mult=[1, 2, 4, 4], num_res_blocks=[2, 2, 2, 2],
+                num_head_channels=64, num_heads=-1, num_classes="sequential",
+                transformer_depth_output=[1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0])
+BASES = {"SD15": synth.SD15_UNET, "SD20": synth.SD21_UNET, "SDXL": synth.SDXL_UNET,
+         "SDXLRefiner": synth.SDXL_REFINER_UNET}
+def full_config(F):
+    names = [c.__name__ for c in F.__mro__]
+    base = next((BASES[n] for n in names if n in BASES), synth.SD15_UNET)
+    cfg = copy.deepcopy(base)
+    cfg.update(num_heads=-1, num_head_channels=64)
+    part = {k: v for k, v in F.unet_config.items()}
+    cfg.update(part)
+    cfg.update(F.unet_extra_config)
+    if cfg.get("adm_in_channels") and cfg.get("num_classes") is None:
+        cfg["num_classes"] = "sequential"
+    if cfg.get("use_temporal_resblock"):
+        for k, v in TEMPORAL.items():
+            cfg.setdefault(k, v) if k in part else cfg.__setitem__(k, v)
+    td = cfg["transformer_depth"]
+    nrb = cfg.get("num_res_blocks", [2] * len(cfg["channel_mult"]))
+    if isinstance(nrb, int):
+        nrb = [nrb] * len(cfg["channel_mult"])
+    levels = len(td) // nrb[0] if len(td) % nrb[0] == 0 else len(cfg["channel_mult"])
+    if len(td) != sum(nrb):       # KOALA-style shorter lists -> one res block per level
+        cfg["num_res_blocks"] = [1] * len(td)
+        cfg["channel_mult"] = cfg["channel_mult"][:len(td)]
+        nrb = cfg["num_res_blocks"]
+    if "transformer_depth_output" not in part:
+        out = []
+        for lvl in range(len(cfg["channel_mult"])):
+            d = td[sum(nrb[:lvl])] if sum(nrb[:lvl]) < len(td) else 0
+            out += [d] * (nrb[lvl] + 1)
+        cfg["transformer_depth_output"] = out
+    cfg["transformer_depth_middle"] = cfg.get("transformer_depth_middle", max(td))
+    if cfg.get("num_classes") == 1000:
+        cfg["num_classes"] = 1000
+    cfg.pop("image_size", None)
+    cfg.pop("use_checkpoint", None)
+    return cfg
+ok, skipped = [], []
+for F in RSM.models:
+    if F.__name__.startswith("Stable_Cascade"):
+        continue
+    cfg = full_config(F)
+    try:
+        with torch.device("meta"):
+            net = UNetModel(**cfg, dtype=torch.float16, device=torch.device("meta"))
+    except Exception as e:
+        skipped.append((F.__name__, repr(e)[:120]))
+        continue
+    sd = {"model.diffusion_model." + k: v for k, v in net.state_dict().items()}
+    if F.__name__ == "Stable_Zero123":
+        sd["cc_projection.weight"] = torch.empty(768, 772, device="meta")
+        sd["cc_projection.bias"] = torch.empty(768, device="meta")
+    r = RD.model_config_from_unet(sd, "model.diffusion_model.")
+    o = OD.model_config_from_unet(sd, "model.diffusion_model.")
+    rn = type(r).__name__ if r is not None else None
+    on = type(o).__name__ if o is not None else None
+    assert rn == on, (F.__name__, rn, on)
+    if r is not None:
+        for k, v in r.unet_config.items():
+            if k in o.unet_config:
+                ov = o.unet_config[k]
+                assert ov == v or (isinstance(v, (list, tuple)) and list(ov) == list(v)), (F.__name__, k, v, ov)
+    ok.append((F.__name__, rn))
+print("detect ok", ok, "skipped", skipped)
+assert len(ok) >= 14, (ok, skipped)
+'''
+
+
+def test_architecture_detection_matches_reference(tmp_path):
+    """``model_config_from_unet`` on meta-tensor state dicts of every UNet family of the reference's
+    registry (comfy/model_detection.py:32-183, supported_models.py:479-481): the same family class is
+    picked in the same registry order and the detected unet_config agrees key by key. (Stable Cascade
+    B/C use their own stage models: tests/test_cascade.py.)"""
+    out = _run(_DETECT, tmp_path)
+    assert "detect ok" in out, out
