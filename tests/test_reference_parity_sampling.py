@@ -393,3 +393,78 @@ def test_architecture_detection_matches_reference(tmp_path):
     B/C use their own stage models: tests/test_cascade.py.)"""
     out = _run(_DETECT, tmp_path)
     assert "detect ok" in out, out
+
+
+_CASCADE_CN = r'''
+import copy
+import comfy.ops
+from comfy.ldm.cascade.stage_c import StageC as RC
+from comfy.ldm.cascade.stage_b import StageB as RB
+from comfy.ldm.cascade.stage_a import StageA as RA
+from comfy.cldm.cldm import ControlNet as RCN
+from comfy_gen_server_amd.models import cascade as SC
+from comfy_gen_server_amd.models.cldm import ControlNet as OCN
+from comfy_gen_server_amd.models.layers import init_random_
+from comfy_gen_server_amd.tools.synth import TINY_UNET
+ops_ = comfy.ops.disable_weight_init
+
+def load_same(ours, ref):
+    sd = ours.state_dict()
+    m, u = ref.load_state_dict(sd, strict=False)
+    bufs = {n for n, _ in ref.named_buffers()}
+    assert not [k for k in m if k not in bufs] and not u, (m[:5], u[:5])
+
+# Stage C (prior) with ControlNet-style residuals
+cc = dict(c_in=16, c_out=16, c_r=16, c_cond=32, c_hidden=[32, 32], nhead=[2, 2], blocks=[[1, 1], [1, 1]],
+          block_repeat=[[1, 1], [2, 1]], level_config=["CTA", "CTA"], c_clip_text=24, c_clip_text_pooled=24,
+          c_clip_img=768, c_clip_seq=2, switch_level=[False])
+oc = SC.StageC(**cc); init_random_(oc, seed=7)
+rc = RC(**cc, operations=ops_); load_same(oc, rc)
+g = torch.Generator().manual_seed(0)
+x = torch.randn(2, 16, 6, 6, generator=g); r = torch.tensor([0.3, 0.7])
+ct, ctp, ci = torch.randn(2, 7, 24, generator=g), torch.randn(2, 1, 24, generator=g), torch.randn(2, 1, 768, generator=g)
+with torch.no_grad():
+    print("stage_c", close(oc(x, r, ct, ctp, ci), rc(x, r, ct, ctp, ci), 2e-4))
+# Stage B (decoder)
+bc = dict(c_in=4, c_out=4, c_r=16, patch_size=2, c_cond=32, c_hidden=[16, 24, 32], nhead=[-1, 2, 2],
+          blocks=[[1, 1, 1], [1, 1, 1]], block_repeat=[[1, 1, 1], [2, 1, 1]], level_config=["CT", "CTA", "CTA"],
+          c_clip=24, c_clip_seq=2, c_effnet=16)
+ob = SC.StageB(**bc); init_random_(ob, seed=8)
+rb = RB(**bc, operations=ops_); load_same(ob, rb)
+xb = torch.randn(2, 4, 16, 16, generator=g); eff = torch.randn(2, 16, 3, 3, generator=g)
+clip = torch.randn(2, 1, 24, generator=g)
+with torch.no_grad():
+    print("stage_b", close(ob(xb, torch.tensor([0.5, 0.25]), eff, clip), rb(xb, torch.tensor([0.5, 0.25]), eff, clip), 2e-4))
+# Stage A (VQGAN): encode (no quantize) and decode
+oa = SC.StageA(levels=2, bottleneck_blocks=2, c_hidden=32, c_latent=4, codebook_size=64); init_random_(oa, seed=9)
+oa.eval()
+ra = RA(levels=2, bottleneck_blocks=2, c_hidden=32, c_latent=4, codebook_size=64); load_same(oa, ra); ra.eval()
+img = torch.rand(1, 3, 32, 32, generator=g)
+with torch.no_grad():
+    ea, eb = oa.encode(img), ra.encode(img)
+    ea, eb = (ea[0] if isinstance(ea, tuple) else ea), (eb[0] if isinstance(eb, tuple) else eb)
+    print("stage_a enc", close(ea, eb, 2e-4))
+    print("stage_a dec", close(oa.decode(eb), ra.decode(eb), 2e-4))
+# cldm ControlNet (SD-style, tiny): per-block residual outputs
+cfg = copy.deepcopy(TINY_UNET)
+cfg.update(num_heads=2, num_head_channels=-1)
+ocn = OCN(hint_channels=3, **cfg); init_random_(ocn, seed=3)
+rcfg = dict(cfg); rcfg.pop("out_channels", None)
+rcn = RCN(hint_channels=3, operations=ops_, **rcfg); load_same(ocn, rcn)
+xh = torch.randn(2, 4, 8, 8, generator=g); hint = torch.rand(2, 3, 64, 64, generator=g)
+ts = torch.tensor([500.0, 20.0]); ctx = torch.randn(2, 9, 64, generator=g)
+with torch.no_grad():
+    a = ocn(x=xh, hint=hint, timesteps=ts, context=ctx)
+    b = rcn(x=xh, hint=hint, timesteps=ts, context=ctx)
+assert len(a) == len(b), (len(a), len(b))
+for i, (u, v) in enumerate(zip(a, b)):
+    close(u, v, 2e-4, ("controlnet out", i))
+print("cascade/controlnet ok")
+'''
+
+
+def test_stage_c_b_and_controlnet_match_reference_modules(tmp_path):
+    """Stable Cascade Stage C / Stage B / Stage A and the cldm ControlNet, loaded with the same random weights
+    into this engine's modules and the reference's (comfy/ldm/cascade/stage_{c,b,a}.py,
+    comfy/cldm/cldm.py:285-311), give the same outputs (fp32, CPU)."""
+    assert "cascade/controlnet ok" in _run(_CASCADE_CN, tmp_path)
