@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--cfg", type=float, default=8.0)
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (use with --family tiny)")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the denoiser")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="prompt-level multi-stream overlap: job n's VAE decode on a side stream (dp.run_many)")
     ap.add_argument("--profile-ops", action="store_true", help="(kept for compatibility; op backends are always reported)")
     args = ap.parse_args()
 
@@ -102,8 +104,14 @@ def main():
     comm.barrier()
     ops.reset_stats()
     t1 = time.perf_counter()
-    for i in range(args.steps):
-        out = one_step(args.warmup + i)
+    if args.pipeline:
+        jobs = (Job(**{**job.__dict__, "seed": 1000 + args.warmup + i}) for i in range(args.steps))
+        with torch.inference_mode():
+            for i, out in enumerate(gen.run_many(jobs, pipeline=True)):
+                log(f"job {args.warmup + i} done (pipelined)")
+    else:
+        for i in range(args.steps):
+            out = one_step(args.warmup + i)
     if not args.cpu:
         torch.cuda.synchronize()
     comm.barrier()
@@ -138,7 +146,7 @@ def main():
                        "global_batch": global_batch, "seq_len": (args.res // 8) ** 2,
                        "resolution": args.res, "sampler_steps": args.sampler_steps, "sampler": args.sampler,
                        "cfg": args.cfg, "unet_batch_per_gpu": 2 * args.batch_per_gpu,
-                       "parallelism": f"dp{N}"},
+                       "parallelism": f"dp{N}", "pipelined": bool(args.pipeline)},
             "build_s": round(t_build, 1),
         }
         from comfy_gen_server_amd.parallel import dp as _dp

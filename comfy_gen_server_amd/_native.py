@@ -127,10 +127,14 @@ KERNEL_SIGNATURES = {
     "cgs_step_advance": [_P, _P],
     "cgs_vae_out_u8": [_P, _P, _L, _P],                                # bf16 NHWC -> uint8 image (K23)
     "cgs_conv2d_nhwc_ex": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    # v7 split-K tail: workspace bytes for (M, N, K) and the GEMM / conv launchers that take it
+    "cgs_v7_ws_bytes": [_I, _I, _I],
+    "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
+    "cgs_conv2d_nhwc_v7ws": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P],
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_gemm_set_variant": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
             "cgs_attn_set_variant": None}
 

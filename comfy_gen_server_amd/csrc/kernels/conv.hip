@@ -39,7 +39,17 @@ struct ConvArgs {
   int flags;
   int tiles_n;
   int group_m;
+  unsigned cq_magic;   // ceil(2^32 / (Cin / 64)), 0 when Cin == 64 (ConvGatherK tap decode)
+  int kw_m16;          // ceil(65536 / kw)
+  ppk::Split sp;       // v7 split-K tail (S <= 1: none)
 };
+
+// Host: the multiply-shift constants of ConvGatherK (exact for k0 < kh*kw*Cin, kh*kw <= 32).
+static void conv_magic(ConvArgs& a) {
+  const unsigned cq = (unsigned)(a.Cin / 64);
+  a.cq_magic = cq <= 1 ? 0u : (unsigned)(((1ull << 32) + cq - 1) / cq);
+  a.kw_m16 = (65536 + a.kw - 1) / a.kw;
+}
 
 template <int BN>
 __global__ __launch_bounds__(512, 1) void conv_nhwc_v2_kernel(ConvArgs a) {
@@ -281,7 +291,126 @@ struct ConvGatherA8 {
     const int cb = second ? ci0 - a->C1 : ci0;
     return (const void*)(t + (((long long)pn[s] * a->H + iy) * a->W + ix) * cs + cb + choff[s & 1]);
   }
+  __device__ __forceinline__ void dma(int s, int k0, unsigned char* dst) const { mc::lds_dma16(src(s, k0), dst); }
 };
+
+// Leaner gather for the v5/v7 main loops (no CONV_UP2X, kh*kw <= 32): per slot the lane keeps the
+// pixel index of its output's top-left tap and a bit mask of in-bounds taps (built once per tile);
+// per K-tile the uniform (tap, channel) decode is two multiply-shifts instead of two integer
+// divisions, and the lane address is one 64-bit multiply-add -- the loader runs in the same waves
+// as the MFMAs, so its VALU/SALU cost comes straight out of the matrix-core issue budget.
+template <bool WIDE>   // WIDE: an input is >= 4 GiB (64-bit element offsets); else 32-bit byte offsets
+struct ConvGatherK {
+  const ConvArgs* a;
+  int pix[4];
+  uint32_t vm[4];
+  __device__ __forceinline__ void setup(int s, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    const bool ok = row < M;
+    row = ok ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    const int n = row / hw;
+    const int rem = row - n * hw;
+    const int oy = rem / a->Wo;
+    const int py = oy * a->stride - a->pad, px = (rem - oy * a->Wo) * a->stride - a->pad;
+    pix[s] = (n * a->H + py) * a->W + px;
+    uint32_t m = 0;
+    if (ok) {
+      for (int ky = 0; ky < a->kh; ++ky) {
+        const bool ry = (unsigned)(py + ky) < (unsigned)a->H;
+        for (int kx = 0; kx < a->kw; ++kx)
+          if (ry && (unsigned)(px + kx) < (unsigned)a->W) m |= 1u << (ky * a->kw + kx);
+      }
+    }
+    vm[s] = m;
+  }
+  __device__ __forceinline__ const void* src(int s, int k0) const {
+    const unsigned kq = (unsigned)k0 >> 6;
+    const unsigned tap = a->cq_magic ? __umulhi(kq, a->cq_magic) : kq;
+    const int ci0 = k0 - (int)tap * a->Cin;
+    const int ky = (int)((tap * (unsigned)a->kw_m16) >> 16);
+    const int kx = (int)tap - ky * a->kw;
+    if (!((vm[s] >> tap) & 1u)) return (const void*)(g_conv_zero_page + 16 * (threadIdx.x & 15));
+    const bool second = ci0 >= a->C1;
+    const unsigned char* t = reinterpret_cast<const unsigned char*>(second ? a->in2 : a->in);
+    const int cs = second ? a->Cin - a->C1 : a->C1;
+    const int cb = (second ? ci0 - a->C1 : ci0) + 8 * pp::src_chunk8(s & 1);
+    const unsigned p = (unsigned)(pix[s] + ky * a->W + kx);
+    if constexpr (WIDE) return (const void*)(t + 2 * ((size_t)p * (unsigned)cs + (unsigned)cb));
+    else return (const void*)(t + 2u * (p * (unsigned)cs + (unsigned)cb));
+  }
+};
+
+// v7's gather: the same decode, issued as buffer_load ... lds through one descriptor per input
+// (built from kernel arguments only: wave-uniform). A padding tap gets an out-of-range voffset and
+// the descriptor's range check returns zeros -- no zero page, no 64-bit VGPR address pairs (v7 runs
+// at the 256-VGPR cap). Inputs must each span < 2 GiB.
+struct ConvGatherKB {
+  const ConvArgs* a;
+  int pix[4];
+  uint32_t vm[4];
+  __amdgpu_buffer_rsrc_t r1, r2;
+  __device__ __forceinline__ void init() {
+    const unsigned px = (unsigned)(a->N * a->H * a->W);
+    r1 = __builtin_amdgcn_make_buffer_rsrc((void*)a->in, 0, (int)(px * (unsigned)a->C1 * 2u), 0x00020000);
+    r2 = __builtin_amdgcn_make_buffer_rsrc((void*)(a->in2 ? a->in2 : a->in), 0,
+                                           (int)(px * (unsigned)(a->in2 ? a->Cin - a->C1 : a->C1) * 2u), 0x00020000);
+  }
+  __device__ __forceinline__ void setup(int s, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    const bool ok = row < M;
+    row = ok ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    const int n = row / hw;
+    const int rem = row - n * hw;
+    const int oy = rem / a->Wo;
+    const int py = oy * a->stride - a->pad, px = (rem - oy * a->Wo) * a->stride - a->pad;
+    pix[s] = (n * a->H + py) * a->W + px;
+    uint32_t m = 0;
+    if (ok) {
+      for (int ky = 0; ky < a->kh; ++ky) {
+        const bool ry = (unsigned)(py + ky) < (unsigned)a->H;
+        for (int kx = 0; kx < a->kw; ++kx)
+          if (ry && (unsigned)(px + kx) < (unsigned)a->W) m |= 1u << (ky * a->kw + kx);
+      }
+    }
+    vm[s] = m;
+  }
+  __device__ __forceinline__ void dma(int s, int k0, unsigned char* dst) const {
+    const unsigned kq = (unsigned)k0 >> 6;
+    const unsigned tap = a->cq_magic ? __umulhi(kq, a->cq_magic) : kq;
+    const int ci0 = k0 - (int)tap * a->Cin;
+    const int ky = (int)((tap * (unsigned)a->kw_m16) >> 16);
+    const int kx = (int)tap - ky * a->kw;
+    const bool second = ci0 >= a->C1;
+    const int cs = second ? a->Cin - a->C1 : a->C1;
+    const int cb = (second ? ci0 - a->C1 : ci0) + 8 * pp::src_chunk8(s & 1);
+    const unsigned p = (unsigned)(pix[s] + ky * a->W + kx);
+    const unsigned off = ((vm[s] >> tap) & 1u) ? 2u * (p * (unsigned)cs + (unsigned)cb) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? r2 : r1, (lds_void*)dst, 16, off, 0, 0, 0);
+  }
+};
+
+static bool conv_fast_ok(const ConvArgs& a) { return !(a.flags & CONV_UP2X) && a.kh * a.kw <= 32; }
+// an input tensor spans >= 2 GiB (v7's ConvGatherKB descriptors need < 2 GiB)
+static bool conv_wide(const ConvArgs& a) {
+  const long long px = (long long)a.N * a.H * a.W;
+  return px * a.C1 * 2 >= (1ll << 31) || (a.in2 && px * (a.Cin - a.C1) * 2 >= (1ll << 31));
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v5k_kernel(ConvArgs a) {
+  // (64-bit offsets: v5 keeps VGPR headroom; the VAE's 4-GiB activations take this path)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
+  ConvGatherK<true> al;
+  al.a = &a;
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
+}
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v5_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -305,7 +434,17 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   const int M = a.N * a.Ho * a.Wo;
   a.tiles_n = (a.Cout + pp::BN - 1) / pp::BN;
   const long long nwg = (long long)((M + pp::BM - 1) / pp::BM) * a.tiles_n;
-  conv_nhwc_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+  if (conv_fast_ok(a)) {
+    static bool attr_k = false;
+    if (!attr_k) {
+      (void)hipFuncSetAttribute((const void*)conv_nhwc_v5k_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, pp::LDS);
+      attr_k = true;
+    }
+    conv_magic(a);
+    conv_nhwc_v5k_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+  } else {
+    conv_nhwc_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+  }
 }
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
@@ -342,27 +481,50 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
 }
 
 // v7: the persistent 256 x 256 ping-pong with cross-tile prefetch and register epilogue (mfma_ppk.h)
+template <bool FAST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v7_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  ConvGatherA8 al;
+  typename std::conditional<FAST, ConvGatherKB, ConvGatherA8>::type al;
   al.a = &a;
+  if constexpr (FAST) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
-  ppk::run<false>(al, a.w, K, M, a.Cout, K, e, smem, (M + ppk::BM - 1) / ppk::BM, a.tiles_n, a.group_m);
+  ppk::run<false>(al, a.w, K, M, a.Cout, K, e, smem, (M + ppk::BM - 1) / ppk::BM, a.tiles_n, a.group_m, a.sp);
 }
 
-static void conv_v7_go(ConvArgs& a, hipStream_t stream) {
+static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ppk::LDS);
     attr = true;
   }
   const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
   a.tiles_n = (a.Cout + ppk::BN - 1) / ppk::BN;
   const long long T = (long long)((M + ppk::BM - 1) / ppk::BM) * a.tiles_n;
-  const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
-  conv_nhwc_v7_kernel<<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+  a.sp = ppk::Split{0, 1, nullptr, nullptr};
+  long long U = T;
+  if (ws && ws_bytes >= ppk::split_ws_bytes(T, K / ppk::BK, conv_num_cus())) {
+    a.sp.S = ppk::split_plan(T, K / ppk::BK, conv_num_cus(), a.sp.t_full);
+    if (a.sp.S > 1) {
+      const long long tail = T - a.sp.t_full;
+      a.sp.part = (float4*)ws;
+      a.sp.cnt = (int*)((char*)ws + tail * a.sp.S * 32ll * ppk::THREADS * 16);
+      if (hipMemsetAsync(a.sp.cnt, 0, tail * sizeof(int), stream) != hipSuccess) a.sp.S = 1;
+      else U = a.sp.t_full + tail * a.sp.S;
+    }
+  }
+  const int grid = (int)(U < conv_num_cus() ? U : conv_num_cus());
+  if (conv_fast_ok(a) && !conv_wide(a)) {
+    conv_magic(a);
+    conv_nhwc_v7_kernel<true><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+  } else {
+    conv_nhwc_v7_kernel<false><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+  }
 }
 
 static int g_conv_group = 8;
@@ -370,7 +532,7 @@ CGS_EXPORT void cgs_conv_set_tile_group(int g) { g_conv_group = g < 1 ? 1 : g; }
 static int g_conv_variant = -1;   // -1 auto (v3/8 waves where legal), 2 = v2 only, 3 = v3/4 waves, 4 = v3/8 waves
 CGS_EXPORT void cgs_conv_set_variant(int v) { g_conv_variant = v; }
 
-static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
+static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
   a.group_m = g_conv_group;
   if (variant == 5 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0)) {
     conv_v5_go(a, stream);
@@ -378,7 +540,7 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
   }
   if (variant == 7 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
       ((uintptr_t)a.bias % 8) == 0 && (long long)a.Cout * a.kh * a.kw * a.Cin * 2 < (1ll << 32)) {
-    conv_v7_go(a, stream);
+    conv_v7_go(a, stream, ws, ws_bytes);
     return (int)hipGetLastError();
   }
   if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
@@ -394,11 +556,11 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-static int conv_launch(ConvArgs& a, hipStream_t stream, int variant = -2) {
+static int conv_launch(ConvArgs& a, hipStream_t stream, int variant = -2, void* ws = nullptr, long long ws_bytes = 0) {
   if (variant == -2) variant = g_conv_variant;
   // v3 needs Cout % 8 == 0 for the 16-B epilogue stores (SD/SDXL/VAE convs: all but the 3/4-channel
   // heads, which take v2).
-  if (variant != 2 && a.Cout % 8 == 0) return conv_v3_launch(a, variant, stream);
+  if (variant != 2 && a.Cout % 8 == 0) return conv_v3_launch(a, variant, stream, ws, ws_bytes);
   a.group_m = g_conv_group;
   static bool attr = false;
   if (!attr) {
@@ -452,4 +614,17 @@ CGS_EXPORT int cgs_conv2d_nhwc_v(const void* x, const void* x2, int C1, const vo
              Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
              (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0, 1};
   return conv_launch(a, stream, variant);
+}
+
+// v7 with the split-K tail workspace (>= cgs_v7_ws_bytes(N*Ho*Wo, Cout, kh*kw*Cin) bytes).
+CGS_EXPORT int cgs_conv2d_nhwc_v7ws(const void* x, const void* x2, int C1, const void* w, const void* bias,
+                                    const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
+                                    int stride, int pad, int Ho, int Wo, int flags, void* ws, long long ws_bytes,
+                                    hipStream_t stream) {
+  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && (Cin % 64 || (x2 && C1 % 64))))
+    return (int)hipErrorInvalidValue;
+  ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
+             Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
+             (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0, 1};
+  return conv_launch(a, stream, 7, ws, ws_bytes);
 }

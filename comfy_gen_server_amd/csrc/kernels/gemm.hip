@@ -517,6 +517,7 @@ struct DenseA32 {
     off[slot] = (uint32_t)(((long long)row * lda + 8 * pp::src_chunk8(slot & 1)) * 2);
   }
   __device__ __forceinline__ const void* src(int slot, int k0) const { return A + (off[slot] + (uint32_t)(k0 * 2)); }
+  __device__ __forceinline__ void dma(int slot, int k0, unsigned char* dst) const { mc::lds_dma16(src(slot, k0), dst); }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -525,16 +526,18 @@ template <bool GG>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v7_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_m, int tiles_n, int group_m) {
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m, ppk::Split sp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   DenseA32 al{reinterpret_cast<const unsigned char*>(A), lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
-  ppk::run<GG>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  ppk::run<GG>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m, sp);
 }
 
+// ws (may be null): split-K tail workspace of >= cgs_v7_ws_bytes(M, N, K) bytes; without it the
+// tail round runs whole tiles.
 static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                           long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                          hipStream_t stream) {
+                          void* ws, long long ws_bytes, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -546,16 +549,36 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
   const int tiles_n = (N + ppk::BN - 1) / ppk::BN;
   const int tiles_m = (M + ppk::BM - 1) / ppk::BM;
   const long long T = (long long)tiles_m * tiles_n;
-  const int grid = (int)(T < num_cus() ? T : num_cus());
+  ppk::Split sp{0, 1, nullptr, nullptr};
+  long long U = T;
+  if (ws && ws_bytes >= ppk::split_ws_bytes(T, K / ppk::BK, num_cus())) {
+    sp.S = ppk::split_plan(T, K / ppk::BK, num_cus(), sp.t_full);
+    if (sp.S > 1) {
+      const long long tail = T - sp.t_full;
+      sp.part = (float4*)ws;
+      sp.cnt = (int*)((char*)ws + tail * sp.S * 32ll * ppk::THREADS * 16);
+      hipError_t err = hipMemsetAsync(sp.cnt, 0, tail * sizeof(int), stream);
+      if (err != hipSuccess) return (int)err;
+      U = sp.t_full + tail * sp.S;
+    }
+  }
+  const int grid = (int)(U < num_cus() ? U : num_cus());
   if (epi & EPI_GEGLU)
     gemm_bf16_nt_v7_kernel<true><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
         (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_m, tiles_n, g_tile_group);
+        alpha, tiles_m, tiles_n, g_tile_group, sp);
   else
     gemm_bf16_nt_v7_kernel<false><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
         (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_m, tiles_n, g_tile_group);
+        alpha, tiles_m, tiles_n, g_tile_group, sp);
   return (int)hipGetLastError();
+}
+
+// Split-K tail workspace size of the v7 GEMM / conv for an M x N x K problem (0: no split).
+CGS_EXPORT long long cgs_v7_ws_bytes(int M, int N, int K) {
+  if (K % ppk::BK || K < 2 * ppk::BK) return 0;
+  const long long T = (long long)((M + ppk::BM - 1) / ppk::BM) * ((N + ppk::BN - 1) / ppk::BN);
+  return ppk::split_ws_bytes(T, K / ppk::BK, num_cus());
 }
 
 static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 waves), 4 = v3 (8 waves), 5 = v5 ping-pong
@@ -564,7 +587,7 @@ CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                         int variant, hipStream_t stream) {
+                         int variant, hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
   if (K % 8 || lda % 8 || ldw % 8) return (int)hipErrorInvalidValue;
   if ((epi & EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
@@ -580,7 +603,7 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
     return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&
       ((uintptr_t)bias % 8 == 0) && (long long)M * lda * 2 < (1ll << 32) && (long long)N * ldw * 2 < (1ll << 32))
-    return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
   if (v3_ok && K % 64 == 0 && variant == 5)
     return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && (variant >= 3 || variant == -1)) {
@@ -629,4 +652,11 @@ CGS_EXPORT int cgs_gemm_bf16_v(const void* A, const void* W, void* C, const void
                                int variant, hipStream_t stream) {
   if (variant == -2) variant = g_gemm_variant;   // -2: the process-wide override (default auto)
   return gemm_dispatch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, variant, stream);
+}
+
+// v7 with the split-K tail workspace (ws from the caller's allocator, >= cgs_v7_ws_bytes bytes).
+CGS_EXPORT int cgs_gemm_bf16_v7ws(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                                  int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                                  float alpha, void* ws, long long ws_bytes, hipStream_t stream) {
+  return gemm_dispatch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, 7, stream, ws, ws_bytes);
 }

@@ -6,25 +6,35 @@
 // one-tile-per-workgroup kernel pays, per tile, a cold pipeline fill (~2 us of HBM latency before
 // the first MFMA) and an LDS-staged epilogue during which the MFMA pipes idle -- 15-30 % of the
 // tile. Here:
-//   * the grid is one workgroup per CU; workgroup b walks logical tiles b, b + G, ... (XCD-aware
+//   * the grid is one workgroup per CU; workgroup b walks work units b, b + G, ... (XCD-aware
 //     order, grouped_tile() so XCD-mates share A/W panels in their L2);
-//   * the loaders target the global K-tile sequence: while the last two K-tiles of tile t are
-//     consumed, the parts of tile t+1's first two K-tiles are DMA'd (each loader slot is re-pointed
-//     to the next tile right before its first next-tile stage), so tile t+1 starts with its data
+//   * the loaders target the global K-tile sequence: while the last two K-tiles of unit t are
+//     consumed, the parts of unit t+1's first two K-tiles are DMA'd (each loader slot is re-pointed
+//     to the next unit right before its first next-unit stage), so unit t+1 starts with its data
 //     already in LDS;
 //   * the MFMAs compute C^T (W fragment as the A operand), so a lane's accumulator holds 4
-//     consecutive output COLUMNS of one row -> the epilogue stores 8 B per lane straight from
-//     registers (no LDS round trip: the LDS keeps prefetching), with bias from scalar loads (no
-//     vector load, so no vmcnt drain of the in-flight DMAs), GEGLU pairs in-lane (interleaved
-//     16-row groups: MFMA col tiles 2p / 2p+1 = a / g of the same columns), residual via 8-B loads;
+//     consecutive output COLUMNS of one row; the W rows are staged in a permuted order so that the
+//     lane's two MFMA column tiles hold 8 consecutive columns -> the epilogue writes 16 B per lane
+//     and every store instruction covers 64 contiguous bytes of 16 rows (full 64-B L2 requests:
+//     measured +6..13 % over 8-B stores on the K = 640 / 1280 shapes, where the output write is as
+//     large as the operand reads). Straight from registers (the LDS keeps prefetching), bias from
+//     scalar loads (no vmcnt drain of the in-flight DMAs), GEGLU pairs in-lane, residual via 16-B
+//     loads;
 //   * the epilogue's stores sit in the vmcnt order between two DMA stages: the waits of the next
 //     K-tile allow STORES more outstanding ops (a full tile issues every store; a partial tile keeps
-//     the plain counts, which over-wait and are therefore safe).
+//     the plain counts, which over-wait and are therefore safe);
+//   * split-K tail (wave quantisation): with T tiles on G CUs the last round holds T mod G tiles,
+//     e.g. 64 of 256 for every SDXL level-2 1280-wide GEMM / conv (M = 16384: 320 tiles) -- 2
+//     rounds for 1.25 rounds of work. When a workspace is given, those tail tiles are cut into S
+//     K-ranges (S*tail <= G, chosen on the host); each range unit writes its fp32 partial tile,
+//     and the LAST unit of a tile to arrive (agent-scope release/acquire + one atomic counter per
+//     tile, no spin-waiting anywhere) sums the other partials and runs the normal epilogue.
 // Needs K % 64 == 0, K >= 128, N % 8 == 0, 16-B aligned rows, operands < 4 GiB (32-bit byte offsets).
 #pragma once
 #include "common.h"
 #include "mfma_core.h"
 #include "mfma_pp.h"
+#include <algorithm>
 
 namespace ppk {
 
@@ -44,19 +54,42 @@ typedef const __attribute__((address_space(4))) uint32_t* cptr_u32;
 
 template <bool GG>
 struct Stores {
-  static constexpr int N = GG ? 16 : 32;   // global stores per lane per tile
+  static constexpr int N = GG ? 8 : 16;   // global stores per lane per full tile
+};
+
+// Split-K tail plan (host and device agree on it through these fields).
+struct Split {
+  int t_full;        // tiles computed whole (a multiple of the CU count)
+  int S;             // K-ranges per tail tile (1: no split)
+  float4* part;      // [tail * S][32][512] fp32 partial tiles
+  int* cnt;          // [tail] arrival counters (zeroed before the launch)
 };
 
 template <int EXTRA>
-__device__ __forceinline__ void wait_window(bool after_epilogue, bool probe = false) {
-  if (probe) mc::wait_vmcnt<63>();     // EXPERIMENT flag 256: ignore the stores (timing probe; unsafe)
-  else if (after_epilogue) mc::wait_vmcnt<10 + EXTRA>();
+__device__ __forceinline__ void wait_window(bool after_epilogue) {
+  if (after_epilogue) mc::wait_vmcnt<10 + EXTRA>();
   else mc::wait_vmcnt<10>();
+}
+
+// tile column (0..255) staged at row r (0..127) of B part nq: the lane holding MFMA column tile j,
+// row 4*fq + t of wave wc's 32-row slice must see output column wc*64 + nq*32 + 8*fq + 4*j + t
+// (GEGLU: output column oc = wc*32 + 8*fq + 4*nq + t of the a (j = 0) / g (j = 1) half, whose
+// weight row sits at (oc / 16) * 32 + 16 * j + oc % 16 in the interleaved layout).
+template <bool GG>
+__device__ __forceinline__ int b_col_perm(int nq, int r) {
+  const int wc = r >> 5, j = (r >> 4) & 1, fq = (r >> 2) & 3, t = r & 3;
+  if constexpr (GG) {
+    const int oc = wc * 32 + 8 * fq + 4 * nq + t;
+    return (oc >> 4) * 32 + 16 * j + (oc & 15);
+  } else {
+    return wc * 64 + nq * 32 + 8 * fq + 4 * j + t;
+  }
 }
 
 template <bool GG, class AL>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
-                                    const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
+                                    const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m,
+                                    Split sp = Split{0, 1, nullptr, nullptr}) {
   constexpr int E = Stores<GG>::N;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -64,11 +97,28 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / BK;
   const int T = tiles_m * tiles_n;
+  const int S = sp.S;
+  const int U = S > 1 ? sp.t_full + (T - sp.t_full) * S : T;   // work units
   const int G = gridDim.x;
-  const int l0 = xcd_remap(blockIdx.x, G);
-  if (l0 >= T) return;
+  const int u0 = xcd_remap(blockIdx.x, G);
+  if (u0 >= U) return;
 
-  auto coords = [&](int l, int& m0, int& n0) {
+  // unit -> (tile origin, K range, partial slot or -1)
+  auto unit = [&](int u, int& m0, int& n0, int& kb, int& ke, int& slot) {
+    int l;
+    if (S <= 1 || u < sp.t_full) {
+      l = u;
+      kb = 0;
+      ke = nk;
+      slot = -1;
+    } else {
+      const int v = u - sp.t_full;
+      const int q = v / S, r = v - q * S;
+      l = sp.t_full + q;
+      kb = r * nk / S;
+      ke = (r + 1) * nk / S;
+      slot = v;
+    }
     int tm, tn;
     grouped_tile(l, tiles_m, tiles_n, group_m, tm, tn);
     m0 = tm * BM;
@@ -89,24 +139,22 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         const int r = g * 64 + lrow;
-        int n = n0 + pp::b_col(nq, r);
+        int n = n0 + b_col_perm<GG>(nq, r);
         n = n < N ? n : N - 1;
         boff[nq][g] = (uint32_t)(((long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7))) * 2);
       }
   };
   // stage part `part` of the K-tile with global sequence number s (-> LDS buffer s & 1), taking
-  // K offset kt * BK from whatever tile the part's loader slots currently point at
+  // K offset kt * BK from whatever unit the part's loader slots currently point at
   auto stage = [&](int part, long long s, int kt) {
     const int k0 = kt * BK;
     unsigned char* base = smem + (int)(s & 1) * BUF + part * PART + wave * 1024;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const void* src;
-      if (part == P_A0) src = al.src(0 * 2 + g, k0);
-      else if (part == P_A1) src = al.src(1 * 2 + g, k0);
-      else if (part == P_B0) src = (const void*)(Wb + (boff[0][g] + (uint32_t)(k0 * 2)));
-      else src = (const void*)(Wb + (boff[1][g] + (uint32_t)(k0 * 2)));
-      mc::lds_dma16(src, base + g * 8192);
+      if (part == P_A0) al.dma(0 * 2 + g, k0, base + g * 8192);
+      else if (part == P_A1) al.dma(1 * 2 + g, k0, base + g * 8192);
+      else if (part == P_B0) mc::lds_dma16((const void*)(Wb + (boff[0][g] + (uint32_t)(k0 * 2))), base + g * 8192);
+      else mc::lds_dma16((const void*)(Wb + (boff[1][g] + (uint32_t)(k0 * 2))), base + g * 8192);
     }
   };
 
@@ -135,7 +183,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         b[j][kk] = *reinterpret_cast<const bf16x8*>(P + r * 128 + 16 * c);
       }
   };
-  // C^T tiles: lane (fr, fq) accumulates C[row 16i + fr][col 16j + 4fq + 0..3] of its quadrant
+  // C^T tiles: lane (fr, fq) accumulates C[row 16i + fr][4 columns, see b_col_perm] of its quadrant
   auto mma = [&](auto mqc, auto nqc, const bf16x8 (&b)[2][2]) {
     constexpr int mq = decltype(mqc)::value, nq = decltype(nqc)::value;
     __builtin_amdgcn_s_setprio(1);
@@ -153,10 +201,15 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   using I1 = std::integral_constant<int, 1>;
 
   // ---- epilogue straight from registers. Row of acc[mq*4+i][.] = m0 + wr*128 + mq*64 + 16i + fr;
-  // col of acc[.][nq*2+j] = n0 + wc*64 + nq*32 + 16j + 4fq + (0..3).
+  // acc[.][nq*2+j][t] is column n0 + wc*64 + nq*32 + 8fq + 4j + t (GEGLU: see b_col_perm).
   auto epilogue_t = [&](int m0, int n0, auto hb_c, auto hr_c) {
     constexpr bool HB = decltype(hb_c)::value, HR = decltype(hr_c)::value;
-    const int ncw = n0 + wc * 64;                 // first column of this wave
+    const int ncw = n0 + wc * 64;                 // first (staged) column of this wave
+    // bias column offset (from ncw) of acc[.][nq*2+j][0] for this lane
+    auto bcol = [&](int nq, int j) {
+      if constexpr (GG) return (fq >> 1) * 32 + 16 * j + 8 * (fq & 1) + 4 * nq;
+      else return nq * 32 + 8 * fq + 4 * j;
+    };
     float4 bv[2][2];
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq)
@@ -173,9 +226,13 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const int b0 = nq * 16 + 8 * j;
-            const uint32_t w0 = fq == 0 ? sb[b0] : fq == 1 ? sb[b0 + 2] : fq == 2 ? sb[b0 + 4] : sb[b0 + 6];
-            const uint32_t w1 = fq == 0 ? sb[b0 + 1] : fq == 1 ? sb[b0 + 3] : fq == 2 ? sb[b0 + 5] : sb[b0 + 7];
+            // dword of column bcol(nq, j) for fq = 0..3 (compile-time per fq, selected per lane)
+            int d[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+              d[f] = (GG ? (f >> 1) * 32 + 16 * j + 8 * (f & 1) + 4 * nq : nq * 32 + 8 * f + 4 * j) >> 1;
+            const uint32_t w0 = fq == 0 ? sb[d[0]] : fq == 1 ? sb[d[1]] : fq == 2 ? sb[d[2]] : sb[d[3]];
+            const uint32_t w1 = fq == 0 ? sb[d[0] + 1] : fq == 1 ? sb[d[1] + 1] : fq == 2 ? sb[d[2] + 1] : sb[d[3] + 1];
             bv[nq][j] = unpack4_bf16(uint2{w0, w1});
           }
       } else {
@@ -183,7 +240,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            int col = ncw + nq * 32 + 16 * j + 4 * fq;
+            int col = ncw + bcol(nq, j);
             col = col < N ? col : N - 4;
             bv[nq][j] = unpack4_bf16(*reinterpret_cast<const uint2*>(e.bias + col));
           }
@@ -191,11 +248,13 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     }
     if constexpr (GG) {
       const int Nout = N >> 1;
+      const int ocol = (n0 >> 1) + wc * 32 + 8 * fq;   // 8 output columns of this lane
 #pragma unroll
       for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = m0 + wr * 128 + mq * 64 + 16 * i + fr;
+          uint2 h[2];
 #pragma unroll
           for (int nq = 0; nq < 2; ++nq) {
             const f32x4 a = acc[mq * 4 + i][nq * 2 + 0], g = acc[mq * 4 + i][nq * 2 + 1];
@@ -204,14 +263,14 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             const float o1 = (a[1] * e.alpha + ba.y) * gelu_fast(g[1] * e.alpha + bg.y);
             const float o2 = (a[2] * e.alpha + ba.z) * gelu_fast(g[2] * e.alpha + bg.z);
             const float o3 = (a[3] * e.alpha + ba.w) * gelu_fast(g[3] * e.alpha + bg.w);
-            const int ocol = ((ncw + nq * 32) >> 1) + 4 * fq;
-            if (row < M && ocol < Nout)
-              *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + ocol) = pack4_bf16(o0, o1, o2, o3);
+            h[nq] = pack4_bf16(o0, o1, o2, o3);
           }
+          if (row < M && ocol < Nout)
+            *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + ocol) = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
         }
     } else {
-      // residual words: all 32 loads issued before the first store (one wait, one drain)
-      uint2 rw[2][4][2][2];
+      // residual words: all 16 loads issued before the first store (one wait, one drain)
+      uint4 rw[2][4][2];
       if constexpr (HR) {
 #pragma unroll
         for (int mq = 0; mq < 2; ++mq)
@@ -220,13 +279,11 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             int row = m0 + wr * 128 + mq * 64 + 16 * i + fr;
             row = row < M ? row : M - 1;
 #pragma unroll
-            for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                int col = ncw + nq * 32 + 16 * j + 4 * fq;
-                col = col < N ? col : N - 4;
-                rw[mq][i][nq][j] = *reinterpret_cast<const uint2*>(e.R + (long long)row * e.ldr + col);
-              }
+            for (int nq = 0; nq < 2; ++nq) {
+              int col = ncw + nq * 32 + 8 * fq;
+              col = col < N ? col : N - 8;
+              rw[mq][i][nq] = *reinterpret_cast<const uint4*>(e.R + (long long)row * e.ldr + col);
+            }
           }
       }
 #pragma unroll
@@ -235,7 +292,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         for (int i = 0; i < 4; ++i) {
           const int row = m0 + wr * 128 + mq * 64 + 16 * i + fr;
 #pragma unroll
-          for (int nq = 0; nq < 2; ++nq)
+          for (int nq = 0; nq < 2; ++nq) {
+            uint2 h[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
               const f32x4 v = acc[mq * 4 + i][nq * 2 + j];
@@ -243,14 +301,16 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
               float v0 = v[0] * e.alpha + b.x, v1 = v[1] * e.alpha + b.y;
               float v2 = v[2] * e.alpha + b.z, v3 = v[3] * e.alpha + b.w;
               if constexpr (HR) {
-                const float4 rv = unpack4_bf16(rw[mq][i][nq][j]);
+                const uint4 rq = rw[mq][i][nq];
+                const float4 rv = unpack4_bf16(j ? uint2{rq.z, rq.w} : uint2{rq.x, rq.y});
                 v0 += rv.x; v1 += rv.y; v2 += rv.z; v3 += rv.w;
               }
-              const int col = ncw + nq * 32 + 16 * j + 4 * fq;
-              // EXPERIMENT flag 64: store only one quadrant (timing probe of the store-drain cost)
-              if (row < M && col < N && (!(e.flags & 64) || (mq == 0 && nq == 0)))
-                *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pack4_bf16(v0, v1, v2, v3);
+              h[j] = pack4_bf16(v0, v1, v2, v3);
             }
+            const int col = ncw + nq * 32 + 8 * fq;
+            if (row < M && col < N)
+              *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
+          }
         }
     }
   };
@@ -266,24 +326,57 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       else epilogue_t(m0, n0, F{}, F{});
     }
   };
+  __shared__ int last_flag;
+  // split unit: publish the fp32 partial; the tile's last arriver reduces and runs the epilogue
+  auto split_epilogue = [&](int m0, int n0, int slot) {
+    float4* mine = sp.part + (size_t)slot * (32 * THREADS);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const f32x4 v = acc[q >> 2][q & 3];
+      mine[q * THREADS + tid] = float4{v[0], v[1], v[2], v[3]};
+    }
+    // Publish: the workgroup barrier orders every wave's partial stores (all in this XCD's L2 once
+    // the barrier's vmcnt(0) retires them) before ONE agent-scope release by thread 0 -- a per-wave
+    // release would write the L2 back once per wave; then the arrival count. The last arriver's
+    // thread 0 acquires (invalidates this CU's caches) before the barrier that lets every wave
+    // read the other units' partials.
+    mc::wait_vmcnt<0>();         // this wave's partial stores have reached the L2
+    __syncthreads();
+    const int tile = slot / S;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int old = __hip_atomic_fetch_add(sp.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = old == S - 1;
+      if (old == S - 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    const int r0 = tile * S;
+    for (int r = 0; r < S; ++r) {
+      if (r0 + r == slot) continue;
+      const float4* o = sp.part + (size_t)(r0 + r) * (32 * THREADS);
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        const float4 w = o[q * THREADS + tid];
+        acc[q >> 2][q & 3] += f32x4{w.x, w.y, w.z, w.w};
+      }
+    }
+    epilogue(m0, n0);
+  };
 
-  // EXPERIMENT flag 128: odd workgroups start ~half a tile later (store-burst desync probe)
-  if ((e.flags & 128) && (blockIdx.x & 1)) {
-    for (int t = 0; t < nk * 3000 / 8128 / 2 + 1; ++t) __builtin_amdgcn_s_sleep(127);
-  }
-  // ---- prologue: A0 B0 B1 A1 of K-tile 0, A0 B0 B1 of K-tile 1 -> wait for A0(0), B0(0)
-  int l = l0, m0, n0;
-  coords(l, m0, n0);
+  // ---- prologue: A0 B0 B1 A1 of the first K-tile, A0 B0 B1 of the second -> wait for A0, B0
+  int u = u0, m0, n0, kb, ke, slot;
+  unit(u, m0, n0, kb, ke, slot);
   setup_a(0, m0);
   setup_a(1, m0);
   setup_b(n0);
-  stage(P_A0, 0, 0);
-  stage(P_B0, 0, 0);
-  stage(P_B1, 0, 0);
-  stage(P_A1, 0, 0);
-  stage(P_A0, 1, 1);
-  stage(P_B0, 1, 1);
-  stage(P_B1, 1, 1);
+  stage(P_A0, 0, kb);
+  stage(P_B0, 0, kb);
+  stage(P_B1, 0, kb);
+  stage(P_A1, 0, kb);
+  stage(P_A0, 1, kb + 1);
+  stage(P_B0, 1, kb + 1);
+  stage(P_B1, 1, kb + 1);
   mc::wait_vmcnt<10>();
   pp::barrier();
   if (wr == 1) pp::barrier();   // stagger: group 1 runs one segment behind group 0
@@ -291,42 +384,43 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   long long s = 0;              // global K-tile sequence number of this workgroup
   bool stores_pending = false;  // the previous tile's full set of epilogue stores is in the vmcnt window
   while (true) {
-    const int ln = l + G;
-    const bool has_next = ln < T;
-    int nm0 = m0, nn0 = n0;
-    if (has_next) coords(ln, nm0, nn0);
+    const int un = u + G;
+    const bool has_next = un < U;
+    int nm0 = m0, nn0 = n0, nkb = kb, nke = ke, nslot = -1;
+    if (has_next) unit(un, nm0, nn0, nkb, nke, nslot);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
+    for (int kt = kb; kt < ke; ++kt) {
       const int buf = (int)(s & 1);
-      const bool after = stores_pending && kt == 0;
-      const bool probe = (e.flags & 256) && stores_pending && kt < 3;
-      const int kt1 = kt + 1 < nk ? kt + 1 : (has_next ? 0 : nk - 1);
-      const int kt2 = kt + 2 < nk ? kt + 2 : (has_next ? kt + 2 - nk : nk - 1);
+      const bool after = stores_pending && kt == kb;
+      // K-tiles one and two ahead in this workgroup's sequence (the next unit's first two, or a
+      // dummy reload of this unit's last one after the final unit); every unit spans >= 2 K-tiles
+      const int kt1 = kt + 1 < ke ? kt + 1 : (has_next ? nkb + (kt + 1 - ke) : ke - 1);
+      const int kt2 = kt + 2 < ke ? kt + 2 : (has_next ? nkb + (kt + 2 - ke) : ke - 1);
       // phase 1 (mq0, nq0): read A0, B0; DMA A1 of sequence s+1
       read_a(buf, 0);
       read_b(buf, 0, bf0);
-      if (kt + 1 == nk && has_next) setup_a(1, nm0);
+      if (kt + 1 == ke && has_next) setup_a(1, nm0);
       stage(P_A1, s + 1, kt1);
-      wait_window<E>(after, probe);
+      wait_window<E>(after);
       pp::wait_lgkm0();
       pp::barrier();
       mma(I0{}, I0{}, bf0);
       pp::barrier();
       // phase 2 (mq0, nq1): read B1; DMA A0 of s+2
       read_b(buf, 1, bf1);
-      if (kt + 2 == nk && has_next) setup_a(0, nm0);
+      if (kt + 2 == ke && has_next) setup_a(0, nm0);
       stage(P_A0, s + 2, kt2);
-      wait_window<E>(after, probe);
+      wait_window<E>(after);
       pp::wait_lgkm0();
       pp::barrier();
       mma(I0{}, I1{}, bf1);
       pp::barrier();
       // phase 3 (mq1, nq1): read A1; DMA B0 of s+2
       read_a(buf, 1);
-      if (kt + 2 == nk && has_next) setup_b(nn0);
+      if (kt + 2 == ke && has_next) setup_b(nn0);
       stage(P_B0, s + 2, kt2);
       pp::wait_lgkm0();
       pp::barrier();
@@ -334,22 +428,58 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       pp::barrier();
       // phase 4 (mq1, nq0): DMA B1 of s+2; retire A0(s+1), B0(s+1) for the next phase 1
       stage(P_B1, s + 2, kt2);
-      wait_window<E>(after, probe);
+      wait_window<E>(after);
       pp::barrier();
       mma(I1{}, I0{}, bf0);
       pp::barrier();
       ++s;
     }
+    if (slot >= 0) {
+      // a split unit is its workgroup's last (S * tail <= G): drain, then reduce / publish
+      mc::wait_vmcnt<0>();
+      if (wr == 0) pp::barrier();   // balance the stagger before the workgroup barriers
+      split_epilogue(m0, n0, slot);
+      return;
+    }
     epilogue(m0, n0);
     // a full tile issued every one of its E stores (partial tiles may skip some: keep plain waits)
     stores_pending = (m0 + BM <= M) && (n0 + BN <= N);
     if (!has_next) break;
-    l = ln;
+    u = un;
     m0 = nm0;
     n0 = nn0;
+    kb = nkb;
+    ke = nke;
+    slot = nslot;
   }
   if (wr == 0) pp::barrier();   // balance the stagger
   mc::wait_vmcnt<0>();          // trailing dummy DMAs must land before the workgroup's LDS is released
+}
+
+// Host: split-K tail plan for T tiles of nk K-tiles on G CUs. Returns S (1 = no split) and the
+// number of whole tiles; the workspace needs tail * S * 256 KiB of partials + tail counters.
+inline int split_plan(long long T, int nk, int G, int& t_full) {
+  const long long tail = T % G;
+  t_full = (int)(T - tail);
+  if (tail == 0 || tail * 2 > G || nk < 4) return 1;
+  // last-round cost in K-tile times: nk / S of MFMA work + ~3 per extra partial the fixup reads
+  // (256 KiB at one CU's share of HBM bandwidth) + ~1.5 for writing the partials
+  int best = 1;
+  double best_cost = nk;
+  const int smax = (int)std::min<long long>(std::min<long long>(G / tail, nk / 2), 16);
+  for (int S = 2; S <= smax; ++S) {
+    const double c = (double)nk / S + 3.0 * (S - 1) + 1.5;
+    if (c < best_cost) { best_cost = c; best = S; }
+  }
+  return best;
+}
+
+inline long long split_ws_bytes(long long T, int nk, int G) {
+  int t_full;
+  const int S = split_plan(T, nk, G, t_full);
+  if (S <= 1) return 0;
+  const long long tail = T - t_full;
+  return tail * S * 32ll * THREADS * 16 + ((tail * 4 + 255) / 256) * 256;
 }
 
 }  // namespace ppk

@@ -76,7 +76,10 @@ class CrossAttention(nn.Module, DerivedMixin):
             ctx_cache[cache_key] = (context, k, v)
         return k, v
 
-    def forward(self, x, context=None, value=None, mask=None, residual=None, ctx_cache=None, cache_key=None):
+    def forward(self, x, context=None, value=None, mask=None, residual=None, ctx_cache=None, cache_key=None,
+                sp=None):
+        """``sp`` (parallel.sp.SeqParallel): x is this rank's token shard; self-attention runs over
+        the whole sequence through ``sp.attention`` (cross-attention needs no exchange)."""
         inner = self.heads * self.dim_head
         if context is None and value is None and x.dtype == self.to_q.weight.dtype \
                 and x.device == self.to_q.weight.device:
@@ -86,7 +89,10 @@ class CrossAttention(nn.Module, DerivedMixin):
             q = self.to_q(x)
             ctx = x if context is None else context
             k, v = self.project_kv(ctx, value, ctx_cache, cache_key)
-        o = ops.attention(q, k, v, self.heads, mask=mask)
+        if sp is not None and context is None and value is None and mask is None:
+            o = sp.attention(q.contiguous(), k.contiguous(), v.contiguous(), self.heads)
+        else:
+            o = ops.attention(q, k, v, self.heads, mask=mask)
         return self.to_out[0](o, residual=residual)
 
 
@@ -189,7 +195,7 @@ class BasicTransformerBlock(nn.Module):
         if self.disable_self_attn:
             x = self.attn1(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 1))
         else:
-            x = self.attn1(n, residual=x)
+            x = self.attn1(n, residual=x, sp=to.get("sp"))
         n = self.norm2(x)
         x = self.attn2(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 2))
         return self.ff(self.norm3(x), residual=x)
@@ -278,6 +284,11 @@ class SpatialTransformer(nn.Module):
         to = transformer_options if transformer_options is not None else {}
         if not isinstance(context, list):
             context = [context] * len(self.transformer_blocks)
+        sp = to.get("sp")
+        if sp is not None and sp.P > 1 and not to.get("patches") and not to.get("patches_replace") \
+                and (x.shape[2] * x.shape[3]) % sp.P == 0 and all(bk._plain for bk in self.transformer_blocks):
+            return self._forward_sp(x, context, to, sp)
+        to = dict(to, sp=None) if sp is not None else to
         b, c, h, w = x.shape
         x_in = x
         x = self.norm(x)
@@ -299,3 +310,31 @@ class SpatialTransformer(nn.Module):
             return x.reshape(b, h, w, c).permute(0, 3, 1, 2) + x_in
         x = x.reshape(b, h, w, -1).permute(0, 3, 1, 2)
         return self.proj_out(x, residual=x_in)
+
+    def _forward_sp(self, x, context, to, sp):
+        """Token-parallel stack (latency mode): GroupNorm on the full image (replicated), then only
+        this rank's contiguous token shard through proj_in, the blocks and proj_out (+ the fused
+        residual), then one all-gather of the tokens back into the image."""
+        b, c, h, w = x.shape
+        T = h * w
+        lo, hi = sp.rank * (T // sp.P), (sp.rank + 1) * (T // sp.P)
+        x_tok = x.permute(0, 2, 3, 1).reshape(b, T, c)
+        n = self.norm(x)
+        if not self.use_linear:
+            n = self.proj_in(n)
+        t = n.permute(0, 2, 3, 1).reshape(b, T, -1)[:, lo:hi].contiguous()
+        if self.use_linear:
+            t = self.proj_in(t)
+        for i, blk in enumerate(self.transformer_blocks):
+            to["block_index"] = i
+            t = blk(t, context=context[i], transformer_options=to)
+        res = x_tok[:, lo:hi].contiguous()
+        if self.use_linear:
+            t = self.proj_out(t, residual=res)
+        else:
+            # the 1x1 conv on tokens is the same GEMM
+            wgt = self.proj_out.weight.reshape(c, -1).to(device=t.device, dtype=t.dtype)
+            bias = None if self.proj_out.bias is None else self.proj_out.bias.to(device=t.device, dtype=t.dtype)
+            t = ops.linear(t, wgt, bias, residual=res)
+        full = sp.gather(t, dim=1)                          # [b, T, c]
+        return full.reshape(b, h, w, c).permute(0, 3, 1, 2)

@@ -55,6 +55,20 @@ def _ptr(t):
 # ----------------------------------------------------------------------------------------------
 # GEMM family
 # ----------------------------------------------------------------------------------------------
+_V7WS: dict = {}
+_V7_SPLIT = os.environ.get("CGS_V7_SPLIT", "1") != "0"
+
+
+def _v7_ws(M: int, N: int, K: int, device):
+    """Split-K tail workspace of the v7 GEMM / conv (mfma_ppk.h), from the caching allocator so it
+    follows stream and graph-pool semantics; None when the shape's last round is full."""
+    n = _V7WS.get((M, N, K))
+    if n is None:
+        n = int(_lib().cgs_v7_ws_bytes(M, N, K)) if _V7_SPLIT and _native.has_kernel("cgs_v7_ws_bytes") else 0
+        _V7WS[(M, N, K)] = n
+    return torch.empty(n, dtype=torch.uint8, device=device) if n else None
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            residual: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ weight^T (+ bias) (+ residual). ``residual`` has y's shape (fused epilogue add).
@@ -86,6 +100,12 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
 
         def run_hip(variant):
             out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+            ws = _v7_ws(M, N, K, x.device) if variant == 7 else None
+            if ws is not None:
+                _check(_lib().cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
+                                                 M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
+                                                 ws.data_ptr(), ws.numel(), _stream()), "cgs_gemm_bf16_v7ws")
+                return out
             _check(_lib().cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
                                           M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
                                           variant, _stream()), "cgs_gemm_bf16")
@@ -174,6 +194,12 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
 
         def run_hip(variant):
             out = torch.empty((M, N2 // 2), device=x.device, dtype=x.dtype)
+            ws = _v7_ws(M, N2, K, x.device) if variant == 7 else None
+            if ws is not None:
+                _check(_lib().cgs_gemm_bf16_v7ws(a.data_ptr(), weight.data_ptr(), out.data_ptr(), _ptr(bias), None,
+                                                 M, N2, K, K, K, N2 // 2, 0, epi, 1.0, ws.data_ptr(), ws.numel(),
+                                                 _stream()), "cgs_gemm_bf16_v7ws")
+                return out
             _check(_lib().cgs_gemm_bf16_v(a.data_ptr(), weight.data_ptr(), out.data_ptr(), _ptr(bias), None,
                                           M, N2, K, K, K, N2 // 2, 0, epi, 1.0, variant, _stream()),
                    "cgs_gemm_bf16")
@@ -439,8 +465,6 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         Ho = (Hl + 2 * padding - kh) // stride + 1
         Wo = (Wl + 2 * padding - kw) // stride + 1
         xc = x.contiguous(memory_format=torch.channels_last)
-        out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype,
-                          memory_format=torch.channels_last)
         r = None
         if residual is not None:
             r = residual.contiguous(memory_format=torch.channels_last)
@@ -449,6 +473,13 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         def run(variant):
             out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype,
                               memory_format=torch.channels_last)
+            ws = _v7_ws(N * Ho * Wo, Cout, kh * kw * Cin, x.device) if variant == 7 else None
+            if ws is not None:
+                _check(_lib().cgs_conv2d_nhwc_v7ws(xc.data_ptr(), _ptr(x2c), C1, weight_nhwc.data_ptr(), _ptr(bias),
+                                                   _ptr(r), out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride,
+                                                   padding, Ho, Wo, flags, ws.data_ptr(), ws.numel(), _stream()),
+                       "cgs_conv2d_nhwc_v7ws")
+                return out
             _check(_lib().cgs_conv2d_nhwc_v(xc.data_ptr(), _ptr(x2c), C1, weight_nhwc.data_ptr(), _ptr(bias), _ptr(r),
                                             out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding, Ho, Wo,
                                             flags, variant, _stream()), "cgs_conv2d_nhwc")

@@ -151,7 +151,14 @@ class Comm:
         return torch.load(io.BytesIO(st.get(key)), weights_only=True)
 
     def shutdown(self):
+        """Leave together: a barrier first (unless degraded: dead peers never arrive), so no rank
+        tears its transport down while a peer still talks to it (Gloo aborts the process then)."""
         if self.world > 1 and dist.is_initialized():
+            if not self.degraded:
+                try:
+                    dist.barrier()
+                except Exception:       # pragma: no cover - peers already gone
+                    pass
             dist.destroy_process_group()
 
 

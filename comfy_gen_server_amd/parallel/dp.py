@@ -133,8 +133,6 @@ class DataParallelGenerator:
                 return None
             return generate_local(self.patcher, self.clip, self.vae, job, 0, job.batch, decode="uint8")
         job = c.broadcast_object(job)
-        per = job.batch // c.world
-        rem = job.batch % c.world
         offset, local = self._shard(job, c.rank)
         u8 = generate_local(self.patcher, self.clip, self.vae, job, offset, local, decode="uint8")
         if gather and c.enabled and fault_tolerant:
@@ -143,19 +141,73 @@ class DataParallelGenerator:
             if dead:
                 return self._recover(job, u8, dead, rid)
         if gather and c.enabled:
-            if rem:
-                pad = torch.zeros((per + 1 - local,) + tuple(u8.shape[1:]), dtype=u8.dtype, device=u8.device)
-                u8 = torch.cat([u8, pad])
-            allimgs = c.all_gather(u8.to(c.device))
-            if rem:
-                keep = []
-                for r in range(c.world):
-                    n = per + (1 if r < rem else 0)
-                    keep.append(allimgs[r * (per + (1 if rem else 0)): r * (per + (1 if rem else 0)) + n])
-                allimgs = torch.cat(keep)
-            return allimgs
+            return self._gather_plain(job, u8)
         return u8
 
+    def _gather_plain(self, job, u8):
+        c = self.comm
+        if not c.enabled:
+            return u8
+        per, rem = job.batch // c.world, job.batch % c.world
+        local = u8.shape[0]
+        if rem:
+            pad = torch.zeros((per + 1 - local,) + tuple(u8.shape[1:]), dtype=u8.dtype, device=u8.device)
+            u8 = torch.cat([u8, pad])
+        allimgs = c.all_gather(u8.to(c.device))
+        if rem:
+            keep = []
+            for r in range(c.world):
+                n = per + (1 if r < rem else 0)
+                keep.append(allimgs[r * (per + 1): r * (per + 1) + n])
+            allimgs = torch.cat(keep)
+        return allimgs
+
+    def run_many(self, jobs, pipeline=None):
+        """Serve a stream of jobs; yields each job's uint8 images (rank 0: the whole batch).
+
+        ``pipeline`` (default: env ``CGS_DP_PIPELINE=1``): prompt-level multi-stream overlap (SURVEY
+        §2.5 "multi-stream" row, §7.2 step 9). Job n's VAE decode + image all-gather are issued on a
+        side HIP stream, ordered after job n's sampling by an event, while the host goes on to issue
+        job n+1's CLIP encode and sampler steps on the main stream -- the two share the GPU, so the
+        VAE's low-occupancy phases (small-spatial convs, GroupNorm reductions, the one-workgroup-
+        per-CU mid attention) and the host gaps between jobs are filled with UNet work. Results come
+        out one job late, in order, with the main stream made to wait for them. The liveness /
+        recovery protocol of ``run(fault_tolerant=True)`` is not used on this path."""
+        c = self.comm
+        if pipeline is None:
+            pipeline = os.environ.get("CGS_DP_PIPELINE", "0") == "1"
+        use_side = pipeline and torch.cuda.is_available() and dm.get_torch_device().type == "cuda"
+        side = torch.cuda.Stream(device=dm.get_torch_device()) if use_side else None
+        pending = None
+        for job in jobs:
+            job = c.broadcast_object(job)
+            offset, local = self._shard(job, c.rank)
+            if side is None:
+                u8 = generate_local(self.patcher, self.clip, self.vae, job, offset, local, decode="uint8")
+                yield self._gather_plain(job, u8)
+                continue
+            samples = generate_local(self.patcher, self.clip, self.vae, job, offset, local, decode=False)
+            sampled = torch.cuda.Event()
+            sampled.record()
+            with torch.cuda.stream(side):
+                side.wait_event(sampled)
+                samples.record_stream(side)
+                with _stage("vae"):
+                    out = self._gather_plain(job, self.vae.decode_uint8(samples))
+                done = torch.cuda.Event()
+                done.record(side)
+            if pending is not None:
+                yield self._collect(*pending)
+            pending = (out, done)
+        if pending is not None:
+            yield self._collect(*pending)
+
+    @staticmethod
+    def _collect(out, done):
+        cur = torch.cuda.current_stream()
+        cur.wait_event(done)
+        out.record_stream(cur)
+        return out
 
     def _recover(self, job, u8, dead, rid):
         """Degraded gather: survivors hand their shards to rank 0 through the store,

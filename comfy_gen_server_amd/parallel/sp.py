@@ -18,6 +18,8 @@ Both take the *local* sequence shard of q / k / v — [B, S / P, H * D] on each 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -118,3 +120,46 @@ def gather_sequence(x, group=None, dim=1):
     parts = [torch.empty_like(x) for _ in range(P)]
     dist.all_gather(parts, x.contiguous(), group=group)
     return torch.cat(parts, dim=dim)
+
+
+def kv_gather_attention(q, k, v, heads: int, group=None):
+    """Local query shard against the all-gathered keys/values (one all-gather of K and V, then the
+    single-GPU flash kernel on [B, S/P] x [B, S] -- any head count; the choice when heads % P != 0,
+    e.g. SDXL's 10-head level-1 blocks on 4 ranks)."""
+    P, _ = _world(group)
+    if P == 1:
+        return ops.attention(q, k, v, heads)
+    kv = gather_sequence(torch.cat([k, v], dim=-1), group)
+    HD = q.shape[-1]
+    return ops.attention(q, kv[..., :HD], kv[..., HD:], heads)
+
+
+class SeqParallel:
+    """Token (sequence) parallelism of the UNet's transformer stacks over ``group`` (latency mode,
+    ``parallel/latency.py``): a SpatialTransformer keeps only its rank's contiguous token shard
+    through LayerNorm / QKV / FF / projections; self-attention exchanges through ``attention``
+    (Ulysses all-to-all when the heads divide over the ranks, else the K/V all-gather form);
+    cross-attention needs nothing (the text context is replicated); the stack output is
+    all-gathered back to the full image for the (replicated) ResBlocks."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.P, self.rank = _world(group)
+        self.mode = os.environ.get("CGS_SP_ATTN", "auto")   # auto | ulysses | kvgather | ring
+        self.stats = {"ulysses": 0, "kvgather": 0, "ring": 0}
+
+    def attention(self, q, k, v, heads: int):
+        if self.mode == "ring":
+            self.stats["ring"] += 1
+            return ring_attention(q, k, v, heads, self.group)
+        if self.mode != "kvgather" and heads % self.P == 0:
+            self.stats["ulysses"] += 1
+            return ulysses_attention(q, k, v, heads, self.group)
+        self.stats["kvgather"] += 1
+        return kv_gather_attention(q, k, v, heads, self.group)
+
+    def shard(self, x, dim=1):
+        return shard_sequence(x, self.group, dim)
+
+    def gather(self, x, dim=1):
+        return gather_sequence(x, self.group, dim)

@@ -61,8 +61,8 @@ class GraphedForward:
     def _eligible(self, x, control, to, kw):
         if not enabled() or not x.is_cuda or control is not None:
             return False
-        if to and (to.get("patches") or to.get("patches_replace")):
-            return False
+        if to and (to.get("patches") or to.get("patches_replace") or to.get("sp") is not None):
+            return False            # Python hooks / latency-mode collectives run eagerly
         for v in kw.values():
             if isinstance(v, torch.Tensor) and not v.is_cuda:
                 return False

@@ -40,7 +40,7 @@ VAE = [
     ("vae 256->128 @1024", 8, 1024, 1024, 256, 128, 3, 1),
     ("vae 128 @1024", 8, 1024, 1024, 128, 128, 3, 1),
 ]
-VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v7": 7}
+VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v7": 7, "v7s": 8}   # v7s: v7 + split-K tail
 
 
 def _time(fn, iters):
@@ -76,8 +76,14 @@ def main(argv):
         it = max(2, int(3e11 / flops))
         ref = F.conv2d(x[:1].float(), w.float(), b.float(), s, p)
         res = {}
+        nws = lib.cgs_v7_ws_bytes(N * Ho * Wo, Cout, k * k * Cin)
+        ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
         for vn, v in VARIANTS.items():
             def run(v=v):
+                if v == 8:
+                    return lib.cgs_conv2d_nhwc_v7ws(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
+                                                    out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0,
+                                                    ws.data_ptr(), nws, core._stream())
                 return lib.cgs_conv2d_nhwc_v(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
                                              out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0, v,
                                              core._stream())
@@ -99,7 +105,7 @@ def main(argv):
                     " | ".join("bad" if res[v] == -1.0 else f"{res[v]:.0f}" for v in VARIANTS) +
                     f" | {res['miopen']:.0f} |")
         print(rows[-1], flush=True)
-        del x, w, wn, out
+        del x, w, wn, out, ws
     text = "\n".join(rows)
     if argv:
         open(argv[0], "w").write(text + "\n")

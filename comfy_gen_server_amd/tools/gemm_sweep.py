@@ -19,6 +19,8 @@ if "--nowait" in sys.argv:           # v7 probe: DMA waits ignore epilogue store
     EPI |= 256
 if "--stagger" in sys.argv:          # v7 probe: odd workgroups start half a tile late (flag 128)
     EPI |= 128
+if "--wide16" in sys.argv:          # v7 probe: 16-B epilogue stores, 64 contiguous B per row (flag 512)
+    EPI |= 512
 if "--kseries" in sys.argv:        # per-tile fixed cost vs per-K-tile cost: 1024 tiles (4 rounds), K swept
     SHAPES = [(16384, 4096, k) for k in (128, 256, 640, 1280, 2560, 5120)] + [(16384, 10240, 1280), (65536, 4096, 640)]
     VARIANTS = [5, 7]

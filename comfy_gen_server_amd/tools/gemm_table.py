@@ -27,7 +27,7 @@ SHAPES = [
     ("kv_ctx1280", 1232, 2560, 2048, False, False),
 ]
 
-VARIANTS = {"v5": 5, "v6": 6, "v7": 7, "v4": 4, "auto": -1}
+VARIANTS = {"v5": 5, "v6": 6, "v7": 7, "v7s": 8, "v4": 4, "auto": -1}   # v7s: v7 + split-K tail
 
 
 def _time(fn, iters):
@@ -69,7 +69,15 @@ def main(argv):
         ref = None
         res_tf = {}
         for vname, v in VARIANTS.items():
+            nws = lib.cgs_v7_ws_bytes(M, N, K)
+            ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
+
             def run(v=v):
+                if v == 8:
+                    return lib.cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(),
+                                                  None if r is None else r.data_ptr(), M, N, K, K, K, nout,
+                                                  nout if r is not None else 0, epi, 1.0, ws.data_ptr(), nws,
+                                                  core._stream())
                 return lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(),
                                            None if r is None else r.data_ptr(), M, N, K, K, K, nout,
                                            nout if r is not None else 0, epi, 1.0, v, core._stream())

@@ -270,3 +270,71 @@ def test_dp_ws3_equals_ws1(tmp_path, sampler):
     assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), (a - b).abs().max()
     # distinct images really got distinct noise (no rank-correlated images)
     assert (b[2] - b[0]).abs().mean() > 0.05 and (b[4] - b[0]).abs().mean() > 0.05
+
+
+def test_run_many_matches_run_cpu(monkeypatch):
+    """``run_many`` (the serving loop; its pipelined form needs a GPU) gives each job's images in
+    order, identical to ``run`` per job."""
+    monkeypatch.setenv("CGS_FORCE_CPU", "1")
+    from comfy_gen_server_amd.parallel.dp import DataParallelGenerator, Job
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=5)
+        gen = DataParallelGenerator(patcher, clip, vae)
+        jobs = [Job(batch=2, steps=3, seed=s, width=64, height=64) for s in (3, 4)]
+        many = list(gen.run_many(iter(jobs), pipeline=True))     # no GPU: falls back to in-order
+        one = [gen.run(j) for j in jobs]
+    assert len(many) == 2
+    for a, b in zip(many, one):
+        assert a.dtype == torch.uint8 and torch.equal(a, b)
+
+
+_LAT_WORKER = r'''
+import os, sys, torch
+sys.path.insert(0, os.environ["PYTHONPATH"])
+from comfy_gen_server_amd.parallel.comm import init_from_env
+from comfy_gen_server_amd.runtime import device as dm
+dm.set_cpu_mode(True)
+c = init_from_env(backend="gloo")
+from comfy_gen_server_amd.tools.synth import build_pipeline
+from comfy_gen_server_amd.parallel.dp import generate_local, Job
+from comfy_gen_server_amd.parallel.latency import LatencyParallel
+lay = int(os.environ["CGS_TEST_LAYOUT_BATCH"])
+with torch.inference_mode():
+    patcher, clip, vae = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=5)
+    lp = LatencyParallel(c, batch=lay)
+    job = Job(batch=1, steps=4, width=64, height=64, seed=21)
+    ref = generate_local(patcher, clip, vae, job, 0, 1, decode=False)
+    got = generate_local(lp.patch(patcher), clip, vae, job, 0, 1, decode=False)
+assert lp.calls >= 4, lp.calls
+if lp.Q > 1:
+    st = lp.sp.stats
+    assert sum(st.values()) > 0, st
+    mode = os.environ.get("CGS_SP_ATTN", "auto")
+    if mode in ("ring", "kvgather"):
+        assert st[mode] > 0, st
+d = (got - ref).abs().max().item()
+print("layout", lay, "G", lp.G, "Q", lp.Q, "maxdiff", d, "sp", None if lp.sp is None else lp.sp.stats, flush=True)
+assert d < 1e-4, d
+c.shutdown()
+'''
+
+
+@pytest.mark.parametrize("world,layout_batch,attn", [(2, 2, "auto"), (2, 1, "auto"), (2, 1, "kvgather"),
+                                                     (4, 2, "auto"), (2, 1, "ring")])
+def test_latency_mode_matches_single_gpu(tmp_path, world, layout_batch, attn):
+    """Latency mode (parallel/latency.py) on gloo: CFG/batch split (G groups) x token-parallel
+    SpatialTransformers (Q ranks: Ulysses / K-V all-gather / ring attention) sample the same
+    latents as the plain single-process sampler."""
+    script = tmp_path / "lat_worker.py"
+    script.write_text(_LAT_WORKER)
+    env = _env()
+    env.update(MASTER_ADDR="127.0.0.1", CGS_TEST_LAYOUT_BATCH=str(layout_batch), CGS_SP_ATTN=attn)
+    port = str(_free_port())
+    procs = [subprocess.Popen([sys.executable, str(script)], cwd=ROOT,
+                              env=dict(env, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r), MASTER_PORT=port),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, (o[-2000:], e[-3000:])
+    assert all("maxdiff" in o for o, _ in outs)

@@ -467,3 +467,84 @@ def test_unet_skip_concat_never_materialised(cuda):
                context=c.to(cuda, torch.bfloat16), transformer_options={})
         yc = cpu(x, t, context=c, transformer_options={})
     assert _rel(yd.float().cpu(), yc) < 3e-2
+
+
+# v7 split-K tail (mfma_ppk.h): shapes whose last round of 256x256 tiles is at most half full get
+# their tail tiles cut into K ranges, reduced by the last-arriving unit of each tile.
+@pytest.mark.parametrize("M,N,K,epi", [(16384, 1280, 1280, "bias_res"), (16384, 1280, 5120, "bias"),
+                                       (1024, 1024, 2048, "none"), (1232, 2560, 2048, "bias"),
+                                       (4096, 1280, 640, "bias_res"), (16200, 1288, 1280, "bias_res")])
+def test_gemm_v7_split_tail(cuda, M, N, K, epi):
+    lib = _native.load_kernels()
+    ws_bytes = lib.cgs_v7_ws_bytes(M, N, K)
+    assert ws_bytes > 0, "shape chosen to exercise the split tail"
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
+    flags = (1 if b is not None else 0) | (2 if r is not None else 0)
+    ws = torch.full((ws_bytes,), 0x7F, dtype=torch.uint8, device=cuda)   # garbage counters / partials
+    outs = []
+    for _ in range(2):                                                   # counters self-consistent on reuse
+        y = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        assert lib.cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), y.data_ptr(), None if b is None else b.data_ptr(),
+                                      None if r is None else r.data_ptr(), M, N, K, K, K, N, N if r is not None else 0,
+                                      flags, 1.0, ws.data_ptr(), ws_bytes, core._stream()) == 0
+        outs.append(y)
+    torch.cuda.synchronize()
+    ref = a.float() @ w.float().t()
+    if b is not None:
+        ref += b.float()
+    if r is not None:
+        ref += r.float()
+    assert _rel(outs[0], ref) < 1e-2
+    assert torch.equal(outs[0], outs[1]) or _rel(outs[1], ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N2,K", [(16384, 2560, 1280), (1024, 5120, 640)])
+def test_gemm_v7_split_tail_geglu(cuda, M, N2, K):
+    lib = _native.load_kernels()
+    ws_bytes = lib.cgs_v7_ws_bytes(M, N2, K)
+    assert ws_bytes > 0
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N2, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N2, device=cuda).to(torch.bfloat16)
+    wi, bi = core.geglu_interleave(w), core.geglu_interleave(b)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    y = torch.empty(M, N2 // 2, device=cuda, dtype=torch.bfloat16)
+    assert lib.cgs_gemm_bf16_v7ws(a.data_ptr(), wi.data_ptr(), y.data_ptr(), bi.data_ptr(), None, M, N2, K, K, K,
+                                  N2 // 2, 0, 1 | core.EPI_GEGLU, 1.0, ws.data_ptr(), ws_bytes, core._stream()) == 0
+    h = a.float() @ w.float().t() + b.float()
+    x1, g = h.chunk(2, dim=-1)
+    assert _rel(y, x1 * F.gelu(g)) < 1e-2
+
+
+@pytest.mark.parametrize("N,C1,C2,H,W,Cout,k,res", [(4, 1280, 0, 32, 32, 1280, 3, True), (4, 1280, 1280, 32, 32, 1280, 3, False),
+                                                    (2, 640, 0, 64, 48, 640, 3, True), (4, 2560, 0, 32, 32, 1280, 1, False)])
+def test_conv_v7_split_tail(cuda, N, C1, C2, H, W, Cout, k, res):
+    """v7 conv with the buffer-load gather (ConvGatherKB) and the split-K tail, dual source included."""
+    lib = _native.load_kernels()
+    Cin = C1 + C2
+    ws_bytes = lib.cgs_v7_ws_bytes(N * H * W, Cout, k * k * Cin)
+    assert ws_bytes > 0
+    torch.manual_seed(0)
+    a = torch.randn(N, C1, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x2 = (torch.randn(N, C2, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+          if C2 else None)
+    w = (torch.randn(Cout, Cin, k, k, device=cuda) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
+    bias = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    full = a if x2 is None else torch.cat([a, x2], 1)
+    ref = F.conv2d(full.float(), w.float(), bias.float(), 1, k // 2)
+    r = None
+    if res:
+        r = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        ref = ref + r.float()
+    wn = w.permute(0, 2, 3, 1).contiguous()
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    y = torch.empty(N, Cout, H, W, device=cuda, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert lib.cgs_conv2d_nhwc_v7ws(a.data_ptr(), None if x2 is None else x2.data_ptr(), C1, wn.data_ptr(),
+                                    bias.data_ptr(), None if r is None else r.data_ptr(), y.data_ptr(), N, H, W, Cin,
+                                    Cout, k, k, 1, k // 2, H, W, 0, ws.data_ptr(), ws_bytes, core._stream()) == 0
+    assert _rel(y, ref) < 1e-2
