@@ -34,8 +34,10 @@ def main():
     ap.add_argument("--cfg", type=float, default=8.0)
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (use with --family tiny)")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the denoiser")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="prompt-level multi-stream overlap: job n's VAE decode on a side stream (dp.run_many)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="disable the prompt-level multi-stream overlap (job n's VAE decode + gather on a side "
+                         "stream while job n+1 samples: dp.run_many); every job still completes inside the "
+                         "timed region")
     ap.add_argument("--profile-ops", action="store_true", help="(kept for compatibility; op backends are always reported)")
     args = ap.parse_args()
 
@@ -97,8 +99,14 @@ def main():
         log(f"step {i}: {time.perf_counter() - ts:.2f}s")
         return r
 
-    for i in range(args.warmup):
-        one_step(i)
+    if args.pipeline and args.warmup:
+        jobs = (Job(**{**job.__dict__, "seed": 1000 + i}) for i in range(args.warmup))
+        with torch.inference_mode():
+            for i, _ in enumerate(gen.run_many(jobs, pipeline=True)):
+                log(f"warmup job {i} done (pipelined)")
+    else:
+        for i in range(args.warmup):
+            one_step(i)
     if not args.cpu:
         torch.cuda.synchronize()
     comm.barrier()

@@ -506,7 +506,7 @@ static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long
   const int K = a.kh * a.kw * a.Cin;
   a.tiles_n = (a.Cout + ppk::BN - 1) / ppk::BN;
   const long long T = (long long)((M + ppk::BM - 1) / ppk::BM) * a.tiles_n;
-  a.sp = ppk::Split{0, 1, nullptr, nullptr};
+  a.sp = ppk::Split{0, 1, nullptr, nullptr, 0};
   long long U = T;
   if (ws && ws_bytes >= ppk::split_ws_bytes(T, K / ppk::BK, conv_num_cus())) {
     a.sp.S = ppk::split_plan(T, K / ppk::BK, conv_num_cus(), a.sp.t_full);

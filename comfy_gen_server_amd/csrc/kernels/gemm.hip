@@ -11,6 +11,7 @@
 // lane groups and conflict-free ds_write_b128. 1-D grid with the XCD-aware bijective remap so
 // neighbouring output tiles (sharing A / W panels) run on the same XCD L2.
 #include "common.h"
+#include <stdlib.h>
 #include "mfma_core.h"
 #include "mfma_pp.h"
 #include "mfma_pp160.h"
@@ -549,7 +550,7 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
   const int tiles_n = (N + ppk::BN - 1) / ppk::BN;
   const int tiles_m = (M + ppk::BM - 1) / ppk::BM;
   const long long T = (long long)tiles_m * tiles_n;
-  ppk::Split sp{0, 1, nullptr, nullptr};
+  ppk::Split sp{0, 1, nullptr, nullptr, 0};
   long long U = T;
   if (ws && ws_bytes >= ppk::split_ws_bytes(T, K / ppk::BK, num_cus())) {
     sp.S = ppk::split_plan(T, K / ppk::BK, num_cus(), sp.t_full);
@@ -557,8 +558,12 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
       const long long tail = T - sp.t_full;
       sp.part = (float4*)ws;
       sp.cnt = (int*)((char*)ws + tail * sp.S * 32ll * ppk::THREADS * 16);
-      hipError_t err = hipMemsetAsync(sp.cnt, 0, tail * sizeof(int), stream);
-      if (err != hipSuccess) return (int)err;
+      static const int dbg = getenv("CGS_V7_SPLIT_DBG") ? atoi(getenv("CGS_V7_SPLIT_DBG")) : 0;
+      sp.dbg = dbg;
+      if (!(dbg & 2)) {
+        hipError_t err = hipMemsetAsync(sp.cnt, 0, tail * sizeof(int), stream);
+        if (err != hipSuccess) return (int)err;
+      }
       U = sp.t_full + tail * sp.S;
     }
   }

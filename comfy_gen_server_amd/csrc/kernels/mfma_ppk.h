@@ -51,6 +51,14 @@ using pp::P_B0;
 using pp::P_B1;
 
 typedef const __attribute__((address_space(4))) uint32_t* cptr_u32;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-B output store; flag 64 (probe): non-temporal (streaming) form
+__device__ __forceinline__ void store16(u16* p, uint2 lo, uint2 hi, int flags) {
+  const u32x4_t v = {lo.x, lo.y, hi.x, hi.y};
+  if (flags & 64) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+  else *reinterpret_cast<u32x4_t*>(p) = v;
+}
 
 template <bool GG>
 struct Stores {
@@ -63,6 +71,7 @@ struct Split {
   int S;             // K-ranges per tail tile (1: no split)
   float4* part;      // [tail * S][32][512] fp32 partial tiles
   int* cnt;          // [tail] arrival counters (zeroed before the launch)
+  int dbg;           // timing probes (CGS_V7_SPLIT_DBG): 1 no fences, 4 no partial reads
 };
 
 template <int EXTRA>
@@ -89,7 +98,7 @@ __device__ __forceinline__ int b_col_perm(int nq, int r) {
 template <bool GG, class AL>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m,
-                                    Split sp = Split{0, 1, nullptr, nullptr}) {
+                                    Split sp = Split{0, 1, nullptr, nullptr, 0}) {
   constexpr int E = Stores<GG>::N;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -265,8 +274,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             const float o3 = (a[3] * e.alpha + ba.w) * gelu_fast(g[3] * e.alpha + bg.w);
             h[nq] = pack4_bf16(o0, o1, o2, o3);
           }
-          if (row < M && ocol < Nout)
-            *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + ocol) = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
+          if (row < M && ocol < Nout) store16(e.C + (long long)row * e.ldc + ocol, h[0], h[1], e.flags);
         }
     } else {
       // residual words: all 16 loads issued before the first store (one wait, one drain)
@@ -308,8 +316,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
               h[j] = pack4_bf16(v0, v1, v2, v3);
             }
             const int col = ncw + nq * 32 + 8 * fq;
-            if (row < M && col < N)
-              *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
+            if (row < M && col < N) store16(e.C + (long long)row * e.ldc + col, h[0], h[1], e.flags);
           }
         }
     }
@@ -344,16 +351,21 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     __syncthreads();
     const int tile = slot / S;
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (!(sp.dbg & 1)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      mc::wait_vmcnt<0>();       // keep: the fence's own wait may be dropped, and it must precede the ticket
       const int old = __hip_atomic_fetch_add(sp.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last_flag = old == S - 1;
-      if (old == S - 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (old == S - 1) {
+        __hip_atomic_store(sp.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // self-reset
+        if (!(sp.dbg & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        mc::wait_vmcnt<0>();
+      }
     }
     __syncthreads();
     if (!last_flag) return;
     const int r0 = tile * S;
     for (int r = 0; r < S; ++r) {
-      if (r0 + r == slot) continue;
+      if (r0 + r == slot || (sp.dbg & 4)) continue;
       const float4* o = sp.part + (size_t)(r0 + r) * (32 * THREADS);
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
@@ -458,17 +470,19 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 
 // Host: split-K tail plan for T tiles of nk K-tiles on G CUs. Returns S (1 = no split) and the
 // number of whole tiles; the workspace needs tail * S * 256 KiB of partials + tail counters.
+// Cost of the last round in K-tile times (one K-tile = 256x256x64 on one CU, ~1.5 us), calibrated
+// on MI355X (tools/split_probe.py): nk / S of MFMA work + ~19 fixed (release fence + partial-slab
+// write + restart) + ~4.7 per extra slab the last arriver reads (256 KiB at one block's ~100 GB/s).
+// Short K (<= 32 K-tiles) never pays; the level-2 convs (nk = 90..360) and K = 5120 do.
 inline int split_plan(long long T, int nk, int G, int& t_full) {
   const long long tail = T % G;
   t_full = (int)(T - tail);
   if (tail == 0 || tail * 2 > G || nk < 4) return 1;
-  // last-round cost in K-tile times: nk / S of MFMA work + ~3 per extra partial the fixup reads
-  // (256 KiB at one CU's share of HBM bandwidth) + ~1.5 for writing the partials
   int best = 1;
   double best_cost = nk;
   const int smax = (int)std::min<long long>(std::min<long long>(G / tail, nk / 2), 16);
   for (int S = 2; S <= smax; ++S) {
-    const double c = (double)nk / S + 3.0 * (S - 1) + 1.5;
+    const double c = (double)nk / S + 4.7 * (S - 1) + 19.0;
     if (c < best_cost) { best_cost = c; best = S; }
   }
   return best;

@@ -43,6 +43,9 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--jobs", type=int, default=1,
+                    help="jobs per timed sample through DataParallelGenerator.run_many (CGS_DP_PIPELINE in a "
+                         "--cfg selects the pipelined form); the reported time is per job")
     args = ap.parse_args(argv)
     cfgs = []
     for c in args.cfg:
@@ -62,9 +65,15 @@ def main(argv=None):
     def job(seed):
         t = time.perf_counter()
         with torch.inference_mode():
-            gen.run(Job(batch=args.batch, steps=args.steps, width=args.res, height=args.res, seed=seed))
+            if args.jobs == 1:
+                gen.run(Job(batch=args.batch, steps=args.steps, width=args.res, height=args.res, seed=seed))
+            else:
+                jobs = (Job(batch=args.batch, steps=args.steps, width=args.res, height=args.res, seed=seed + i)
+                        for i in range(args.jobs))
+                for _ in gen.run_many(jobs):
+                    pass
         torch.cuda.synchronize()
-        return time.perf_counter() - t
+        return (time.perf_counter() - t) / args.jobs
     seed = 0
     for r in range(args.rounds + 1):
         for name, env in cfgs:

@@ -13,14 +13,8 @@ SHAPES = [(16384, 3840, 1280), (16384, 1280, 5120), (65536, 1920, 640), (4096, 4
 VARIANTS = [5, 6, 7]
 GROUPS = [1, 4, 8, 16]
 EPI = 0
-if "--quarter-stores" in sys.argv:   # v7 timing probe: epilogue stores 1/4 of the tile (flag 64)
-    EPI = 64
-if "--nowait" in sys.argv:           # v7 probe: DMA waits ignore epilogue stores for 3 K-tiles (flag 256)
-    EPI |= 256
-if "--stagger" in sys.argv:          # v7 probe: odd workgroups start half a tile late (flag 128)
-    EPI |= 128
-if "--wide16" in sys.argv:          # v7 probe: 16-B epilogue stores, 64 contiguous B per row (flag 512)
-    EPI |= 512
+if "--nt" in sys.argv:              # v7 probe: non-temporal epilogue stores (flag 64)
+    EPI |= 64
 if "--kseries" in sys.argv:        # per-tile fixed cost vs per-K-tile cost: 1024 tiles (4 rounds), K swept
     SHAPES = [(16384, 4096, k) for k in (128, 256, 640, 1280, 2560, 5120)] + [(16384, 10240, 1280), (65536, 4096, 640)]
     VARIANTS = [5, 7]

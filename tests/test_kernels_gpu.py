@@ -471,9 +471,9 @@ def test_unet_skip_concat_never_materialised(cuda):
 
 # v7 split-K tail (mfma_ppk.h): shapes whose last round of 256x256 tiles is at most half full get
 # their tail tiles cut into K ranges, reduced by the last-arriving unit of each tile.
-@pytest.mark.parametrize("M,N,K,epi", [(16384, 1280, 1280, "bias_res"), (16384, 1280, 5120, "bias"),
-                                       (1024, 1024, 2048, "none"), (1232, 2560, 2048, "bias"),
-                                       (4096, 1280, 640, "bias_res"), (16200, 1288, 1280, "bias_res")])
+@pytest.mark.parametrize("M,N,K,epi", [(16384, 1280, 5120, "bias_res"), (16384, 1280, 5120, "bias"),
+                                       (1024, 1024, 8192, "none"), (4096, 1280, 5120, "bias"),
+                                       (16200, 1288, 5120, "bias_res")])
 def test_gemm_v7_split_tail(cuda, M, N, K, epi):
     lib = _native.load_kernels()
     ws_bytes = lib.cgs_v7_ws_bytes(M, N, K)
@@ -502,7 +502,7 @@ def test_gemm_v7_split_tail(cuda, M, N, K, epi):
     assert torch.equal(outs[0], outs[1]) or _rel(outs[1], ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,N2,K", [(16384, 2560, 1280), (1024, 5120, 640)])
+@pytest.mark.parametrize("M,N2,K", [(16384, 2560, 5120), (1024, 5120, 5120)])
 def test_gemm_v7_split_tail_geglu(cuda, M, N2, K):
     lib = _native.load_kernels()
     ws_bytes = lib.cgs_v7_ws_bytes(M, N2, K)
@@ -522,7 +522,7 @@ def test_gemm_v7_split_tail_geglu(cuda, M, N2, K):
 
 
 @pytest.mark.parametrize("N,C1,C2,H,W,Cout,k,res", [(4, 1280, 0, 32, 32, 1280, 3, True), (4, 1280, 1280, 32, 32, 1280, 3, False),
-                                                    (2, 640, 0, 64, 48, 640, 3, True), (4, 2560, 0, 32, 32, 1280, 1, False)])
+                                                    (2, 640, 0, 64, 48, 640, 3, True), (4, 2560, 2560, 32, 32, 1280, 1, False)])
 def test_conv_v7_split_tail(cuda, N, C1, C2, H, W, Cout, k, res):
     """v7 conv with the buffer-load gather (ConvGatherKB) and the split-K tail, dual source included."""
     lib = _native.load_kernels()
