@@ -514,7 +514,8 @@ static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long
       const long long tail = T - a.sp.t_full;
       a.sp.part = (float4*)ws;
       a.sp.cnt = (int*)((char*)ws + tail * a.sp.S * 32ll * ppk::THREADS * 16);
-      if (hipMemsetAsync(a.sp.cnt, 0, tail * sizeof(int), stream) != hipSuccess) a.sp.S = 1;
+      ppk::zero_counters_kernel<<<1, 256, 0, stream>>>(a.sp.cnt, (int)tail);
+      if (hipGetLastError() != hipSuccess) a.sp.S = 1;
       else U = a.sp.t_full + tail * a.sp.S;
     }
   }

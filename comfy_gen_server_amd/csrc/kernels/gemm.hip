@@ -561,7 +561,8 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
       static const int dbg = getenv("CGS_V7_SPLIT_DBG") ? atoi(getenv("CGS_V7_SPLIT_DBG")) : 0;
       sp.dbg = dbg;
       if (!(dbg & 2)) {
-        hipError_t err = hipMemsetAsync(sp.cnt, 0, tail * sizeof(int), stream);
+        ppk::zero_counters_kernel<<<1, 256, 0, stream>>>(sp.cnt, (int)tail);
+        hipError_t err = hipGetLastError();
         if (err != hipSuccess) return (int)err;
       }
       U = sp.t_full + tail * sp.S;

@@ -53,11 +53,9 @@ using pp::P_B1;
 typedef const __attribute__((address_space(4))) uint32_t* cptr_u32;
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// 16-B output store; flag 64 (probe): non-temporal (streaming) form
-__device__ __forceinline__ void store16(u16* p, uint2 lo, uint2 hi, int flags) {
-  const u32x4_t v = {lo.x, lo.y, hi.x, hi.y};
-  if (flags & 64) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
-  else *reinterpret_cast<u32x4_t*>(p) = v;
+// 16-B output store (non-temporal stores measured no better: tools/gemm_sweep.py history)
+__device__ __forceinline__ void store16(u16* p, uint2 lo, uint2 hi, int) {
+  *reinterpret_cast<u32x4_t*>(p) = u32x4_t{lo.x, lo.y, hi.x, hi.y};
 }
 
 template <bool GG>
@@ -486,6 +484,14 @@ inline int split_plan(long long T, int nk, int G, int& t_full) {
     if (c < best_cost) { best_cost = c; best = S; }
   }
   return best;
+}
+
+// Zero the tail-tile arrival counters ahead of the launch with a kernel, not hipMemsetAsync: a
+// memset issued on a capturing stream did not replay as part of the hipGraph here (replays with new
+// inputs saw stale counters -> unreduced tail tiles), while a kernel launch is captured like the
+// GEMM itself.
+static __global__ void zero_counters_kernel(int* cnt, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) cnt[i] = 0;
 }
 
 inline long long split_ws_bytes(long long T, int nk, int G) {

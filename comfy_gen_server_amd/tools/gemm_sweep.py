@@ -13,8 +13,6 @@ SHAPES = [(16384, 3840, 1280), (16384, 1280, 5120), (65536, 1920, 640), (4096, 4
 VARIANTS = [5, 6, 7]
 GROUPS = [1, 4, 8, 16]
 EPI = 0
-if "--nt" in sys.argv:              # v7 probe: non-temporal epilogue stores (flag 64)
-    EPI |= 64
 if "--kseries" in sys.argv:        # per-tile fixed cost vs per-K-tile cost: 1024 tiles (4 rounds), K swept
     SHAPES = [(16384, 4096, k) for k in (128, 256, 640, 1280, 2560, 5120)] + [(16384, 10240, 1280), (65536, 4096, 640)]
     VARIANTS = [5, 7]

@@ -159,3 +159,46 @@ def test_step_graph_with_controlnet_matches_eager(cuda, monkeypatch, window):
         err = (a - b).abs().max().item()
         assert err < 2e-2 * (a.abs().max().item() + 1), err
     assert (res["1"][0] - res["1"][1]).abs().max() > 1e-3     # different hints -> different images
+
+
+@pytest.mark.gpu
+def test_split_k_tail_inside_captured_graph(cuda):
+    """The v7 split-K tail (arrival counters zeroed by a kernel node ahead of the GEMM) replays
+    correctly from a hipGraph with NEW inputs -- a memset on the capturing stream did not."""
+    from comfy_gen_server_amd import _native
+    from comfy_gen_server_amd.ops import core
+    lib = _native.load_kernels()
+    M, N, K = 16384, 1280, 5120
+    assert lib.cgs_v7_ws_bytes(M, N, K) > 0
+    lib.cgs_gemm_set_variant(7)
+    try:
+        with torch.inference_mode():
+            a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+            w = (torch.randn(N, K, device=cuda) / K ** 0.5).to(torch.bfloat16)
+            b = torch.randn(N, device=cuda).to(torch.bfloat16)
+            ws = torch.empty(lib.cgs_v7_ws_bytes(M, N, K), dtype=torch.uint8, device=cuda)
+            out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+
+            def call():
+                assert lib.cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), None, M, N, K,
+                                              K, K, N, 0, 1, 1.0, ws.data_ptr(), ws.numel(), core._stream()) == 0
+            call()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    call()
+            torch.cuda.current_stream().wait_stream(s)
+            for seed in (1, 2):
+                torch.manual_seed(seed)
+                a.copy_(torch.randn(M, K, device=cuda).to(torch.bfloat16))
+                ws.fill_(0x7F)                     # poison partials and counters between replays
+                g.replay()
+                torch.cuda.synchronize()
+                ref = a.float() @ w.float().t() + b.float()
+                err = ((out.float() - ref).norm() / ref.norm()).item()
+                assert err < 1e-2, (seed, err)
+    finally:
+        lib.cgs_gemm_set_variant(-1)
