@@ -127,6 +127,11 @@ KERNEL_SIGNATURES = {
     "cgs_step_advance": [_P, _P],
     "cgs_vae_out_u8": [_P, _P, _L, _P],                                # bf16 NHWC -> uint8 image (K23)
     "cgs_conv2d_nhwc_ex": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    # K17/K24 region accumulate: out, div, piece, pdt, mult, mdt, B, C, Ho, Wo, h, w, oy, ox, piece strides x4,
+    # Cm, mult strides x4, feather, scale
+    "cgs_region_accumulate": [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _L, _L, _L, _L, _I, _L, _L,
+                              _L, _L, _I, _F, _P],
+    "cgs_region_normalize": [_P, _P, _P, _L, _I, _P],
     # v7 split-K tail: workspace bytes for (M, N, K) and the GEMM / conv launchers that take it
     "cgs_v7_ws_bytes": [_I, _I, _I],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],

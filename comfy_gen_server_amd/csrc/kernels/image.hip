@@ -231,6 +231,58 @@ __global__ void __launch_bounds__(256) grn_apply_kernel(const void* x, const flo
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K17 / K24: weighted accumulate of a piece into a region of an fp32 [B, C, Ho, Wo] accumulator
+// pair (reference comfy/samplers.py:205-228 area/mask conds; comfy/utils.py tiled_scale feather):
+//   out[b, c, oy + y, ox + x] += piece[b, c, y, x] * w(b, c, y, x);  div[...] += w(b, c, y, x)
+// w = mult tensor [B, Cm, h, w] (Cm = 1 broadcasts over channels; any strides, any float dtype),
+// times the separable feather ramp of the reference tiled blend when feather > 0 (rows / cols
+// within `feather` of a tile edge scaled by (t+1)/feather, both edges when the tile is small),
+// times `scale`. piece: any strides / float dtype. One thread per element of the piece.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float feather_ramp(int t, int n, int f) {
+  float a = 1.f;
+  if (t < f) a *= (float)(t + 1) / (float)f;
+  if (n - 1 - t < f) a *= (float)(n - t) / (float)f;
+  return a;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) region_acc_kernel(float* out, float* div, const void* piece, const void* mult,
+                                                         int mdt, int B, int C, int Ho, int Wo, int h, int w, int oy,
+                                                         int ox, long long ps0, long long ps1, long long ps2,
+                                                         long long ps3, int Cm, long long ms0, long long ms1,
+                                                         long long ms2, long long ms3, int feather, float scale) {
+  const long long total = (long long)B * C * h * w;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int x = (int)(i % w);
+    const int y = (int)((i / w) % h);
+    const int c = (int)((i / ((long long)w * h)) % C);
+    const int b = (int)(i / ((long long)w * h * C));
+    const int Y = oy + y, X = ox + x;
+    if (Y < 0 || Y >= Ho || X < 0 || X >= Wo) continue;
+    float wt = scale;
+    if (mult) {
+      const long long mi = b * ms0 + (Cm == 1 ? 0 : c) * ms1 + y * ms2 + x * ms3;
+      wt *= mdt == CGS_F32 ? ldv<CGS_F32>(mult, mi) : mdt == CGS_BF16 ? ldv<CGS_BF16>(mult, mi)
+                                                                       : ldv<CGS_F16>(mult, mi);
+    }
+    if (feather > 0) wt *= feather_ramp(y, h, feather) * feather_ramp(x, w, feather);
+    const float v = ldv<DT>(piece, b * ps0 + c * ps1 + y * ps2 + x * ps3);
+    const long long o = (((long long)b * C + c) * Ho + Y) * Wo + X;
+    out[o] += v * wt;
+    if (div) div[o] += wt;
+  }
+}
+
+// y = out / div (fp32 -> dtype of y), the final normalisation of both accumulations
+template <int DT>
+__global__ void __launch_bounds__(256) region_norm_kernel(const float* out, const float* div, void* y, long long n) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    stv<DT>(y, i, out[i] / div[i]);
+}
+
 }  // namespace
 
 CGS_EXPORT int cgs_fused_bias_act(const void* x, const void* b, void* y, long long n, int C, long long inner,
@@ -354,5 +406,26 @@ CGS_EXPORT int cgs_vae_out_u8(const void* x, void* y, long long n, hipStream_t s
   long long b = (n / 8 + 255) / 256;
   const int blocks = (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
   vae_out_u8_kernel<<<blocks, 256, 0, stream>>>((const u16*)x, (uint8_t*)y, n);
+  return (int)hipGetLastError();
+}
+
+// K17 / K24 region accumulate (see region_acc_kernel). Strides in elements; mult may be null.
+CGS_EXPORT int cgs_region_accumulate(float* out, float* div, const void* piece, int pdt, const void* mult, int mdt,
+                                     int B, int C, int Ho, int Wo, int h, int w, int oy, int ox, long long ps0,
+                                     long long ps1, long long ps2, long long ps3, int Cm, long long ms0, long long ms1,
+                                     long long ms2, long long ms3, int feather, float scale, hipStream_t stream) {
+  const long long n = (long long)B * C * h * w;
+  if (n <= 0) return 0;
+  if (!out || (Cm != 1 && Cm != C)) return (int)hipErrorInvalidValue;
+  CGS_DISPATCH_DT(pdt, region_acc_kernel, <<<grid_for(n), 256, 0, stream>>>(out, div, piece, mult, mdt, B, C, Ho, Wo,
+                                                                            h, w, oy, ox, ps0, ps1, ps2, ps3, Cm, ms0,
+                                                                            ms1, ms2, ms3, feather, scale));
+  return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_region_normalize(const float* out, const float* div, void* y, long long n, int ydt,
+                                    hipStream_t stream) {
+  if (n <= 0) return 0;
+  CGS_DISPATCH_DT(ydt, region_norm_kernel, <<<grid_for(n), 256, 0, stream>>>(out, div, y, n));
   return (int)hipGetLastError();
 }

@@ -725,6 +725,69 @@ def interpolate(x: torch.Tensor, size, mode: str = "nearest", align_corners: boo
     return F.interpolate(x, size=(Ho, Wo), mode=mode, **kw)
 
 
+def _feather_mask(h: int, w: int, feather: int, device) -> torch.Tensor:
+    """Separable ramp of the reference tiled blend (comfy/utils.py tiled_scale)."""
+    def ramp(n):
+        t = torch.arange(n, device=device, dtype=torch.float32)
+        a = torch.ones(n, device=device)
+        a = torch.where(t < feather, a * (t + 1) / feather, a)
+        a = torch.where(n - 1 - t < feather, a * (n - t) / feather, a)
+        return a
+    return ramp(h)[:, None] * ramp(w)[None, :]
+
+
+def region_accumulate(out: torch.Tensor, div: torch.Tensor | None, piece: torch.Tensor, oy: int, ox: int,
+                      mult: torch.Tensor | None = None, feather: int = 0, scale: float = 1.0):
+    """In place: ``out[:, :, oy:oy+h, ox:ox+w] += piece * wt`` and ``div[...] += wt`` with
+    ``wt = scale * mult (broadcast over channels when it has one) * feather ramp`` -- the area /
+    mask cond accumulation of ``calc_cond_batch`` (K17, reference comfy/samplers.py:205-228) and the
+    feathered tile blend of ``tiled_scale`` (K24). ``out`` / ``div``: fp32 [B, C, Ho, Wo] contiguous.
+    Device path: one HIP kernel (any piece / mult strides and float dtype), no temporaries."""
+    B, C, h, w = piece.shape
+    be = backend_for("region_acc", out, "cgs_region_accumulate")
+    if (be == "hip" and out.dtype == torch.float32 and out.is_contiguous() and piece.dtype in _DT
+            and (div is None or (div.shape == out.shape and div.dtype == torch.float32 and div.is_contiguous()))
+            and (mult is None or (mult.dim() == 4 and mult.dtype in _DT and mult.shape[1] in (1, C)))):
+        count("region_acc", "hip")
+        Ho, Wo = out.shape[2], out.shape[3]
+        if mult is not None:
+            mult = mult.expand(B, mult.shape[1], h, w)
+            ms = mult.stride()
+        else:
+            ms = (0, 0, 0, 0)
+        ps = piece.stride()
+        _check(_lib().cgs_region_accumulate(out.data_ptr(), _ptr(div), piece.data_ptr(), _DT[piece.dtype],
+                                            _ptr(mult), _DT[mult.dtype] if mult is not None else 0, B, C, Ho, Wo,
+                                            h, w, int(oy), int(ox), ps[0], ps[1], ps[2], ps[3],
+                                            1 if mult is None else mult.shape[1], ms[0], ms[1], ms[2], ms[3],
+                                            int(feather), float(scale), _stream()), "cgs_region_accumulate")
+        return
+    count("region_acc", "torch")
+    wt = torch.full((1, 1, h, w), float(scale), device=out.device, dtype=torch.float32)
+    if feather > 0:
+        wt = wt * _feather_mask(h, w, feather, out.device)
+    if mult is not None:
+        wt = wt * mult.float()
+    hh, ww = min(h, out.shape[2] - oy), min(w, out.shape[3] - ox)
+    wt = wt.expand(B, -1, h, w)[:, :, :hh, :ww]
+    out[:, :, oy:oy + hh, ox:ox + ww] += piece[:, :, :hh, :ww].float() * wt
+    if div is not None:
+        div[:, :, oy:oy + hh, ox:ox + ww] += wt.expand(B, C, hh, ww) if wt.shape[1] == 1 else wt
+
+
+def region_normalize(out: torch.Tensor, div: torch.Tensor, dtype=None) -> torch.Tensor:
+    """``(out / div).to(dtype)`` (the final step of both accumulations) in one kernel."""
+    dtype = dtype or out.dtype
+    be = backend_for("region_acc", out, "cgs_region_normalize")
+    if be == "hip" and out.is_contiguous() and div.is_contiguous() and dtype in _DT and div.dtype == torch.float32:
+        count("region_acc", "hip")
+        y = torch.empty(out.shape, device=out.device, dtype=dtype)
+        _check(_lib().cgs_region_normalize(out.data_ptr(), div.data_ptr(), y.data_ptr(), out.numel(), _DT[dtype],
+                                           _stream()), "cgs_region_normalize")
+        return y
+    return (out / div).to(dtype)
+
+
 def fused_bias_act(x: torch.Tensor, bias: torch.Tensor | None, negative_slope: float = 0.2,
                    scale: float = 2 ** 0.5) -> torch.Tensor:
     """StyleGAN2 FusedLeakyReLU (K32, ``face/fused_act.py``): leaky_relu(x + bias[c]) * scale,

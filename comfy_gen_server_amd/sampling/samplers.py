@@ -25,6 +25,8 @@ import math
 
 import torch
 
+from .. import ops
+
 from ..runtime import device as dm
 from ..utils import telemetry
 from . import k_samplers as kds
@@ -210,9 +212,9 @@ def calc_cond_batch(model, conds, x_in, timestep, model_options):
         outs, order = _run_batch(model, batch, timestep, model_options)
         for o, (p, ci) in zip(outs, batch):
             a = p.area
-            out_conds[ci][:, :, a[2]:a[0] + a[2], a[3]:a[1] + a[3]] += o * p.mult
-            out_counts[ci][:, :, a[2]:a[0] + a[2], a[3]:a[1] + a[3]] += p.mult
-    return [oc / cnt for oc, cnt in zip(out_conds, out_counts)]
+            # out[area] += o * mult ; count[area] += mult (one HIP kernel on the device, K17)
+            ops.region_accumulate(out_conds[ci], out_counts[ci], o, a[2], a[3], mult=p.mult)
+    return [ops.region_normalize(oc, cnt) for oc, cnt in zip(out_conds, out_counts)]
 
 
 def calc_cond_uncond_batch(model, cond, uncond, x_in, timestep, model_options):

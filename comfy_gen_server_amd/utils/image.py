@@ -99,6 +99,7 @@ def get_tiled_scale_steps(width, height, tile_x, tile_y, overlap):
 @torch.inference_mode()
 def tiled_scale(samples, function, tile_x=64, tile_y=64, overlap=8, upscale_amount=4, out_channels=3,
                 output_device="cpu", pbar=None):
+    from .. import ops
     out_full = torch.empty((samples.shape[0], out_channels, round(samples.shape[2] * upscale_amount),
                             round(samples.shape[3] * upscale_amount)), device=output_device)
     for b in range(samples.shape[0]):
@@ -112,20 +113,13 @@ def tiled_scale(samples, function, tile_x=64, tile_y=64, overlap=8, upscale_amou
                 y0 = max(0, min(s.shape[-2] - overlap, y))
                 piece = s[:, :, y0:y0 + tile_y, x0:x0 + tile_x]
                 ps = function(piece).to(output_device)
-                mask = torch.ones_like(ps)
                 feather = round(overlap * upscale_amount)
-                for t in range(feather):
-                    a = (1.0 / feather) * (t + 1)
-                    mask[:, :, t:1 + t, :] *= a
-                    mask[:, :, mask.shape[2] - 1 - t:mask.shape[2] - t, :] *= a
-                    mask[:, :, :, t:1 + t] *= a
-                    mask[:, :, :, mask.shape[3] - 1 - t:mask.shape[3] - t] *= a
                 oy, ox = round(y0 * upscale_amount), round(x0 * upscale_amount)
-                out[:, :, oy:oy + ps.shape[2], ox:ox + ps.shape[3]] += ps * mask
-                div[:, :, oy:oy + ps.shape[2], ox:ox + ps.shape[3]] += mask
+                # out += piece * ramp ; div += ramp (separable feather ramp; one HIP kernel, K24)
+                ops.region_accumulate(out, div, ps, oy, ox, feather=feather)
                 if pbar is not None:
                     pbar.update(1)
-        out_full[b:b + 1] = out / div
+        out_full[b:b + 1] = ops.region_normalize(out, div)
     return out_full
 
 

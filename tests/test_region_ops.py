@@ -1,0 +1,56 @@
+"""K17 / K24 region accumulate: the cond area/mask accumulation of calc_cond_batch (reference
+comfy/samplers.py:205-228) and the feathered tile blend of tiled_scale (comfy/utils.py)."""
+import pytest
+import torch
+
+from comfy_gen_server_amd import ops
+
+
+def _feather_ref(ps, feather):
+    mask = torch.ones_like(ps)
+    for t in range(feather):                       # the reference's loop form
+        a = (1.0 / feather) * (t + 1)
+        mask[:, :, t:1 + t, :] *= a
+        mask[:, :, mask.shape[2] - 1 - t:mask.shape[2] - t, :] *= a
+        mask[:, :, :, t:1 + t] *= a
+        mask[:, :, :, mask.shape[3] - 1 - t:mask.shape[3] - t] *= a
+    return mask
+
+
+def _check(dev, dtype):
+    g = torch.Generator().manual_seed(0)
+    out = torch.zeros(2, 3, 20, 24)
+    div = torch.ones(2, 3, 20, 24) * 1e-37
+    ref_o, ref_d = out.clone(), div.clone()
+    piece = torch.randn(2, 3, 9, 11, generator=g)
+    mult = torch.rand(2, 1, 9, 11, generator=g)
+    # area + mask (mult broadcast over channels), a strided piece
+    o_dev, d_dev = out.to(dev), div.to(dev)
+    pd = torch.randn(2, 11, 9, 3, generator=g)
+    piece_strided = pd.permute(0, 3, 2, 1)
+    ops.region_accumulate(o_dev, d_dev, piece_strided.to(dev, dtype), 5, 7, mult=mult.to(dev, dtype))
+    ref_o[:, :, 5:14, 7:18] += piece_strided.to(dtype).float() * mult.to(dtype).float()
+    ref_d[:, :, 5:14, 7:18] += mult.to(dtype).float()
+    # feathered tile, clipped at the border
+    ps = torch.randn(2, 3, 8, 8, generator=g)
+    ops.region_accumulate(o_dev, d_dev, ps.to(dev, dtype), 14, 18, feather=3)
+    m = _feather_ref(ps, 3)[:, :, :6, :6]
+    ref_o[:, :, 14:20, 18:24] += ps.to(dtype).float()[:, :, :6, :6] * m
+    ref_d[:, :, 14:20, 18:24] += m
+    y = ops.region_normalize(o_dev, d_dev)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert torch.allclose(o_dev.cpu(), ref_o, atol=tol, rtol=tol)
+    assert torch.allclose(d_dev.cpu(), ref_d, atol=tol, rtol=tol)
+    assert torch.allclose(y.cpu(), ref_o / ref_d, atol=tol * 10, rtol=tol * 10)
+
+
+def test_region_accumulate_cpu():
+    _check(torch.device("cpu"), torch.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_region_accumulate_hip(cuda, dtype):
+    ops.reset_stats()
+    _check(cuda, dtype)
+    assert ops.stats().get(("region_acc", "hip"), 0) == 3
