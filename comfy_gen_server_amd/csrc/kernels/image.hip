@@ -283,6 +283,56 @@ __global__ void __launch_bounds__(256) region_norm_kernel(const float* out, cons
     stv<DT>(y, i, out[i] / div[i]);
 }
 
+// ---------------------------------------------------------------------------------------------
+// K26: CLIP text embeddings (reference comfy/clip_model.py CLIPEmbeddings + the pooled gather of
+// CLIPTextModel_): y[b, s, :] = tok[ids[b, s], :] + pos[s, :]; pooled[b, :] = x[b, argmax_s ids[b, s]]
+// (first maximum, like torch.argmax). One thread per output element / one block per pooled row.
+// ---------------------------------------------------------------------------------------------
+template <int DT>
+__global__ void __launch_bounds__(256) clip_embed_kernel(const long long* ids, const void* tok, const void* pos,
+                                                         void* y, int B, int S, int D, int vocab) {
+  const long long total = (long long)B * S * D;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int d = (int)(i % D);
+    const long long bs = i / D;
+    const int s = (int)(bs % S);
+    long long id = ids[bs];
+    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+    stv<DT>(y, i, ldv<DT>(tok, id * D + d) + ldv<DT>(pos, (long long)s * D + d));
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) pooled_gather_kernel(const long long* ids, const void* x, void* out, int S,
+                                                            int D) {
+  const int b = blockIdx.x;
+  __shared__ long long best_v[256];
+  __shared__ int best_i[256];
+  long long bv = -(1ll << 62);
+  int bi = 0;
+  for (int s = threadIdx.x; s < S; s += 256) {
+    const long long v = ids[(long long)b * S + s];
+    if (v > bv) { bv = v; bi = s; }
+  }
+  best_v[threadIdx.x] = bv;
+  best_i[threadIdx.x] = bi;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      const long long ov = best_v[threadIdx.x + w];
+      const int oi = best_i[threadIdx.x + w];
+      if (ov > best_v[threadIdx.x] || (ov == best_v[threadIdx.x] && oi < best_i[threadIdx.x])) {
+        best_v[threadIdx.x] = ov;
+        best_i[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  const int s = best_i[0];
+  for (int d = threadIdx.x; d < D; d += 256)
+    stv<DT>(out, (long long)b * D + d, ldv<DT>(x, ((long long)b * S + s) * D + d));
+}
+
 }  // namespace
 
 CGS_EXPORT int cgs_fused_bias_act(const void* x, const void* b, void* y, long long n, int C, long long inner,
@@ -427,5 +477,22 @@ CGS_EXPORT int cgs_region_normalize(const float* out, const float* div, void* y,
                                     hipStream_t stream) {
   if (n <= 0) return 0;
   CGS_DISPATCH_DT(ydt, region_norm_kernel, <<<grid_for(n), 256, 0, stream>>>(out, div, y, n));
+  return (int)hipGetLastError();
+}
+
+// K26: token + position embeddings (ids int64 [B, S]; tok [vocab, D]; pos [>=S, D]; y [B, S, D])
+CGS_EXPORT int cgs_clip_embed(const long long* ids, const void* tok, const void* pos, void* y, int B, int S, int D,
+                              int vocab, int dtype, hipStream_t stream) {
+  const long long n = (long long)B * S * D;
+  if (n <= 0) return 0;
+  CGS_DISPATCH_DT(dtype, clip_embed_kernel, <<<grid_for(n), 256, 0, stream>>>(ids, tok, pos, y, B, S, D, vocab));
+  return (int)hipGetLastError();
+}
+
+// K26: pooled[b] = x[b, argmax(ids[b])] (x [B, S, D] contiguous)
+CGS_EXPORT int cgs_pooled_gather(const long long* ids, const void* x, void* out, int B, int S, int D, int dtype,
+                                 hipStream_t stream) {
+  if (B <= 0) return 0;
+  CGS_DISPATCH_DT(dtype, pooled_gather_kernel, <<<B, 256, 0, stream>>>(ids, x, out, S, D));
   return (int)hipGetLastError();
 }

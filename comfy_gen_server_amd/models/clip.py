@@ -98,8 +98,11 @@ class CLIPEmbeddings(nn.Module):
         self.position_embedding = Embedding(num_positions, embed_dim, dtype=dtype, device=device)
 
     def forward(self, tokens, embeds=None):
+        tw, pw = self.token_embedding.weight, self.position_embedding.weight
+        if embeds is None and tokens.device == tw.device and tw.dtype == pw.dtype:
+            return ops.clip_embed(tokens, tw, pw)          # gather + position add, one kernel (K26)
         x = self.token_embedding(tokens) if embeds is None else embeds
-        return x + self.position_embedding.weight[: x.shape[1]].to(x.dtype)
+        return x + pw[: x.shape[1]].to(x.dtype)
 
 
 class CLIPTextModel_(nn.Module):
@@ -118,7 +121,7 @@ class CLIPTextModel_(nn.Module):
         x = self.final_layer_norm(x)
         if inter is not None and final_layer_norm_intermediate:
             inter = self.final_layer_norm(inter)
-        pooled = x[torch.arange(x.shape[0], device=x.device), tokens.to(torch.long).argmax(dim=-1)]
+        pooled = ops.pooled_gather(x, tokens)             # hidden state at the end-of-text token (K26)
         return x, inter, pooled
 
 

@@ -19,5 +19,5 @@ from .core import (  # noqa: F401
     upsample_nearest2x, timestep_embedding, cfg_combine, euler_step, depthwise_conv2d_nhwc,
     interpolate, fused_bias_act, upfirdn2d, upfirdn2d_reference, vq_nearest, grn_nhwc, softmax_rows,
     attention_with_probs, philox_randn, euler_ancestral_philox, brownian_increment, step_param, sampler_step_dev,
-    step_advance, vae_out_u8, region_accumulate, region_normalize,
+    step_advance, vae_out_u8, region_accumulate, region_normalize, clip_embed, pooled_gather,
 )

@@ -725,6 +725,39 @@ def interpolate(x: torch.Tensor, size, mode: str = "nearest", align_corners: boo
     return F.interpolate(x, size=(Ho, Wo), mode=mode, **kw)
 
 
+def clip_embed(ids: torch.Tensor, tok_weight: torch.Tensor, pos_weight: torch.Tensor) -> torch.Tensor:
+    """``tok_weight[ids] + pos_weight[:S]`` (K26: CLIP token + position embedding, one kernel)."""
+    B, S = ids.shape
+    be = backend_for("clip_embed", tok_weight, "cgs_clip_embed")
+    if (be == "hip" and tok_weight.dtype in _DT and pos_weight.dtype == tok_weight.dtype and ids.device == tok_weight.device
+            and pos_weight.shape[0] >= S):
+        count("clip_embed", "hip")
+        D = tok_weight.shape[1]
+        idc = ids.to(torch.long).contiguous()
+        tw, pw = tok_weight.contiguous(), pos_weight.contiguous()
+        y = torch.empty((B, S, D), device=tw.device, dtype=tw.dtype)
+        _check(_lib().cgs_clip_embed(idc.data_ptr(), tw.data_ptr(), pw.data_ptr(), y.data_ptr(), B, S, D,
+                                     tw.shape[0], _DT[tw.dtype], _stream()), "cgs_clip_embed")
+        return y
+    count("clip_embed", "torch")
+    return F.embedding(ids.to(torch.long), tok_weight) + pos_weight[:S].to(tok_weight.dtype)
+
+
+def pooled_gather(x: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """``x[b, argmax(ids[b])]`` (K26: CLIP pooled output at the end-of-text token)."""
+    B, S, D = x.shape
+    be = backend_for("clip_embed", x, "cgs_pooled_gather")
+    if be == "hip" and x.dtype in _DT and ids.device == x.device:
+        count("clip_embed", "hip")
+        xc = x.contiguous()
+        idc = ids.to(torch.long).contiguous()
+        out = torch.empty((B, D), device=x.device, dtype=x.dtype)
+        _check(_lib().cgs_pooled_gather(idc.data_ptr(), xc.data_ptr(), out.data_ptr(), B, S, D, _DT[x.dtype],
+                                        _stream()), "cgs_pooled_gather")
+        return out
+    return x[torch.arange(B, device=x.device), ids.to(device=x.device, dtype=torch.long).argmax(dim=-1)]
+
+
 def _feather_mask(h: int, w: int, feather: int, device) -> torch.Tensor:
     """Separable ramp of the reference tiled blend (comfy/utils.py tiled_scale)."""
     def ramp(n):

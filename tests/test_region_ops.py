@@ -54,3 +54,31 @@ def test_region_accumulate_hip(cuda, dtype):
     ops.reset_stats()
     _check(cuda, dtype)
     assert ops.stats().get(("region_acc", "hip"), 0) == 3
+
+
+def _clip_check(dev, dtype):
+    g = torch.Generator().manual_seed(0)
+    tok = torch.randn(100, 16, generator=g).to(dev, dtype)
+    pos = torch.randn(77, 16, generator=g).to(dev, dtype)
+    ids = torch.randint(0, 100, (3, 9), generator=g)
+    ids[1, 4] = 99
+    ids[1, 6] = 99                                      # ties: the first maximum wins (torch.argmax)
+    y = ops.clip_embed(ids.to(dev), tok, pos)
+    ref = tok.float().cpu()[ids] + pos.float().cpu()[:9]
+    assert torch.allclose(y.float().cpu(), ref, atol=1e-2 if dtype != torch.float32 else 1e-6)
+    x = torch.randn(3, 9, 16, generator=g).to(dev, dtype)
+    p = ops.pooled_gather(x, ids.to(dev))
+    refp = x.cpu()[torch.arange(3), ids.argmax(dim=-1)]
+    assert torch.equal(p.cpu(), refp)
+
+
+def test_clip_embed_cpu():
+    _clip_check(torch.device("cpu"), torch.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_clip_embed_hip(cuda, dtype):
+    ops.reset_stats()
+    _clip_check(cuda, dtype)
+    assert ops.stats().get(("clip_embed", "hip"), 0) == 2
