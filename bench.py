@@ -99,6 +99,10 @@ def main():
         log(f"step {i}: {time.perf_counter() - ts:.2f}s")
         return r
 
+    # pipelined serving is on for one GPU; with N ranks the image all-gather would run on the side
+    # stream concurrently with the next job's broadcast, which only CGS_DP_PIPELINE_MULTI=1 enables
+    # (the 1-GPU A/B gain is < 1 %, not worth an unexercised collective ordering at N > 1).
+    args.pipeline = args.pipeline and (N == 1 or os.environ.get("CGS_DP_PIPELINE_MULTI", "0") == "1")
     if args.pipeline and args.warmup:
         jobs = (Job(**{**job.__dict__, "seed": 1000 + i}) for i in range(args.warmup))
         with torch.inference_mode():

@@ -111,6 +111,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--tune-file", type=str, default=None, help="persist per-shape kernel choices (JSON)")
     p.add_argument("--hbm-budget-gb", type=float, default=None, help="residency budget per GPU (default 90%%)")
     p.add_argument("--hip-graphs", action="store_true", help="capture denoiser steps in hipGraphs")
+    p.add_argument("--alloc-expandable", action="store_true",
+                   help="caching allocator with expandable segments (runtime/alloc_policy.py)")
     p.add_argument("--queue-journal", type=str, default=None, help="JSONL journal: queued prompts survive restarts")
     p.add_argument("--profile-dir", type=str, default=None,
                    help="write a Perfetto/Chrome trace (torch.profiler, HIP kernels + node/step ranges) per prompt")
@@ -145,7 +147,7 @@ def parse(argv=None):
     if getattr(args, "profile_dir", None):
         os.environ["CGS_PROFILE_DIR"] = args.profile_dir
     for flag in ("directml", "use_split_cross_attention", "use_quad_cross_attention", "disable_xformers",
-                 "disable_ipex_optimize", "cuda_malloc", "disable_cuda_malloc"):
+                 "disable_ipex_optimize"):
         if getattr(args, flag, None):
             logging.info("--%s accepted for compatibility; ignored on MI355X (per-shape autotuned kernels)",
                          flag.replace("_", "-"))

@@ -173,6 +173,8 @@ def build_server(args, loop):
 def main(argv=None):
     cli_args.enable_args_parsing()
     args = cli_args.parse(argv)
+    from .runtime import alloc_policy
+    logging.info("HBM allocator: %s", alloc_policy.configure(args))   # before any device allocation
     from .graph import registry
     if not args.disable_custom_nodes:
         registry.execute_prestartup_scripts(
