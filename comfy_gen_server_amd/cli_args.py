@@ -111,6 +111,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--tune-file", type=str, default=None, help="persist per-shape kernel choices (JSON)")
     p.add_argument("--hbm-budget-gb", type=float, default=None, help="residency budget per GPU (default 90%%)")
     p.add_argument("--hip-graphs", action="store_true", help="capture denoiser steps in hipGraphs")
+    p.add_argument("--weight-arena-gb", type=float, default=None,
+                   help="place resident model weights in one HBM slab of this size per GPU (runtime/arena.py)")
     p.add_argument("--alloc-expandable", action="store_true",
                    help="caching allocator with expandable segments (runtime/alloc_policy.py)")
     p.add_argument("--queue-journal", type=str, default=None, help="JSONL journal: queued prompts survive restarts")

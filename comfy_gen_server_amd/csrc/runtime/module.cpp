@@ -94,6 +94,23 @@ PYBIND11_MODULE(_cgs_runtime, m) {
       .def("encode_word", &BPE::encode_word)
       .def("vocab_size", &BPE::vocab_size);
 
+  py::class_<Arena>(m, "Arena")
+      .def(py::init<uint64_t, uint64_t>(), py::arg("capacity"), py::arg("align") = 256)
+      .def("alloc", &Arena::alloc)
+      .def("free", &Arena::free)
+      .def_property_readonly("align", &Arena::align)
+      .def("stats", [](const Arena& a) {
+        const ArenaStats s = a.stats();
+        py::dict d;
+        d["capacity"] = s.capacity;
+        d["used"] = s.used;
+        d["peak"] = s.peak;
+        d["largest_free"] = s.largest_free;
+        d["free_blocks"] = s.free_blocks;
+        d["live_blocks"] = s.live_blocks;
+        return d;
+      });
+
   m.def("blake3_hex", [](py::bytes data, size_t out_len) {
     std::string s = data;
     py::gil_scoped_release nogil;

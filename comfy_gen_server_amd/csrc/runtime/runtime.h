@@ -13,6 +13,31 @@
 
 namespace cgs {
 
+// ---- HBM weight-arena offset allocator (arena.cpp)
+struct ArenaStats {
+  uint64_t capacity = 0, used = 0, peak = 0, largest_free = 0;
+  size_t free_blocks = 0, live_blocks = 0;
+};
+
+class Arena {
+ public:
+  explicit Arena(uint64_t capacity, uint64_t align = 256);
+  int64_t alloc(uint64_t bytes);      // byte offset, or -1 when no free block fits
+  bool free(uint64_t off);            // false for an offset that is not a live block
+  ArenaStats stats() const;
+  uint64_t align() const { return align_; }
+
+ private:
+  void insert_free(uint64_t off, uint64_t size);
+  void erase_free(uint64_t off, uint64_t size);
+  uint64_t cap_, align_;
+  uint64_t in_use_ = 0, peak_ = 0;
+  std::map<uint64_t, uint64_t> by_off_;        // free: offset -> size
+  std::multimap<uint64_t, uint64_t> by_size_;  // free: size -> offset
+  std::map<uint64_t, uint64_t> used_;          // live: offset -> size
+  mutable std::mutex mu_;
+};
+
 // ---- BLAKE3 (blake3.cpp)
 std::string blake3_hex(const uint8_t* data, size_t len, size_t out_len = 32);
 std::string blake3_file_hex(const std::string& path);

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -94,6 +95,35 @@ int main(int argc, char** argv) {
     for (auto& th : pool) th.join();
   }
   if (bad) return fail("bpe concurrent");
+  // ---- weight-arena allocator: concurrent alloc/free, blocks never overlap, all coalesce back
+  {
+    Arena arena(256ull << 20);
+    std::mutex mu;
+    std::vector<std::pair<int64_t, uint64_t>> live;
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+      pool.emplace_back([&, t] {
+        uint64_t state = 0x9E3779B97F4A7C15ull * (t + 1);
+        std::vector<int64_t> mine;
+        for (int r = 0; r < 2000; ++r) {
+          state ^= state << 13; state ^= state >> 7; state ^= state << 17;
+          if (!mine.empty() && (state & 3) == 0) {
+            if (!arena.free((uint64_t)mine.back())) bad++;
+            mine.pop_back();
+          } else {
+            const uint64_t n = 1 + state % (1u << 20);
+            const int64_t off = arena.alloc(n);
+            if (off >= 0) mine.push_back(off);
+          }
+        }
+        for (int64_t off : mine)
+          if (!arena.free((uint64_t)off)) bad++;
+      });
+    for (auto& th : pool) th.join();
+    const ArenaStats st = arena.stats();
+    if (st.used != 0 || st.free_blocks != 1 || st.live_blocks != 0) bad++;
+  }
+  if (bad) return fail("arena concurrent");
   std::remove(path.c_str());
   std::printf("stress ok (%d threads)\n", threads);
   return 0;

@@ -36,6 +36,8 @@ def apply_args(args):
         os.environ["CGS_TUNE_FILE"] = args.tune_file
     if args.hbm_budget_gb:
         os.environ["CGS_HBM_BUDGET_GB"] = str(args.hbm_budget_gb)
+    if getattr(args, "weight_arena_gb", None):
+        os.environ["CGS_WEIGHT_ARENA_GB"] = str(args.weight_arena_gb)
     if args.hip_graphs:
         os.environ["CGS_GRAPHS"] = "1"
     if args.deterministic:

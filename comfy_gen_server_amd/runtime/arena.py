@@ -1,0 +1,155 @@
+"""HBM weight arena (C27; SURVEY §7.1 runtime/): every resident model's parameters and buffers live
+in ONE device slab per GPU, placed by the C++ offset allocator ``_cgs_runtime.Arena`` (best fit,
+coalescing free list, 256-B aligned blocks -- csrc/runtime/arena.cpp).
+
+Why a slab: 288 GB of HBM holds several SDXL-class pipelines at once; with per-tensor caching-
+allocator blocks, weights interleave with activation blocks of every resolution the server has
+seen, and evicting a model leaves holes the activation pools cannot reuse. The slab keeps weights
+contiguous, makes residency accounting exact (``stats()``), and eviction / reload of a model is a
+block free / best-fit placement without touching the activation pools or the hipGraph pools.
+
+Enable with ``--weight-arena-gb N`` (env ``CGS_WEIGHT_ARENA_GB``); ``ModelPatcher.patch_model`` then
+places modules here instead of ``module.to(device)``, and ``unpatch_model`` evicts them.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+from .. import _native
+
+
+class ArenaFull(RuntimeError):
+    pass
+
+
+class _PyArena:
+    """Same interface as the C++ allocator (used only when _cgs_runtime is not built)."""
+
+    def __init__(self, capacity, align=256):
+        self.align = align
+        self.cap = capacity - capacity % align
+        self.free_list = [(0, self.cap)]
+        self.used = {}
+        self.peak = 0
+
+    def alloc(self, n):
+        need = (max(n, 1) + self.align - 1) // self.align * self.align
+        fits = [(s, o) for o, s in self.free_list if s >= need]
+        if not fits:
+            return -1
+        s, o = min(fits)
+        self.free_list.remove((o, s))
+        if s > need:
+            self.free_list.append((o + need, s - need))
+        self.used[o] = need
+        self.peak = max(self.peak, sum(self.used.values()))
+        return o
+
+    def free(self, o):
+        if o not in self.used:
+            return False
+        size = self.used.pop(o)
+        blocks = sorted(self.free_list + [(o, size)])
+        merged = []
+        for bo, bs in blocks:
+            if merged and merged[-1][0] + merged[-1][1] == bo:
+                merged[-1] = (merged[-1][0], merged[-1][1] + bs)
+            else:
+                merged.append((bo, bs))
+        self.free_list = merged
+        return True
+
+    def stats(self):
+        return {"capacity": self.cap, "used": sum(self.used.values()), "peak": self.peak,
+                "largest_free": max((s for _, s in self.free_list), default=0),
+                "free_blocks": len(self.free_list), "live_blocks": len(self.used)}
+
+
+class WeightArena:
+    def __init__(self, capacity_bytes: int, device, align: int = 256):
+        rt = _native.load_runtime()
+        self.alloc = rt.Arena(int(capacity_bytes), align) if rt is not None and hasattr(rt, "Arena") \
+            else _PyArena(int(capacity_bytes), align)
+        self.device = torch.device(device)
+        self.slab = torch.empty(int(capacity_bytes), dtype=torch.uint8, device=self.device)
+        self.base = self.slab.data_ptr()
+        self.blocks: dict[int, dict[str, int]] = {}      # id(module) -> {tensor name: offset}
+        self.lock = threading.Lock()
+
+    def owns(self, t: torch.Tensor) -> bool:
+        return t.device == self.device and self.base <= t.data_ptr() < self.base + self.slab.numel()
+
+    def _view(self, off: int, t: torch.Tensor) -> torch.Tensor:
+        nbytes = t.numel() * t.element_size()
+        return self.slab[off:off + nbytes].view(t.dtype).view(t.shape)
+
+    def place_module(self, module: torch.nn.Module) -> int:
+        """Move every parameter / buffer of ``module`` into the slab (shared tensors once); raises
+        ArenaFull (after undoing this call's placements) when it does not fit."""
+        placed = 0
+        with self.lock:
+            table = self.blocks.setdefault(id(module), {})
+            seen: dict[int, torch.Tensor] = {}
+            new = []
+            try:
+                for name, t in list(module.named_parameters(recurse=True)) + list(module.named_buffers(recurse=True)):
+                    if t is None or name in table:
+                        continue
+                    key = t.data_ptr() if t.numel() else id(t)
+                    if key in seen:                         # tied weights: one block, same view
+                        t.data = seen[key]
+                        continue
+                    nbytes = t.numel() * t.element_size()
+                    off = self.alloc.alloc(nbytes)
+                    if off < 0:
+                        raise ArenaFull(f"weight arena full: {nbytes} B for {name} ({self.stats()})")
+                    v = self._view(off, t)
+                    v.copy_(t.data)
+                    seen[key] = v
+                    new.append((name, t, t.data))
+                    t.data = v
+                    table[name] = off
+                    placed += nbytes
+            except ArenaFull:
+                for name, t, orig in new:
+                    t.data = orig
+                    self.alloc.free(table.pop(name))
+                raise
+        return placed
+
+    def evict_module(self, module: torch.nn.Module, device_to="cpu") -> int:
+        """Copy the module's tensors out to ``device_to`` and free their blocks."""
+        freed = 0
+        with self.lock:
+            table = self.blocks.pop(id(module), {})
+            for name, t in list(module.named_parameters(recurse=True)) + list(module.named_buffers(recurse=True)):
+                if t is not None and self.owns(t):
+                    t.data = t.data.to(device_to, copy=True)
+            for off in table.values():
+                self.alloc.free(off)
+                freed += 1
+        return freed
+
+    def stats(self) -> dict:
+        return dict(self.alloc.stats())
+
+
+_ARENAS: dict = {}
+_LOCK = threading.Lock()
+
+
+def get(device) -> WeightArena | None:
+    """The arena of ``device`` when enabled (``CGS_WEIGHT_ARENA_GB``), created on first use."""
+    gb = float(os.environ.get("CGS_WEIGHT_ARENA_GB", "0") or 0)
+    device = torch.device(device)
+    if gb <= 0 or device.type != "cuda":
+        return None
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    with _LOCK:
+        a = _ARENAS.get(key)
+        if a is None:
+            a = _ARENAS[key] = WeightArena(int(gb * (1 << 30)), torch.device("cuda", key))
+        return a

@@ -145,6 +145,11 @@ def _set_attr(obj, name, value):
     return prev
 
 
+def _in_arena(t) -> bool:
+    from . import arena
+    return any(a.owns(t) for a in arena._ARENAS.values()) if arena._ARENAS else False
+
+
 class ModelPatcher:
     def __init__(self, model, load_device, offload_device, size=0, weight_inplace_update=False):
         self.size = size
@@ -317,7 +322,10 @@ class ModelPatcher:
         base = self.backup[key]
         dev = device_to if device_to is not None else base.device
         out = calculate_weight(self.patches[key], base.to(dev, torch.float32, copy=True), key)
-        w.data = out.to(base.dtype)
+        if _in_arena(w) and out.shape == w.shape:
+            w.data.copy_(out.to(base.dtype))         # patched weight stays in its arena block
+        else:
+            w.data = out.to(base.dtype)
 
     def patch_model(self, device_to=None, patch_weights=True, force=False):
         for k, obj in self.object_patches.items():
@@ -325,7 +333,13 @@ class ModelPatcher:
             if k not in self.object_patches_backup:
                 self.object_patches_backup[k] = old
         if device_to is not None and not self.is_resident_on(device_to):
-            self.model.to(device_to)
+            from . import arena
+            wa = arena.get(device_to)
+            if wa is not None:
+                wa.place_module(self.model)          # weights into the HBM slab (C27)
+                self.model.to(device_to)             # (anything the arena does not hold)
+            else:
+                self.model.to(device_to)
             from ..models.layers import bump_weights_epoch
             bump_weights_epoch()
         if patch_weights and (force or getattr(self.model, "current_patches_uuid", None) != self.patches_uuid):
@@ -343,12 +357,20 @@ class ModelPatcher:
     def unpatch_model(self, device_to=None, unpatch_weights=True):
         if unpatch_weights:
             for k, w in self.backup.items():
-                _get_attr(self.model, k).data = w
+                t = _get_attr(self.model, k)
+                if _in_arena(t) and t.shape == w.shape:
+                    t.data.copy_(w)
+                else:
+                    t.data = w
             self.backup.clear()
             self.model.current_patches_uuid = None
             from ..models.layers import invalidate_all
             invalidate_all(self.model)
             if device_to is not None:
+                from . import arena
+                for a in list(arena._ARENAS.values()):
+                    if id(self.model) in a.blocks:
+                        a.evict_module(self.model, device_to)
                 self.model.to(device_to)
         for k, v in self.object_patches_backup.items():
             _set_attr(self.model, k, v)
