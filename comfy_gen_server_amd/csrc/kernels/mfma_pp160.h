@@ -33,6 +33,16 @@ constexpr int B_BYTES = BN * 128;
 constexpr int STAGE = A_BYTES + B_BYTES;
 constexpr int LDS = 3 * STAGE;     // 156 KiB
 
+// Tile column staged at B row r. Wave group g reads rows g*80 + 16j + (4fq + t) as MFMA column tile
+// j; the tile pairs (0,1) and (2,3) are interleaved so that the lane holds 8 consecutive columns
+// (32p + 8fq + 4(j&1) + t) -> 16-B epilogue stores covering 64 contiguous bytes per row; tile 4
+// keeps its 16 plain columns (8-B stores).
+__device__ __forceinline__ int b_col160(int r) {
+  const int g = r >= 80, l = r - 80 * g, j = l >> 4, q = l & 15;
+  if (j >= 4) return 80 * g + 64 + q;
+  return 80 * g + 32 * (j >> 1) + 8 * (q >> 2) + 4 * (j & 1) + (q & 3);
+}
+
 // AL: loader with setup(slot, global_row) for slots 0..3 (tile rows slot*64 + (tid >> 3)) and
 // src(slot, k0) -> this lane's 16-B source for K offset k0 (swizzled chunk already applied).
 //
@@ -40,7 +50,8 @@ constexpr int LDS = 3 * STAGE;     // 156 KiB
 // (G = gridDim.x; XCD-mates take consecutive logical tiles, grouped_tile() orders them). The
 // K-tile stream runs ACROSS tiles: the DMAs of the next tile's first two K-tiles are issued during
 // the current tile's last two, and the epilogue (direct 8-B stores from registers, no LDS) runs
-// while they are in flight -- no per-tile prologue bubble, no LDS-staged epilogue. Needs K >= 128.
+// while they are in flight -- no per-tile prologue bubble, no LDS-staged epilogue (16-B stores for
+// 4 of the 5 column tiles, see b_col160). Needs K >= 128, N % 8 == 0.
 template <class AL>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
@@ -71,7 +82,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       const int r = g * 64 + lrow;
-      int n = n0 + (r < BN ? r : BN - 1);
+      int n = n0 + b_col160(r < BN ? r : BN - 1);
       n = n < N ? n : N - 1;
       bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
     }
@@ -122,40 +133,56 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   auto epilogue_t = [&](int m0, int n0, auto has_bias_c, auto has_res_c) {
     constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
     const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
+    // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain
+    auto colj = [&](int j) { return j < 4 ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : 64 + 4 * fq; };
     float4 bv[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      int col = n_w + 16 * j + 4 * fq;
+      int col = n_w + colj(j);
       col = col < N ? col : N - 4;
       bv[j] = HB ? unpack4_bf16(*reinterpret_cast<const uint2*>(e.bias + col)) : float4{0.f, 0.f, 0.f, 0.f};
     }
     uint2 rw[4][5];   // residual words, all loads issued before the first store (one wait)
     if (HR) {
 #pragma unroll
-      for (int j = 0; j < 5; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          int row = m_w + 16 * i + fr, col = n_w + 16 * j + 4 * fq;
-          row = row < M ? row : M - 1;
-          col = col < N ? col : N - 4;
-          rw[i][j] = *reinterpret_cast<const uint2*>(e.R + (long long)row * e.ldr + col);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int col = n_w + 16 * j + 4 * fq;
-#pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = m_w + 16 * i + fr;
-        float v0 = acc[i][j][0] * e.alpha + bv[j].x, v1 = acc[i][j][1] * e.alpha + bv[j].y;
-        float v2 = acc[i][j][2] * e.alpha + bv[j].z, v3 = acc[i][j][3] * e.alpha + bv[j].w;
-        if (HR) {
-          const float4 rv = unpack4_bf16(rw[i][j]);
-          v0 += rv.x; v1 += rv.y; v2 += rv.z; v3 += rv.w;
+        int row = m_w + 16 * i + fr;
+        row = row < M ? row : M - 1;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          int col = n_w + 32 * p + 8 * fq;
+          col = col < N ? col : N - 8;
+          const uint4 q4 = *reinterpret_cast<const uint4*>(e.R + (long long)row * e.ldr + col);
+          rw[i][2 * p] = uint2{q4.x, q4.y};
+          rw[i][2 * p + 1] = uint2{q4.z, q4.w};
         }
-        if (row < M && col < N)
-          *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pack4_bf16(v0, v1, v2, v3);
+        int col = n_w + 64 + 4 * fq;
+        col = col < N ? col : N - 4;
+        rw[i][4] = *reinterpret_cast<const uint2*>(e.R + (long long)row * e.ldr + col);
       }
+    }
+    auto val = [&](int i, int j) {
+      float v0 = acc[i][j][0] * e.alpha + bv[j].x, v1 = acc[i][j][1] * e.alpha + bv[j].y;
+      float v2 = acc[i][j][2] * e.alpha + bv[j].z, v3 = acc[i][j][3] * e.alpha + bv[j].w;
+      if (HR) {
+        const float4 rv = unpack4_bf16(rw[i][j]);
+        v0 += rv.x; v1 += rv.y; v2 += rv.z; v3 += rv.w;
+      }
+      return pack4_bf16(v0, v1, v2, v3);
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m_w + 16 * i + fr;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int col = n_w + 32 * p + 8 * fq;
+        const uint2 lo = val(i, 2 * p), hi = val(i, 2 * p + 1);
+        if (row < M && col < N)
+          *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{lo.x, lo.y, hi.x, hi.y};
+      }
+      const int col = n_w + 64 + 4 * fq;
+      const uint2 w4 = val(i, 4);
+      if (row < M && col < N) *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = w4;
     }
   };
   using T0 = std::false_type;
