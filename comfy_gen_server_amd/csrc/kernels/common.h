@@ -87,6 +87,27 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * x * (1.0f + erf_v);
 }
 
+// Two GELUs at once: the same A&S 7.1.26 erf as gelu_fast, written on float2 so the polynomial,
+// the scalings and the final product issue as packed fp32 ops (v_pk_fma_f32 / v_pk_mul_f32: two
+// lanes' worth of work per instruction); only rcp and exp stay per element. Used by the GEGLU GEMM
+// epilogue, where the gate math is a visible fraction of a short-K tile.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t x) {
+  const f32x2_t z = f32x2_t{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
+  const f32x2_t d = z * 0.3275911f + 1.0f;
+  const f32x2_t t = f32x2_t{__frcp_rn(d.x), __frcp_rn(d.y)};
+  f32x2_t poly = t * 1.061405429f + (-1.453152027f);
+  poly = poly * t + 1.421413741f;
+  poly = poly * t + (-0.284496736f);
+  poly = poly * t + 0.254829592f;
+  poly = poly * t;
+  const f32x2_t zz = z * z;
+  const f32x2_t e = f32x2_t{__expf(-zz.x), __expf(-zz.y)};
+  const f32x2_t erf_abs = 1.0f - poly * e;
+  const f32x2_t erf_v = f32x2_t{__builtin_copysignf(erf_abs.x, x.x), __builtin_copysignf(erf_abs.y, x.y)};
+  return (x * 0.5f) * (erf_v + 1.0f);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

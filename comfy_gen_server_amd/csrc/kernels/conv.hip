@@ -15,6 +15,7 @@
 //   dual input : channels [0, C1) come from in, [C1, Cin) from in2 — torch.cat([h, skip], 1) + conv
 //                (the UNet decoder's skip concat is never materialised).
 #include "common.h"
+#include <stdlib.h>
 #include "mfma_core.h"
 #include "mfma_pp.h"
 #include "mfma_pp160.h"
@@ -339,6 +340,7 @@ struct ConvGatherK {
     if constexpr (WIDE) return (const void*)(t + 2 * ((size_t)p * (unsigned)cs + (unsigned)cb));
     else return (const void*)(t + 2u * (p * (unsigned)cs + (unsigned)cb));
   }
+  __device__ __forceinline__ void dma(int s, int k0, unsigned char* dst) const { mc::lds_dma16(src(s, k0), dst); }
 };
 
 // v7's gather: the same decode, issued as buffer_load ... lds through one descriptor per input
@@ -481,14 +483,16 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
 }
 
 // v7: the persistent 256 x 256 ping-pong with cross-tile prefetch and register epilogue (mfma_ppk.h)
-template <bool FAST>
+// LOADER 0: ConvGatherA8 (generic: UP2X, big filters); 1: ConvGatherKB (buffer_load lds). (ConvGatherK
+// with global_load_lds and 64-bit offsets measured 25-30 % slower here: it spills at the v7 VGPR cap.)
+template <int LOADER>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v7_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  typename std::conditional<FAST, ConvGatherKB, ConvGatherA8>::type al;
+  typename std::conditional<LOADER == 1, ConvGatherKB, ConvGatherA8>::type al;
   al.a = &a;
-  if constexpr (FAST) al.init();
+  if constexpr (LOADER == 1) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   ppk::run<false>(al, a.w, K, M, a.Cout, K, e, smem, (M + ppk::BM - 1) / ppk::BM, a.tiles_n, a.group_m, a.sp);
 }
@@ -496,9 +500,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ppk::LDS);
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ppk::LDS);
     attr = true;
   }
@@ -522,9 +526,9 @@ static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long
   const int grid = (int)(U < conv_num_cus() ? U : conv_num_cus());
   if (conv_fast_ok(a) && !conv_wide(a)) {
     conv_magic(a);
-    conv_nhwc_v7_kernel<true><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+    conv_nhwc_v7_kernel<1><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
   } else {
-    conv_nhwc_v7_kernel<false><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+    conv_nhwc_v7_kernel<0><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
   }
 }
 

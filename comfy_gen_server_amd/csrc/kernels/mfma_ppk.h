@@ -266,11 +266,11 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           for (int nq = 0; nq < 2; ++nq) {
             const f32x4 a = acc[mq * 4 + i][nq * 2 + 0], g = acc[mq * 4 + i][nq * 2 + 1];
             const float4 ba = bv[nq][0], bg = bv[nq][1];
-            const float o0 = (a[0] * e.alpha + ba.x) * gelu_fast(g[0] * e.alpha + bg.x);
-            const float o1 = (a[1] * e.alpha + ba.y) * gelu_fast(g[1] * e.alpha + bg.y);
-            const float o2 = (a[2] * e.alpha + ba.z) * gelu_fast(g[2] * e.alpha + bg.z);
-            const float o3 = (a[3] * e.alpha + ba.w) * gelu_fast(g[3] * e.alpha + bg.w);
-            h[nq] = pack4_bf16(o0, o1, o2, o3);
+            const f32x2_t g01 = gelu_fast2(f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y});
+            const f32x2_t g23 = gelu_fast2(f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w});
+            const f32x2_t o01 = (f32x2_t{a[0], a[1]} * e.alpha + f32x2_t{ba.x, ba.y}) * g01;
+            const f32x2_t o23 = (f32x2_t{a[2], a[3]} * e.alpha + f32x2_t{ba.z, ba.w}) * g23;
+            h[nq] = pack4_bf16(o01.x, o01.y, o23.x, o23.y);
           }
           if (row < M && ocol < Nout) store16(e.C + (long long)row * e.ldc + ocol, h[0], h[1], e.flags);
         }
