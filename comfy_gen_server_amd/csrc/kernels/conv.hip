@@ -449,11 +449,12 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   }
 }
 
+template <bool FAST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  ConvGatherA8 al;
+  typename std::conditional<FAST, ConvGatherK<true>, ConvGatherA8>::type al;
   al.a = &a;
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   pq::run(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n, a.group_m);
@@ -472,14 +473,22 @@ static int conv_num_cus() {
 static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pq::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pq::LDS);
     attr = true;
   }
   const int M = a.N * a.Ho * a.Wo;
   a.tiles_n = (a.Cout + pq::BN - 1) / pq::BN;
   const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
   const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
-  conv_nhwc_v6_kernel<<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+  if (conv_fast_ok(a)) {
+    conv_magic(a);
+    conv_nhwc_v6_kernel<true><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+  } else {
+    conv_nhwc_v6_kernel<false><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+  }
 }
 
 // v7: the persistent 256 x 256 ping-pong with cross-tile prefetch and register epilogue (mfma_ppk.h)
