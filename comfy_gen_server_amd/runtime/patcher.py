@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import copy
 import logging
+import os
 import uuid
 
 import torch
@@ -78,7 +79,7 @@ def calculate_weight(patches, weight, key):
                 shp = [down.shape[1], down.shape[0], mid.shape[2], mid.shape[3]]
                 down = torch.mm(down.transpose(0, 1).flatten(1), mid.transpose(0, 1).flatten(1)).reshape(shp).transpose(0, 1)
             try:
-                diff = torch.mm(up.flatten(1), down.flatten(1)).reshape(weight.shape)
+                diff = _lora_product(up.flatten(1), down.flatten(1)).reshape(weight.shape)
             except RuntimeError as e:
                 logging.error("ERROR %s %s %s", kind, key, e)
                 continue
@@ -128,6 +129,16 @@ def calculate_weight(patches, weight, key):
         else:
             logging.warning("patch type not recognized %s %s", kind, key)
     return weight
+
+
+def _lora_product(up: torch.Tensor, down: torch.Tensor) -> torch.Tensor:
+    """up [O, r] @ down [r, I] (K20). On the GPU: the HIP MFMA GEMM (bf16 factors, fp32 accumulate,
+    one bf16 rounding of the rank-r product, which is then added to the fp32 weight); everywhere else,
+    and for ranks the GEMM does not tile (r % 8), fp32 ``torch.mm`` like the reference."""
+    if up.is_cuda and up.shape[1] % 8 == 0 and up.shape[1] == down.shape[0] and os.environ.get("CGS_LORA_HIP", "1") != "0":
+        from .. import ops
+        return ops.linear(up.to(torch.bfloat16), down.t().contiguous().to(torch.bfloat16)).float()
+    return torch.mm(up, down)
 
 
 def _get_attr(obj, name):

@@ -82,3 +82,17 @@ def test_clip_embed_hip(cuda, dtype):
     ops.reset_stats()
     _clip_check(cuda, dtype)
     assert ops.stats().get(("clip_embed", "hip"), 0) == 2
+
+
+@pytest.mark.gpu
+def test_lora_merge_product_on_hip(cuda):
+    """K20: the LoRA up @ down product of calculate_weight runs on the HIP GEMM on the device."""
+    from comfy_gen_server_amd.runtime.patcher import calculate_weight
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(640, 1280, generator=g)
+    up, down = torch.randn(640, 32, generator=g) * 0.1, torch.randn(32, 1280, generator=g) * 0.1
+    ref = calculate_weight([(0.8, ("lora", (up, down, 16.0, None, None)), 1.0)], w.clone(), "k")
+    ops.reset_stats()
+    out = calculate_weight([(0.8, ("lora", (up.to(cuda), down.to(cuda), 16.0, None, None)), 1.0)], w.to(cuda), "k")
+    assert ops.stats().get(("gemm", "hip"), 0) == 1
+    assert torch.allclose(out.cpu(), ref, atol=2e-3, rtol=1e-3)
