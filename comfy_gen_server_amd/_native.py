@@ -135,6 +135,9 @@ KERNEL_SIGNATURES = {
     # K26 CLIP embeddings: ids, tok, pos, y, B, S, D, vocab, dtype / pooled gather: ids, x, out, B, S, D, dtype
     "cgs_clip_embed": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "cgs_pooled_gather": [_P, _P, _P, _I, _I, _I, _I, _P],
+    # LayerNorm folded into the GEMM: row stats (x, rs, rows, C, eps, dtype) and the v7 GEMM with the fold
+    "cgs_layernorm_stats": [_P, _P, _I, _I, _F, _I, _P],
+    "cgs_gemm_bf16_lnfold": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _I, _P, _L, _P],
     # v7 split-K tail: workspace bytes for (M, N, K) and the GEMM / conv launchers that take it
     "cgs_v7_ws_bytes": [_I, _I, _I],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],

@@ -24,6 +24,7 @@
 #define EPI_BIAS 1
 #define EPI_RESIDUAL 2
 #define EPI_GEGLU 4
+#define EPI_LNFOLD 8
 
 // fp8 e4m3fn (OCP) -> bf16 bits, exact (every e4m3 value is a bf16 value); NaN stays NaN.
 __device__ __forceinline__ u16 fp8e4m3_to_bf16(uint32_t b) {
@@ -523,28 +524,34 @@ struct DenseA32 {
 
 // ------------------------------------------------------------------------------------------------
 // v7: persistent 256 x 256 x 64 ping-pong with cross-tile prefetch and a register epilogue (mfma_ppk.h)
-template <bool GG>
+template <bool GG, bool LN = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v7_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_m, int tiles_n, int group_m, ppk::Split sp) {
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m, ppk::Split sp, const float* rs = nullptr,
+    const float* cs = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   DenseA32 al{reinterpret_cast<const unsigned char*>(A), lda, M, {}};
-  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
-  ppk::run<GG>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m, sp);
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
+  ppk::run<GG, LN>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m, sp);
 }
 
 // ws (may be null): split-K tail workspace of >= cgs_v7_ws_bytes(M, N, K) bytes; without it the
 // tail round runs whole tiles.
 static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                           long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                          void* ws, long long ws_bytes, hipStream_t stream) {
+                          void* ws, long long ws_bytes, hipStream_t stream, const float* rs = nullptr,
+                          const float* cs = nullptr) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ppk::LDS);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
     attr_set = true;
   }
   const int tiles_n = (N + ppk::BN - 1) / ppk::BN;
@@ -569,14 +576,19 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
     }
   }
   const int grid = (int)(U < num_cus() ? U : num_cus());
-  if (epi & EPI_GEGLU)
-    gemm_bf16_nt_v7_kernel<true><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
-        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_m, tiles_n, g_tile_group, sp);
-  else
-    gemm_bf16_nt_v7_kernel<false><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
-        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_m, tiles_n, g_tile_group, sp);
+  const bool ln = (epi & EPI_LNFOLD) != 0;
+#define CGS_V7L(GG, LNF)                                                                                            \
+  gemm_bf16_nt_v7_kernel<GG, LNF><<<grid, ppk::THREADS, ppk::LDS, stream>>>(                                        \
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, \
+      tiles_m, tiles_n, g_tile_group, sp, rs, cs)
+  if (epi & EPI_GEGLU) {
+    if (ln) CGS_V7L(true, true);
+    else CGS_V7L(true, false);
+  } else {
+    if (ln) CGS_V7L(false, true);
+    else CGS_V7L(false, false);
+  }
+#undef CGS_V7L
   return (int)hipGetLastError();
 }
 
@@ -665,4 +677,20 @@ CGS_EXPORT int cgs_gemm_bf16_v7ws(const void* A, const void* W, void* C, const v
                                   int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
                                   float alpha, void* ws, long long ws_bytes, hipStream_t stream) {
   return gemm_dispatch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, 7, stream, ws, ws_bytes);
+}
+
+// LayerNorm folded into the GEMM (MC_EPI_LNFOLD): C = rstd_r * (A W'^T - mean_r * cs) + bias, with
+// rs = per-row (mean, rstd) of A (cgs_layernorm_stats) and W' / cs / bias precomputed by the caller
+// (W' = W * gamma, cs = rowsum(W'), bias = b + W beta). v7 only (+ optional GEGLU, split-K tail).
+CGS_EXPORT int cgs_gemm_bf16_lnfold(const void* A, const void* W, void* C, const void* bias, const float* rs,
+                                    const float* cs, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                                    int epi, void* ws, long long ws_bytes, hipStream_t stream) {
+  const int nout = (epi & EPI_GEGLU) ? N / 2 : N;
+  if (!rs || !cs || K % 64 || K < 128 || lda % 8 || ldw % 8 || ldc % 8 || nout % 8 || (epi & EPI_RESIDUAL) ||
+      ((uintptr_t)A | (uintptr_t)W | (uintptr_t)C) % 16 || ((uintptr_t)bias % 8) || ((uintptr_t)cs % 16) ||
+      ((uintptr_t)rs % 8) || (long long)M * lda * 2 >= (1ll << 32) || (long long)N * ldw * 2 >= (1ll << 32))
+    return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0) return 0;
+  return gemm_v7_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, ws, ws_bytes, stream,
+                        rs, cs);
 }

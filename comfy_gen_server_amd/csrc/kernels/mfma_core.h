@@ -23,6 +23,7 @@ typedef __attribute__((address_space(3))) void mc_lds_void;
 #define MC_EPI_BIAS 1
 #define MC_EPI_RESIDUAL 2
 #define MC_EPI_GEGLU 4
+#define MC_EPI_LNFOLD 8   // y = rstd_r * (acc - mean_r * cs[c]) + bias[c]  (LayerNorm folded into the GEMM)
 
 namespace mc {
 
@@ -66,6 +67,8 @@ struct Epi {
   long long ldc, ldr;
   int flags;
   float alpha;
+  const float* rs = nullptr;   // MC_EPI_LNFOLD: per-row (mean, rstd) pairs of the GEMM's A rows
+  const float* cs = nullptr;   // MC_EPI_LNFOLD: per-column sums of the gamma-scaled weight rows
 };
 
 // s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])

@@ -93,7 +93,7 @@ __device__ __forceinline__ int b_col_perm(int nq, int r) {
   }
 }
 
-template <bool GG, class AL>
+template <bool GG, bool LN = false, class AL>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m,
                                     Split sp = Split{0, 1, nullptr, nullptr, 0}) {
@@ -217,6 +217,45 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       if constexpr (GG) return (fq >> 1) * 32 + 16 * j + 8 * (fq & 1) + 4 * nq;
       else return nq * 32 + 8 * fq + 4 * j;
     };
+    if constexpr (LN) {
+      // LayerNorm folded in (MC_EPI_LNFOLD): the GEMM ran on the raw rows x with W' = W * gamma;
+      // LN(x) W^T = rstd_r * (x W'^T - mean_r * colsum(W')) (+ W beta, folded into the bias)
+      float4 cv[2][2];
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          int col = ncw + bcol(nq, j);
+          col = col < N ? col : N - 4;
+          cv[nq][j] = *reinterpret_cast<const float4*>(e.cs + col);
+        }
+      // one 4-row batch of statistics at a time (all 8 at once spill at the 256-VGPR cap)
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq) {
+        float2 st[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int row = m0 + wr * 128 + mq * 64 + 16 * i + fr;
+          row = row < M ? row : M - 1;
+          st[i] = *reinterpret_cast<const float2*>(e.rs + 2 * (long long)row);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              f32x4& a = acc[mq * 4 + i][nq * 2 + j];
+              const float4 c = cv[nq][j];
+              const float mr = st[i].x * st[i].y;
+              a[0] = st[i].y * a[0] - mr * c.x;
+              a[1] = st[i].y * a[1] - mr * c.y;
+              a[2] = st[i].y * a[2] - mr * c.z;
+              a[3] = st[i].y * a[3] - mr * c.w;
+            }
+        asm volatile("" ::: "memory");      // keep the two batches' loads apart
+      }
+    }
     float4 bv[2][2];
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq)
@@ -323,6 +362,11 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   using Tt = std::true_type;
   const bool hb = (e.flags & MC_EPI_BIAS) != 0, hr = (e.flags & MC_EPI_RESIDUAL) != 0;
   auto epilogue = [&](int m0, int n0) {
+    if constexpr (LN) {                     // folded LayerNorm: no residual form (host-checked)
+      if (hb) epilogue_t(m0, n0, Tt{}, F{});
+      else epilogue_t(m0, n0, F{}, F{});
+      return;
+    }
     if (hr) {
       if (hb) epilogue_t(m0, n0, Tt{}, Tt{});
       else epilogue_t(m0, n0, F{}, Tt{});

@@ -357,6 +357,43 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ 
   }
 }
 
+
+// Row statistics only (the LayerNorm folded into the next GEMM's epilogue, MC_EPI_LNFOLD):
+// rs[2r] = mean, rs[2r+1] = rstd of row r. Same row-group layout and reductions as layernorm_kernel.
+template <int DT, int LPR>
+__global__ __launch_bounds__(256) void ln_stats_kernel(const u16* __restrict__ x, float* __restrict__ rs, int rows,
+                                                      int C, float eps) {
+  constexpr int RPB = 256 / LPR;
+  const int lane = threadIdx.x % LPR;
+  const int row = blockIdx.x * RPB + threadIdx.x / LPR;
+  const bool live = row < rows;
+  const int nch = C >> 3;
+  const u16* xr = x + (size_t)(live ? row : 0) * C;
+  float v[LN_MAXK][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    int ch = lane + LPR * k;
+    if (live && ch < nch) {
+      s16x8 t = reinterpret_cast<const s16x8*>(xr)[ch];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[k][j] = cvt_in<DT>((u16)t[j]); s += v[k][j]; }
+    }
+  }
+  const float mean = group_sum<LPR>(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    int ch = lane + LPR * k;
+    if (live && ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float d = v[k][j] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(group_sum<LPR>(q) / C + eps);
+  if (live && lane == 0) reinterpret_cast<float2*>(rs)[row] = float2{mean, rstd};
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void layernorm_big_kernel(const u16* __restrict__ x, u16* __restrict__ y,
                                                            const u16* __restrict__ w, const u16* __restrict__ b,
@@ -398,5 +435,25 @@ CGS_EXPORT int cgs_layernorm(const void* x, void* y, const void* w, const void* 
     else
       layernorm_big_kernel<CGS_F16><<<grid, 256, 0, stream>>>((const u16*)x, (u16*)y, (const u16*)w, (const u16*)b, rows, C, eps);
   }
+  return (int)hipGetLastError();
+}
+
+// (mean, rstd) per row of x [rows, C] (C % 8 == 0, C <= the register-resident LayerNorm limit)
+CGS_EXPORT int cgs_layernorm_stats(const void* x, float* rs, int rows, int C, float eps, int dtype, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (C % 8 || C / 8 > 32 * LN_MAXK) return (int)hipErrorInvalidValue;
+  const int nch = C / 8;
+  const int L = nch <= 16 * LN_MAXK ? (nch <= 8 * LN_MAXK ? 8 : 16) : 32;
+#define CGS_LNS(LPR) \
+  do { \
+    const int grid = (rows + (256 / LPR) - 1) / (256 / LPR); \
+    if (dtype == CGS_BF16) ln_stats_kernel<CGS_BF16, LPR><<<grid, 256, 0, stream>>>((const u16*)x, rs, rows, C, eps); \
+    else if (dtype == CGS_F16) ln_stats_kernel<CGS_F16, LPR><<<grid, 256, 0, stream>>>((const u16*)x, rs, rows, C, eps); \
+    else return (int)hipErrorInvalidValue; \
+  } while (0)
+  if (L == 8) CGS_LNS(8);
+  else if (L == 16) CGS_LNS(16);
+  else CGS_LNS(32);
+#undef CGS_LNS
   return (int)hipGetLastError();
 }

@@ -76,6 +76,20 @@ class CrossAttention(nn.Module, DerivedMixin):
             ctx_cache[cache_key] = (context, k, v)
         return k, v
 
+    def forward_lnfold(self, x, rs, norm, residual=None, sp=None):
+        """Self-attention on LN(x) with the LayerNorm folded into the fused QKV GEMM (K07): ``x`` raw
+        rows, ``rs`` their (mean, rstd) from ``ops.layernorm_stats``."""
+        inner = self.heads * self.dim_head
+        w2, cs, b2 = self._derived_get(("lnfold_qkv", id(norm)), lambda: ops.lnfold_weights(
+            self._w_qkv(), None, norm.weight, norm.bias))
+        qkv = ops.linear_lnfold(x, rs, w2, cs, b2)
+        q, k, v = qkv[..., :inner], qkv[..., inner:2 * inner], qkv[..., 2 * inner:]
+        if sp is not None:
+            o = sp.attention(q.contiguous(), k.contiguous(), v.contiguous(), self.heads)
+        else:
+            o = ops.attention(q, k, v, self.heads)
+        return self.to_out[0](o, residual=residual)
+
     def forward(self, x, context=None, value=None, mask=None, residual=None, ctx_cache=None, cache_key=None,
                 sp=None):
         """``sp`` (parallel.sp.SeqParallel): x is this rank's token shard; self-attention runs over
@@ -133,6 +147,16 @@ class FeedForward(nn.Module):
     def forward(self, x, residual=None):
         return self.net[2](self.net[0](x), residual=residual)
 
+    def lnfold_ok(self) -> bool:
+        return isinstance(self.net[0], GEGLU)
+
+    def forward_lnfold(self, x, rs, norm, residual=None):
+        """FF on LN(x) with the LayerNorm folded into the GEGLU GEMM (interleaved a/g rows)."""
+        g = self.net[0]
+        w2, cs, b2 = g._derived_get(("lnfold_geglu", id(norm)), lambda: ops.lnfold_weights(
+            ops.core.geglu_interleave(g.proj.weight), ops.core.geglu_interleave(g.proj.bias), norm.weight, norm.bias))
+        return self.net[2](ops.linear_lnfold(x, rs, w2, cs, b2, geglu=True), residual=residual)
+
 
 class BasicTransformerBlock(nn.Module):
     def __init__(self, dim, n_heads, d_head, context_dim=None, gated_ff=True, disable_self_attn=False,
@@ -187,10 +211,26 @@ class BasicTransformerBlock(nn.Module):
             x = self.attn2(n, context=n if self.switch_temporal_ca_to_sa else context, residual=x)
         return self.ff(self.norm3(x), residual=x if self.is_res else None)
 
+    def _lnfold_ok(self, x) -> bool:
+        n1, n3 = self.norm1, self.norm3
+        return (n1.weight is not None and n3.weight is not None and n1.weight.dtype == x.dtype
+                and n3.weight.dtype == x.dtype and self.attn1.to_q.weight.dtype == x.dtype
+                and self.ff.lnfold_ok() and ops.lnfold_available(x, x.shape[-1]))
+
     def _forward_fast(self, x, context, to):
-        """Hook-free path: residual adds fused into the out-projection / FF-out GEMM epilogues."""
+        """Hook-free path: residual adds fused into the out-projection / FF-out GEMM epilogues; on
+        the device the LayerNorms before the fused QKV GEMM and the GEGLU GEMM are folded into those
+        GEMMs (only per-row statistics are computed; LN(x) never materialises)."""
         cache = to.get("ctx_cache")
         key = id(self)
+        if self._lnfold_ok(x):
+            if self.disable_self_attn:
+                x = self.attn1(self.norm1(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 1))
+            else:
+                x = self.attn1.forward_lnfold(x, ops.layernorm_stats(x, self.norm1.eps), self.norm1, residual=x,
+                                              sp=to.get("sp"))
+            x = self.attn2(self.norm2(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 2))
+            return self.ff.forward_lnfold(x, ops.layernorm_stats(x, self.norm3.eps), self.norm3, residual=x)
         n = self.norm1(x)
         if self.disable_self_attn:
             x = self.attn1(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 1))

@@ -758,6 +758,64 @@ def pooled_gather(x: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     return x[torch.arange(B, device=x.device), ids.to(device=x.device, dtype=torch.long).argmax(dim=-1)]
 
 
+_LNFOLD = os.environ.get("CGS_LNFOLD", "1") != "0"
+
+
+def lnfold_available(x: torch.Tensor, K: int) -> bool:
+    """The LayerNorm-folded GEMM path applies (device bf16 rows, v7-legal K)."""
+    return (_LNFOLD and os.environ.get("CGS_LNFOLD", "1") != "0" and x.is_cuda and x.dtype == torch.bfloat16 and K % 64 == 0 and K >= 128 and K <= 2048
+            and backend_for("layernorm", x, "cgs_layernorm_stats") == "hip" and _native.has_kernel("cgs_gemm_bf16_lnfold"))
+
+
+def layernorm_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """Per-row (mean, rstd) of ``x`` [..., C] as float32 [rows, 2] (the statistics half of LayerNorm)."""
+    C = x.shape[-1]
+    a = x.reshape(-1, C)
+    if not a.is_contiguous():
+        a = a.contiguous()
+    rs = torch.empty((a.shape[0], 2), device=x.device, dtype=torch.float32)
+    count("layernorm", "hip")
+    _check(_lib().cgs_layernorm_stats(a.data_ptr(), rs.data_ptr(), a.shape[0], C, float(eps), _DT[x.dtype],
+                                      _stream()), "cgs_layernorm_stats")
+    return rs
+
+
+def lnfold_weights(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch.Tensor | None,
+                   beta: torch.Tensor | None):
+    """(W', colsum(W'), b') with W' = W * gamma (bf16), colsum over the bf16-rounded W' (fp32) and
+    b' = b + W beta, so that LN(x) W^T + b = rstd * (x W'^T - mean * colsum(W')) + b'."""
+    wf = weight.float()
+    w2 = (wf * gamma.float()[None, :]) if gamma is not None else wf
+    w2 = w2.to(torch.bfloat16).contiguous()
+    cs = w2.float().sum(dim=1).contiguous()
+    b = torch.zeros(weight.shape[0], device=weight.device, dtype=torch.float32)
+    if bias is not None:
+        b = b + bias.float()
+    if beta is not None:
+        b = b + wf @ beta.float()
+    return w2, cs, b.to(torch.bfloat16).contiguous()
+
+
+def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch.Tensor, b2: torch.Tensor,
+                  geglu: bool = False) -> torch.Tensor:
+    """``LN(x) @ W^T + b`` (or the GEGLU of it, with interleaved W' rows) from the raw rows ``x``, the
+    row statistics ``rs`` and ``lnfold_weights`` -- the LayerNorm never materialises (K07 folded
+    into the GEMM epilogue of the v7 kernel)."""
+    K = x.shape[-1]
+    a = x.reshape(-1, K)
+    if not a.is_contiguous():
+        a = a.contiguous()
+    M, N = a.shape[0], w2.shape[0]
+    nout = N // 2 if geglu else N
+    out = torch.empty((M, nout), device=x.device, dtype=x.dtype)
+    ws = _v7_ws(M, N, K, x.device)
+    count("gemm_geglu" if geglu else "gemm", "hip")
+    _check(_lib().cgs_gemm_bf16_lnfold(a.data_ptr(), w2.data_ptr(), out.data_ptr(), b2.data_ptr(), rs.data_ptr(),
+                                       cs.data_ptr(), M, N, K, K, K, nout, EPI_BIAS | (EPI_GEGLU if geglu else 0),
+                                       _ptr(ws), 0 if ws is None else ws.numel(), _stream()), "cgs_gemm_bf16_lnfold")
+    return out.view(*x.shape[:-1], nout)
+
+
 def _feather_mask(h: int, w: int, feather: int, device) -> torch.Tensor:
     """Separable ramp of the reference tiled blend (comfy/utils.py tiled_scale)."""
     def ramp(n):

@@ -548,3 +548,47 @@ def test_conv_v7_split_tail(cuda, N, C1, C2, H, W, Cout, k, res):
                                     bias.data_ptr(), None if r is None else r.data_ptr(), y.data_ptr(), N, H, W, Cin,
                                     Cout, k, k, 1, k // 2, H, W, 0, ws.data_ptr(), ws_bytes, core._stream()) == 0
     assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,C,N,geglu", [(4096, 640, 1920, False), (1000, 1280, 3840, False), (2048, 640, 5120, True),
+                                         (16384, 1280, 10240, True)])
+def test_layernorm_folded_gemm(cuda, M, C, N, geglu):
+    """K07 folded: LN(x) @ W^T + b from the raw rows + (mean, rstd) -- fp32 reference of LN then GEMM."""
+    torch.manual_seed(0)
+    x = (torch.randn(M, C, device=cuda) * 3 + 1.5).to(torch.bfloat16)
+    gamma = (torch.rand(C, device=cuda) + 0.5).to(torch.bfloat16)
+    beta = (torch.randn(C, device=cuda) * 0.2).to(torch.bfloat16)
+    w = (torch.randn(N, C, device=cuda) / math.sqrt(C)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16) if geglu else None
+    rs = ops.layernorm_stats(x, 1e-5)
+    ref_ln = F.layer_norm(x.float(), (C,), gamma.float(), beta.float(), 1e-5)
+    assert torch.allclose(rs[:, 0], x.float().mean(1), atol=1e-3)
+    h = ref_ln @ w.float().t() + (b.float() if b is not None else 0)
+    if geglu:
+        wi, bi = core.geglu_interleave(w), core.geglu_interleave(b)
+        w2, cs, b2 = ops.lnfold_weights(wi, bi, gamma, beta)
+        y = ops.linear_lnfold(x, rs, w2, cs, b2, geglu=True)
+        a, g = h.chunk(2, dim=-1)
+        ref = a * F.gelu(g)
+    else:
+        w2, cs, b2 = ops.lnfold_weights(w, None, gamma, beta)
+        y = ops.linear_lnfold(x, rs, w2, cs, b2)
+        ref = h
+    assert _rel(y, ref) < 1.5e-2
+
+
+def test_transformer_block_lnfold_matches_unfolded(cuda, monkeypatch):
+    from comfy_gen_server_amd.models.attention import BasicTransformerBlock
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    torch.manual_seed(0)
+    with torch.inference_mode():
+        blk = BasicTransformerBlock(640, 10, 64, context_dim=2048, dtype=torch.bfloat16, device=cuda)
+        init_random_fast_(blk, seed=2)
+        x = torch.randn(2, 1024, 640, device=cuda).to(torch.bfloat16)
+        ctx = torch.randn(2, 77, 2048, device=cuda).to(torch.bfloat16)
+        ops.reset_stats()
+        y_fold = blk(x, context=ctx, transformer_options={})
+        assert blk._lnfold_ok(x)
+        monkeypatch.setattr(core, "_LNFOLD", False)
+        y_ref = blk(x, context=ctx, transformer_options={})
+    assert _rel(y_fold, y_ref) < 2e-2
