@@ -90,10 +90,40 @@ class CrossAttention(nn.Module, DerivedMixin):
             o = ops.attention(q, k, v, self.heads)
         return self.to_out[0](o, residual=residual)
 
+    def static_kv(self, context, kv):
+        """Cross-attention K/V of a sampling run's constant context, kept in a per-context buffer
+        (``kv`` = (mode, ids of the step plan's static context tensors), sampling/step_graph.py): in
+        "fill" mode the fused K/V GEMM runs and its result is stored; in "use" mode (the captured
+        step graph) the buffer is read, so the replayed steps carry no K/V GEMM -- the run's prologue
+        (``refresh_static_kv``) recomputes it once per job instead of once per step."""
+        mode, sources = kv
+        if id(context) not in sources:
+            return None
+        inner = self.heads * self.dim_head
+        store = self.__dict__.setdefault("_kv_static", {})
+        ent = store.get(id(context))
+        if mode == "fill" or ent is None or ent[0] is not context:
+            kvt = ops.linear(context, self._w_kv())
+            if ent is None or ent[0] is not context or ent[1].shape != kvt.shape:
+                ent = (context, torch.empty_like(kvt))
+                store[id(context)] = ent
+            ent[1].copy_(kvt)
+        buf = ent[1]
+        return buf[..., :inner], buf[..., inner:]
+
+    def refresh_static_kv(self, sources) -> int:
+        n = 0
+        for key, (ctx, buf) in self.__dict__.get("_kv_static", {}).items():
+            if key in sources:
+                buf.copy_(ops.linear(ctx, self._w_kv()))
+                n += 1
+        return n
+
     def forward(self, x, context=None, value=None, mask=None, residual=None, ctx_cache=None, cache_key=None,
-                sp=None):
+                sp=None, kv=None):
         """``sp`` (parallel.sp.SeqParallel): x is this rank's token shard; self-attention runs over
-        the whole sequence through ``sp.attention`` (cross-attention needs no exchange)."""
+        the whole sequence through ``sp.attention`` (cross-attention needs no exchange). ``kv``:
+        step-graph static K/V mode (``static_kv``)."""
         inner = self.heads * self.dim_head
         if context is None and value is None and x.dtype == self.to_q.weight.dtype \
                 and x.device == self.to_q.weight.device:
@@ -102,7 +132,11 @@ class CrossAttention(nn.Module, DerivedMixin):
         else:
             q = self.to_q(x)
             ctx = x if context is None else context
-            k, v = self.project_kv(ctx, value, ctx_cache, cache_key)
+            kvs = None
+            if kv is not None and value is None and context is not None and context.is_cuda \
+                    and context.dtype == self.to_k.weight.dtype:
+                kvs = self.static_kv(context, kv)
+            k, v = kvs if kvs is not None else self.project_kv(ctx, value, ctx_cache, cache_key)
         if sp is not None and context is None and value is None and mask is None:
             o = sp.attention(q.contiguous(), k.contiguous(), v.contiguous(), self.heads)
         else:
@@ -229,7 +263,8 @@ class BasicTransformerBlock(nn.Module):
             else:
                 x = self.attn1.forward_lnfold(x, ops.layernorm_stats(x, self.norm1.eps), self.norm1, residual=x,
                                               sp=to.get("sp"))
-            x = self.attn2(self.norm2(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 2))
+            x = self.attn2(self.norm2(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 2),
+                           kv=to.get("kv_static"))
             return self.ff.forward_lnfold(x, ops.layernorm_stats(x, self.norm3.eps), self.norm3, residual=x)
         n = self.norm1(x)
         if self.disable_self_attn:
@@ -237,7 +272,7 @@ class BasicTransformerBlock(nn.Module):
         else:
             x = self.attn1(n, residual=x, sp=to.get("sp"))
         n = self.norm2(x)
-        x = self.attn2(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 2))
+        x = self.attn2(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 2), kv=to.get("kv_static"))
         return self.ff(self.norm3(x), residual=x)
 
     def _forward_patched(self, x, context, to, patches, replace):
@@ -378,3 +413,13 @@ class SpatialTransformer(nn.Module):
             t = ops.linear(t, wgt, bias, residual=res)
         full = sp.gather(t, dim=1)                          # [b, T, c]
         return full.reshape(b, h, w, c).permute(0, 3, 1, 2)
+
+
+def refresh_static_kv(model: nn.Module, sources) -> int:
+    """Recompute every cross-attention's static K/V buffer of the contexts in ``sources`` (ids of the
+    step plan's static context tensors, just refreshed with a new job's conditioning)."""
+    n = 0
+    for m in model.modules():
+        if isinstance(m, CrossAttention):
+            n += m.refresh_static_kv(sources)
+    return n

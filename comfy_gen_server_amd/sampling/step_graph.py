@@ -30,6 +30,7 @@ disables it.
 from __future__ import annotations
 
 import logging
+import os
 import threading
 
 import torch
@@ -44,7 +45,7 @@ stats = {"capture": 0, "replay": 0, "jobs": 0}
 
 
 class _Plan:
-    __slots__ = ("graphs", "x", "params", "meta", "sig", "den", "cond", "hints", "pool")
+    __slots__ = ("graphs", "x", "params", "meta", "sig", "den", "cond", "hints", "pool", "kv_sources")
 
 
 def _ancestral(s0, s1, eta):
@@ -123,6 +124,13 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     if cond is None or any(not isinstance(v, torch.Tensor) or not v.is_cuda for v in cond.values()):
         return None
     model = guider.inner_model
+    # floating conds in the model's compute dtype up front: apply_model's .to(dtype) is then the
+    # identity, so the UNet sees the plan's static tensors themselves (static K/V keys on them)
+    try:
+        mdt = model.manual_cast_dtype or model.get_dtype()
+        cond = {k: (v.to(mdt) if v.is_floating_point() and k in ("c_crossattn", "y") else v) for k, v in cond.items()}
+    except Exception:
+        pass
     chain = _chain(ctrl)
     batched = 2 if use_uncond else 1
     # ControlNet: the per-step on/off window is decided on the HOST (one captured graph per distinct
@@ -167,6 +175,11 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     plan.x.copy_(x)
     for k, v in cond.items():
         plan.cond[k].copy_(v)
+    if plan.kv_sources:
+        # the run's constant context -> every cross-attention K/V once per job (the captured steps
+        # read the buffers instead of recomputing them each step)
+        from ..models.attention import refresh_static_kv
+        stats["kv_refresh"] = stats.get("kv_refresh", 0) + refresh_static_kv(model.diffusion_model, plan.kv_sources)
     for dst, src in zip(plan.hints, hints):
         if dst is not src:
             dst.copy_(src)
@@ -189,6 +202,9 @@ def _new_plan(x, cond, hints):
     p.sig = torch.empty(x.shape[0], device=dev, dtype=torch.float32)
     p.den = torch.empty_like(p.x)
     p.cond = {k: v.detach().clone() for k, v in cond.items()}
+    # static cross-attention K/V over the plan's context buffers (CGS_STATIC_KV=0 disables)
+    p.kv_sources = frozenset(id(v) for v in p.cond.values()) if os.environ.get("CGS_STATIC_KV", "1") != "0" \
+        else frozenset()
     p.hints = list(hints)           # the first job's prepared hint tensors become the static inputs
     p.graphs = {}
     p.pool = None
@@ -204,7 +220,7 @@ def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
     for cn, h in zip(chain, p.hints):
         cn.cond_hint = h            # get_control() then reads the plan's static hint
 
-    def body():
+    def body(kv_mode):
         ops.step_param(p.sig, p.params, p.meta, 0)
         if use_uncond:
             xin, tin = torch.cat([p.x, p.x]), torch.cat([p.sig, p.sig])
@@ -212,6 +228,8 @@ def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
             xin, tin = p.x, p.sig
         t = dict(to)
         t["sigmas"] = p.sig
+        if p.kv_sources:
+            t["kv_static"] = (kv_mode, p.kv_sources)
         control = None
         if chain:
             control = chain[0].get_control(xin, tin, p.cond, 2 if use_uncond else 1)
@@ -230,13 +248,13 @@ def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            body()                      # warm-up: autotune keys, derived weight layouts, lazy attrs
+            body("fill")                # warm-up: autotune keys, derived weight layouts, lazy attrs, K/V buffers
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if p.pool is None:
             p.pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=p.pool, stream=side):
-            body()
+            body("use")
         torch.cuda.synchronize()
     except Exception as e:  # capture-unsafe op in the step: this plan stays eager
         logging.warning("step hipGraph capture failed (%s); sampling stays eager", e)

@@ -202,3 +202,29 @@ def test_split_k_tail_inside_captured_graph(cuda):
                 assert err < 1e-2, (seed, err)
     finally:
         lib.cgs_gemm_set_variant(-1)
+
+
+@pytest.mark.gpu
+def test_step_graph_static_kv_new_prompt_per_job(cuda, monkeypatch):
+    """Cross-attention K/V of the constant context are computed once per job (prologue) and read by
+    the replayed steps: a second job with a DIFFERENT prompt through the same plan must see its own
+    K/V (equal to the eager loop), not the first job's."""
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    from comfy_gen_server_amd.parallel.dp import Job, generate_local
+    from comfy_gen_server_amd.sampling import step_graph
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_GRAPHS", mode)
+            outs = []
+            for seed, prompt in ((5, "a red cube on a table"), (9, "a forest lake at dawn, mist")):
+                job = Job(prompt=prompt, batch=2, steps=5, cfg=6.0, sampler="euler_ancestral", width=64, height=64,
+                          seed=seed)
+                outs.append(generate_local(patcher, clip, vae, job, 0, 2, decode=False).float())
+            res[mode] = outs
+        torch.cuda.synchronize()
+    assert step_graph.stats.get("kv_refresh", 0) > 0
+    for a, b in zip(res["0"], res["1"]):
+        err = (a - b).abs().max().item()
+        assert err < 2e-2 * (a.abs().max().item() + 1), err
