@@ -468,16 +468,16 @@ static int gemm_v5_launch(const void* A, const void* W, void* C, const void* bia
 
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
+template <bool LN = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_m, int tiles_n, int group_m) {
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m, const float* rs = nullptr, const float* cs = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   DenseA8 al{A, lda, M, {}};
-  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
-  pq::run(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
+  pq::run<DenseA8, LN>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
 }
-
 static int num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -490,10 +490,12 @@ static int num_cus() {
 
 static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                           long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                          hipStream_t stream) {
+                          hipStream_t stream, const float* rs = nullptr, const float* cs = nullptr) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pq::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               pq::LDS);
     attr_set = true;
   }
@@ -501,9 +503,14 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   const int tiles_m = (M + pq::BM - 1) / pq::BM;
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
-  gemm_bf16_nt_v6_kernel<<<grid, pq::THREADS, pq::LDS, stream>>>(
-      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
-      tiles_m, tiles_n, g_tile_group);
+  if (epi & EPI_LNFOLD)
+    gemm_bf16_nt_v6_kernel<true><<<grid, pq::THREADS, pq::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
+        alpha, tiles_m, tiles_n, g_tile_group, rs, cs);
+  else
+    gemm_bf16_nt_v6_kernel<false><<<grid, pq::THREADS, pq::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
+        alpha, tiles_m, tiles_n, g_tile_group);
   return (int)hipGetLastError();
 }
 
@@ -691,6 +698,9 @@ CGS_EXPORT int cgs_gemm_bf16_lnfold(const void* A, const void* W, void* C, const
       ((uintptr_t)rs % 8) || (long long)M * lda * 2 >= (1ll << 32) || (long long)N * ldw * 2 >= (1ll << 32))
     return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
+  // v6 (256x160) for the N = 640 / 1280 projections (the cross-attention query), v7 otherwise
+  if (!(epi & EPI_GEGLU) && N % 160 == 0 && N <= 1280 && K >= 128)
+    return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
   return gemm_v7_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, ws, ws_bytes, stream,
                         rs, cs);
 }

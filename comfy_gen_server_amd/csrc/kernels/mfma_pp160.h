@@ -52,7 +52,7 @@ __device__ __forceinline__ int b_col160(int r) {
 // the current tile's last two, and the epilogue (direct 8-B stores from registers, no LDS) runs
 // while they are in flight -- no per-tile prologue bubble, no LDS-staged epilogue (16-B stores for
 // 4 of the 5 column tiles, see b_col160). Needs K >= 128, N % 8 == 0.
-template <class AL>
+template <class AL, bool LN = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -142,6 +142,30 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       col = col < N ? col : N - 4;
       bv[j] = HB ? unpack4_bf16(*reinterpret_cast<const uint2*>(e.bias + col)) : float4{0.f, 0.f, 0.f, 0.f};
     }
+    if constexpr (LN) {
+      // LayerNorm folded in (MC_EPI_LNFOLD, see mfma_ppk.h): acc = rstd_r * (acc - mean_r * cs[c])
+      float4 cv[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        int col = n_w + colj(j);
+        col = col < N ? col : N - 4;
+        cv[j] = *reinterpret_cast<const float4*>(e.cs + col);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int row = m_w + 16 * i + fr;
+        row = row < M ? row : M - 1;
+        const float2 st = *reinterpret_cast<const float2*>(e.rs + 2 * (long long)row);
+        const float mr = st.x * st.y;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          acc[i][j][0] = st.y * acc[i][j][0] - mr * cv[j].x;
+          acc[i][j][1] = st.y * acc[i][j][1] - mr * cv[j].y;
+          acc[i][j][2] = st.y * acc[i][j][2] - mr * cv[j].z;
+          acc[i][j][3] = st.y * acc[i][j][3] - mr * cv[j].w;
+        }
+      }
+    }
     uint2 rw[4][5];   // residual words, all loads issued before the first store (one wait)
     if (HR) {
 #pragma unroll
@@ -189,6 +213,11 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   using T1 = std::true_type;
   const bool hb = (e.flags & MC_EPI_BIAS) != 0, hr = (e.flags & MC_EPI_RESIDUAL) != 0;
   auto epilogue = [&](int m0, int n0) {
+    if constexpr (LN) {                     // folded LayerNorm: no residual form (host-checked)
+      if (hb) epilogue_t(m0, n0, T1{}, T0{});
+      else epilogue_t(m0, n0, T0{}, T0{});
+      return;
+    }
     if (hr) {
       if (hb) epilogue_t(m0, n0, T1{}, T1{});
       else epilogue_t(m0, n0, T0{}, T1{});

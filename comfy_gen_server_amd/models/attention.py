@@ -90,6 +90,18 @@ class CrossAttention(nn.Module, DerivedMixin):
             o = ops.attention(q, k, v, self.heads)
         return self.to_out[0](o, residual=residual)
 
+    def forward_lnfold_cross(self, x, rs, norm, context, residual=None, ctx_cache=None, cache_key=None, kv=None):
+        """Cross-attention on LN(x) with the LayerNorm folded into the query GEMM."""
+        w2, cs, b2 = self._derived_get(("lnfold_q", id(norm)), lambda: ops.lnfold_weights(
+            self.to_q.weight, None, norm.weight, norm.bias))
+        q = ops.linear_lnfold(x, rs, w2, cs, b2)
+        kvs = None
+        if kv is not None and context.is_cuda and context.dtype == self.to_k.weight.dtype:
+            kvs = self.static_kv(context, kv)
+        k, v = kvs if kvs is not None else self.project_kv(context, None, ctx_cache, cache_key)
+        o = ops.attention(q, k, v, self.heads)
+        return self.to_out[0](o, residual=residual)
+
     def static_kv(self, context, kv):
         """Cross-attention K/V of a sampling run's constant context, kept in a per-context buffer
         (``kv`` = (mode, ids of the step plan's static context tensors), sampling/step_graph.py): in
@@ -263,8 +275,13 @@ class BasicTransformerBlock(nn.Module):
             else:
                 x = self.attn1.forward_lnfold(x, ops.layernorm_stats(x, self.norm1.eps), self.norm1, residual=x,
                                               sp=to.get("sp"))
-            x = self.attn2(self.norm2(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 2),
-                           kv=to.get("kv_static"))
+            if self.attn2.is_cross and self.norm2.weight is not None and self.norm2.weight.dtype == x.dtype:
+                x = self.attn2.forward_lnfold_cross(x, ops.layernorm_stats(x, self.norm2.eps), self.norm2, context,
+                                                    residual=x, ctx_cache=cache, cache_key=(key, 2),
+                                                    kv=to.get("kv_static"))
+            else:
+                x = self.attn2(self.norm2(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 2),
+                               kv=to.get("kv_static"))
             return self.ff.forward_lnfold(x, ops.layernorm_stats(x, self.norm3.eps), self.norm3, residual=x)
         n = self.norm1(x)
         if self.disable_self_attn:

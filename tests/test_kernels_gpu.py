@@ -551,7 +551,7 @@ def test_conv_v7_split_tail(cuda, N, C1, C2, H, W, Cout, k, res):
 
 
 @pytest.mark.parametrize("M,C,N,geglu", [(4096, 640, 1920, False), (1000, 1280, 3840, False), (2048, 640, 5120, True),
-                                         (16384, 1280, 10240, True)])
+                                         (16384, 1280, 10240, True), (4096, 640, 640, False), (2000, 1280, 1280, False)])
 def test_layernorm_folded_gemm(cuda, M, C, N, geglu):
     """K07 folded: LN(x) @ W^T + b from the raw rows + (mean, rstd) -- fp32 reference of LN then GEMM."""
     torch.manual_seed(0)
