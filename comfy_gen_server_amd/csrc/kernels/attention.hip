@@ -861,6 +861,116 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_wide_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wide-head path, materialised form (K22 v2). At one head of D = 512 the flash kernel above is
+// bound by its K/V re-reads (32 queries per workgroup: 64 KB of K/V per 2 MFLOP), while the score
+// matrix of one image (16 k x 16 k fp32 = 1 GiB) is small next to 288 GB of HBM. So the op layer
+// runs, per image and query chunk: S = (scale log2e) Q K^T on the v7 GEMM with an fp32 epilogue
+// (MC_EPI_F32OUT), P = softmax2(S) -> bf16 (below, one pass over S), O = P (V^T)^T on the v7 GEMM
+// (split-K tail) with V^T from the transpose below. Two big MFMA GEMMs + two streaming passes.
+
+// P[r, :] = 2^(S[r, :] - max) / sum, S already in log2 units. One workgroup per row, the row held
+// in registers (NV float4 per thread: cols <= 1024 NV), cols % 4 == 0.
+template <int NV>
+__global__ __launch_bounds__(256) void softmax2_f32_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y,
+                                                                int cols, long long ldx, long long ldy) {
+  __shared__ float red[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* xr = x + (long long)blockIdx.x * ldx;
+  u16* yr = y + (long long)blockIdx.x * ldy;
+  float4 v[NV];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 256 + tid) * 4;
+    v[i] = c < cols ? *reinterpret_cast<const float4*>(xr + c) : float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    mx = fmaxf(mx, fmaxf(fmaxf(v[i].x, v[i].y), fmaxf(v[i].z, v[i].w)));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i].x = __builtin_amdgcn_exp2f(v[i].x - mx);
+    v[i].y = __builtin_amdgcn_exp2f(v[i].y - mx);
+    v[i].z = __builtin_amdgcn_exp2f(v[i].z - mx);
+    v[i].w = __builtin_amdgcn_exp2f(v[i].w - mx);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) red[4 + wave] = s;
+  __syncthreads();
+  const float inv = 1.f / ((red[4] + red[5]) + (red[6] + red[7]));
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 256 + tid) * 4;
+    if (c < cols) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(v[i].x * inv) | ((uint32_t)f2bf(v[i].y * inv) << 16);
+      w.y = (uint32_t)f2bf(v[i].z * inv) | ((uint32_t)f2bf(v[i].w * inv) << 16);
+      *reinterpret_cast<uint2*>(yr + c) = w;
+    }
+  }
+}
+
+CGS_EXPORT int cgs_softmax2_f32_bf16(const float* x, void* y, long long rows, int cols, long long ldx, long long ldy,
+                                     hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (cols <= 0 || cols % 4 || ldx % 4 || ldy % 4 || rows > 0x7fffffffLL || cols > 16384 ||
+      (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 7))
+    return (int)hipErrorInvalidValue;
+  const unsigned g = (unsigned)rows;
+  u16* yy = (u16*)y;
+  if (cols <= 1024) softmax2_f32_bf16_kernel<1><<<g, 256, 0, stream>>>(x, yy, cols, ldx, ldy);
+  else if (cols <= 2048) softmax2_f32_bf16_kernel<2><<<g, 256, 0, stream>>>(x, yy, cols, ldx, ldy);
+  else if (cols <= 4096) softmax2_f32_bf16_kernel<4><<<g, 256, 0, stream>>>(x, yy, cols, ldx, ldy);
+  else if (cols <= 8192) softmax2_f32_bf16_kernel<8><<<g, 256, 0, stream>>>(x, yy, cols, ldx, ldy);
+  else softmax2_f32_bf16_kernel<16><<<g, 256, 0, stream>>>(x, yy, cols, ldx, ldy);
+  return (int)hipGetLastError();
+}
+
+// y[c, r] = x[r, c] for a bf16 [rows, cols] matrix (row stride ldx) -> [cols, rows] (row stride ldy):
+// 64 x 64 tiles through LDS, 16-B global loads and stores. rows, cols % 8 == 0.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restrict__ x, u16* __restrict__ y, int rows,
+                                                             int cols, long long ldx, long long ldy) {
+  __shared__ u16 t[64][64 + 2];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, ch = tid & 7, rr = tid >> 3;   // 8 chunks of 8 elements x 32 rows
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int r = rr + 32 * it, gr = r0 + r, gc = c0 + 8 * ch;
+    s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (gr < rows && gc < cols) v = *reinterpret_cast<const s16x8*>(x + (long long)gr * ldx + gc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[r][8 * ch + j] = (u16)v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = rr + 32 * it, gc = c0 + c, gr = r0 + 8 * ch;
+    if (gc < cols && gr < rows) {
+      s16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (short)t[8 * ch + j][c];
+      *reinterpret_cast<s16x8*>(y + (long long)gc * ldy + gr) = v;
+    }
+  }
+}
+
+CGS_EXPORT int cgs_transpose_bf16(const void* x, void* y, int rows, int cols, long long ldx, long long ldy,
+                                  hipStream_t stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (rows % 8 || cols % 8 || ldx % 8 || ldy % 8 || ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 g((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  transpose_bf16_kernel<<<g, 256, 0, stream>>>((const u16*)x, (u16*)y, rows, cols, ldx, ldy);
+  return (int)hipGetLastError();
+}
+
 static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel, 3 short-KV kernel, 4 D=64 r2
 CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
 

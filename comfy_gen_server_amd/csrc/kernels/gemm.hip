@@ -25,6 +25,7 @@
 #define EPI_RESIDUAL 2
 #define EPI_GEGLU 4
 #define EPI_LNFOLD 8
+#define EPI_F32OUT 16   // fp32 C (v7 only; attention scores of the wide-head path)
 
 // fp8 e4m3fn (OCP) -> bf16 bits, exact (every e4m3 value is a bf16 value); NaN stays NaN.
 __device__ __forceinline__ u16 fp8e4m3_to_bf16(uint32_t b) {
@@ -531,7 +532,7 @@ struct DenseA32 {
 
 // ------------------------------------------------------------------------------------------------
 // v7: persistent 256 x 256 x 64 ping-pong with cross-tile prefetch and a register epilogue (mfma_ppk.h)
-template <bool GG, bool LN = false>
+template <bool GG, bool LN = false, bool F32 = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v7_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   DenseA32 al{reinterpret_cast<const unsigned char*>(A), lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
-  ppk::run<GG, LN>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m, sp);
+  ppk::run<GG, LN, DenseA32, F32>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m, sp);
 }
 
 // ws (may be null): split-K tail workspace of >= cgs_v7_ws_bytes(M, N, K) bytes; without it the
@@ -558,6 +559,8 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v7_kernel<false, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, ppk::LDS);
     attr_set = true;
   }
@@ -588,7 +591,11 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
   gemm_bf16_nt_v7_kernel<GG, LNF><<<grid, ppk::THREADS, ppk::LDS, stream>>>(                                        \
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, \
       tiles_m, tiles_n, g_tile_group, sp, rs, cs)
-  if (epi & EPI_GEGLU) {
+  if (epi & EPI_F32OUT) {
+    gemm_bf16_nt_v7_kernel<false, false, true><<<grid, ppk::THREADS, ppk::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+        tiles_m, tiles_n, g_tile_group, sp, rs, cs);
+  } else if (epi & EPI_GEGLU) {
     if (ln) CGS_V7L(true, true);
     else CGS_V7L(true, false);
   } else {
@@ -624,6 +631,12 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   bool v3_ok = (K % 32 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && (nout % 8 == 0) && (ldc % 8 == 0) &&
                (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
                ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
+  if (epi & EPI_F32OUT) {   // fp32 output: v7 only, plain / bias epilogue
+    if ((epi & (EPI_GEGLU | EPI_RESIDUAL | EPI_LNFOLD)) || !v3_ok || K % 64 || K < 128 || ((uintptr_t)bias % 8) ||
+        (long long)M * lda * 2 >= (1ll << 32) || (long long)N * ldw * 2 >= (1ll << 32))
+      return (int)hipErrorInvalidValue;
+    return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
+  }
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && !(epi & EPI_GEGLU) && ((uintptr_t)bias % 8 == 0))
     return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&

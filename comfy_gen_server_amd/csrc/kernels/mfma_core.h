@@ -24,6 +24,7 @@ typedef __attribute__((address_space(3))) void mc_lds_void;
 #define MC_EPI_RESIDUAL 2
 #define MC_EPI_GEGLU 4
 #define MC_EPI_LNFOLD 8   // y = rstd_r * (acc - mean_r * cs[c]) + bias[c]  (LayerNorm folded into the GEMM)
+#define MC_EPI_F32OUT 16  // v7 only: C is fp32 (ldc in floats), no GEGLU / residual (attention scores, K22)
 
 namespace mc {
 

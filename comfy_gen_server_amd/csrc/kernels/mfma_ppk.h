@@ -93,7 +93,7 @@ __device__ __forceinline__ int b_col_perm(int nq, int r) {
   }
 }
 
-template <bool GG, bool LN = false, class AL>
+template <bool GG, bool LN = false, class AL, bool F32 = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m,
                                     Split sp = Split{0, 1, nullptr, nullptr, 0}) {
@@ -313,6 +313,30 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           }
           if (row < M && ocol < Nout) store16(e.C + (long long)row * e.ldc + ocol, h[0], h[1], e.flags);
         }
+    } else if constexpr (F32 && !HR) {
+      // fp32 output (materialised attention scores): two 16-B stores per (row, nq) -- 32 per lane
+      // per tile, so the caller keeps the plain vmcnt windows (stores_pending stays false)
+      float* Cf = reinterpret_cast<float*>(e.C);
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wr * 128 + mq * 64 + 16 * i + fr;
+#pragma unroll
+          for (int nq = 0; nq < 2; ++nq) {
+            const int col = ncw + nq * 32 + 8 * fq;
+            if (row < M && col < N) {
+              float* p = Cf + (long long)row * e.ldc + col;
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const f32x4 v = acc[mq * 4 + i][nq * 2 + j];
+                const float4 b = bv[nq][j];
+                *reinterpret_cast<float4*>(p + 4 * j) =
+                    float4{v[0] * e.alpha + b.x, v[1] * e.alpha + b.y, v[2] * e.alpha + b.z, v[3] * e.alpha + b.w};
+              }
+            }
+          }
+        }
     } else {
       // residual words: all 16 loads issued before the first store (one wait, one drain)
       uint4 rw[2][4][2];
@@ -497,7 +521,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     }
     epilogue(m0, n0);
     // a full tile issued every one of its E stores (partial tiles may skip some: keep plain waits)
-    stores_pending = (m0 + BM <= M) && (n0 + BN <= N);
+    stores_pending = (m0 + BM <= M) && (n0 + BN <= N) && !F32;
     if (!has_next) break;
     u = un;
     m0 = nm0;

@@ -293,6 +293,11 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
                 1.0 / math.sqrt(D), _ptr(kp), 1 if causal else 0, _stream()), "cgs_flash_attn_fwd")
             return o
 
+        if (wide_ok and heads == 1 and _WIDE_MAT and kp is None and Sk % 64 == 0 and Sk <= 16384
+                and Sq * Sk >= (1 << 22)
+                and _native.has_kernel("cgs_softmax2_f32_bf16") and _wide_mat_ok(q, k, v)):
+            count("attention", "hip")
+            return _attention_wide_mat(q, k, v)
         choice = "hip"
         # The vendor SDPA is a tuning candidate only on explicit request: the hot path is the
         # hand-written kernel (K02/K03), never an SDPA fallback.
@@ -312,6 +317,51 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     else:
         count("attention", "torch")
     return attention_reference(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
+
+
+EPI_F32OUT = 16
+# K22: one-head D=512 attention (KL-VAE mid block) through materialised scores (CGS_WIDE_ATTN=flash
+# keeps the flash kernel). S chunks are capped at 2^28 elements (1 GiB fp32).
+_WIDE_MAT = os.environ.get("CGS_WIDE_ATTN", "mat") != "flash"
+_WIDE_CHUNK_ELEMS = 1 << 28
+
+
+def _wide_mat_ok(q, k, v) -> bool:
+    ts = (q, k, v)
+    return (all(t.stride(1) % 8 == 0 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in ts)
+            and q.shape[1] * q.stride(1) * 2 < (1 << 32) and k.shape[1] * k.stride(1) * 2 < (1 << 32))
+
+
+def _attention_wide_mat(q, k, v):
+    """softmax(q k^T / sqrt(d)) v for one head of d = 512, per image and query chunk:
+    S = (log2e / sqrt(d)) q k^T on the v7 GEMM with an fp32 epilogue, P = softmax2(S) -> bf16 in one
+    pass, O = P V on the v7 GEMM against V^T (transposed once per image). The reference computes the
+    same op through a materialised softmax too (comfy/ldm/modules/diffusionmodules/model.py:227-292)."""
+    B, Sq, D = q.shape
+    Sk = k.shape[1]
+    lib, st = _lib(), _stream()
+    dev = q.device
+    o = torch.empty((B, Sq, D), device=dev, dtype=q.dtype)
+    chunk = max(256, min(Sq, _WIDE_CHUNK_ELEMS // Sk))
+    s = torch.empty((chunk, Sk), device=dev, dtype=torch.float32)
+    p = torch.empty((chunk, Sk), device=dev, dtype=torch.bfloat16)
+    vt = torch.empty((D, Sk), device=dev, dtype=torch.bfloat16)
+    alpha = 1.4426950408889634 / math.sqrt(D)
+    for b in range(B):
+        _check(lib.cgs_transpose_bf16(v[b].data_ptr(), vt.data_ptr(), Sk, D, v.stride(1), Sk, st), "cgs_transpose_bf16")
+        for r0 in range(0, Sq, chunk):
+            m = min(chunk, Sq - r0)
+            qa = q.data_ptr() + 2 * (b * q.stride(0) + r0 * q.stride(1))
+            ws = _v7_ws(m, Sk, D, dev)
+            _check(lib.cgs_gemm_bf16_v7ws(qa, k[b].data_ptr(), s.data_ptr(), None, None, m, Sk, D, q.stride(1),
+                                          k.stride(1), Sk, 0, EPI_F32OUT, alpha, _ptr(ws),
+                                          0 if ws is None else ws.numel(), st), "cgs_gemm_bf16_v7ws(f32)")
+            _check(lib.cgs_softmax2_f32_bf16(s.data_ptr(), p.data_ptr(), m, Sk, Sk, Sk, st), "cgs_softmax2_f32_bf16")
+            ws = _v7_ws(m, D, Sk, dev)
+            oa = o.data_ptr() + 2 * (b * o.stride(0) + r0 * o.stride(1))
+            _check(lib.cgs_gemm_bf16_v7ws(p.data_ptr(), vt.data_ptr(), oa, None, None, m, D, Sk, Sk, Sk, D, 0, 0, 1.0,
+                                          _ptr(ws), 0 if ws is None else ws.numel(), st), "cgs_gemm_bf16_v7ws")
+    return o
 
 
 def _sdpa(q, k, v, heads, causal=False):

@@ -324,6 +324,39 @@ def test_attention_wide_d512(cuda, B, S, Sk):
     assert _rel(o, ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,S,chunk", [(2, 4096, 1 << 28), (1, 4096, 1000 * 4096), (1, 16384, 1 << 28)])
+def test_attention_wide_materialised(cuda, B, S, chunk, monkeypatch):
+    """K22 v2: fp32 scores on the v7 GEMM (MC_EPI_F32OUT) -> one-pass softmax2 -> P (V^T)^T on the
+    v7 GEMM, over q/k/v that are strided views of one fused QKV tensor (the VAE AttnBlock layout),
+    with query chunks (incl. a partial last chunk) vs the fp32 reference."""
+    monkeypatch.setattr(core, "_WIDE_CHUNK_ELEMS", chunk)
+    torch.manual_seed(9)
+    D = 512
+    qkv = (torch.randn(B, S, 3 * D, device=cuda) * 0.6).to(torch.bfloat16)
+    qkv[:, S // 3, D:2 * D] *= 4.0          # a spiked key
+    q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+    o = ops.attention(q, k, v, 1)
+    assert ops.stats().get(("attention", "hip"), 0) == 1
+    rows = torch.arange(0, S, 7, device=cuda)[:512]      # reference on a row subset (S x S fp32 per image)
+    ref = core.attention_reference(q[:, rows].float(), k.float(), v.float(), 1)
+    assert torch.isfinite(o).all()
+    assert _rel(o[:, rows], ref) < 2e-2
+
+
+def test_softmax2_and_transpose_kernels(cuda):
+    lib = core._lib()
+    x = torch.randn(37, 5000, device=cuda) * 6
+    y = torch.empty(37, 5000, device=cuda, dtype=torch.bfloat16)
+    assert lib.cgs_softmax2_f32_bf16(x.data_ptr(), y.data_ptr(), 37, 5000, 5000, 5000, core._stream()) == 0
+    ref = torch.softmax(x * math.log(2.0), dim=-1)
+    assert (y.float() - ref).abs().max().item() < 4e-3 * ref.max().item() + 1e-6
+    assert torch.allclose(y.float().sum(-1), torch.ones(37, device=cuda), atol=2e-2)
+    a = torch.randn(200, 72, device=cuda).to(torch.bfloat16)
+    t = torch.empty(72, 200, device=cuda, dtype=torch.bfloat16)
+    assert lib.cgs_transpose_bf16(a.data_ptr(), t.data_ptr(), 200, 72, 72, 200, core._stream()) == 0
+    assert torch.equal(t, a.t())
+
+
 def test_vae_mid_attention_block_native(cuda):
     """The VAE AttnBlock runs fused-QKV GEMM + the D=512 kernel + out-proj GEMM (no SDPA)."""
     from comfy_gen_server_amd.models.layers import init_random_
