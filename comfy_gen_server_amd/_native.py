@@ -80,6 +80,9 @@ KERNEL_SIGNATURES = {
                            _L, _L, _L,                  # v strides
                            _L, _L, _L,                  # o strides
                            _F, _P, _I, _P],             # scale, key_mask(int8 [B,Sk] or null), causal, stream
+    # same + fp32 LSE [B, H, Sq] out (ring attention merge): q,k,v,o,lse, B,H,Sq,Sk,D, 12 strides, scale
+    "cgs_flash_attn_fwd_lse": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L,
+                               _F, _P],
     # C[M,N] = A[M,K] @ W[N,K]^T (+bias) (+residual) | GEGLU epilogue; bf16 in/out, fp32 acc
     "cgs_gemm_bf16": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
     "cgs_gemm_set_variant": [_I],   # -1 auto, 1 force 128x128 register-staged, 2 force 256-tile glds, 3 mfma32 4-stage

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256, (DP >= 160 ? 1 : 2)) void flash_fwd_kernel(
     int B, int H, int Sq, int Sk, int D,
     long long qsb, long long qss, long long qsh, long long ksb, long long kss, long long ksh,
     long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
-    float scale_log2, const signed char* __restrict__ key_mask, int causal, int nqb) {
+    float scale_log2, const signed char* __restrict__ key_mask, int causal, int nqb, float* __restrict__ lse) {
   constexpr int KS = DP / 16;        // k-steps of the QK product
   constexpr int NDT = DP / 32;       // 32-wide d tiles of the output
   constexpr int LDW = DP + 8;        // padded LDS row (elements)
@@ -189,6 +189,9 @@ __global__ __launch_bounds__(256, (DP >= 160 ? 1 : 2)) void flash_fwd_kernel(
   // ---- epilogue: O[q][d] = O^T[d][q] / l
   float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  // natural-log LSE of the scaled scores (ring attention merge): sum_k e^(s scale) = 2^m_run * l_tot
+  if (lse && q_ok && hf == 0)
+    lse[((long long)b * H + h) * Sq + q_row] = l_tot > 0.f ? (m_run + __log2f(l_tot)) * 0.69314718055994531f : -INFINITY;
   if (q_ok) {
     u16* orow = obase + (long long)q_row * oss;
 #pragma unroll
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
     long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
-    float c, int nqb) {
+    float c, int nqb, float* __restrict__ lse = nullptr) {
   __shared__ __attribute__((aligned(16))) u16 Ks[2][64 * 64];
   __shared__ __attribute__((aligned(16))) u16 Vs[2][64 * 64];
 
@@ -391,6 +394,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
   // epilogue: O[q][d] = O^T[d][q] / l
   float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (lse && q_ok && hf == 0)
+    lse[((long long)b * H + h) * Sq + q_row] = l_tot > 0.f ? (m_run + __log2f(l_tot)) * 0.69314718055994531f : -INFINITY;
   if (q_ok) {
     u16* orow = obase + (long long)q_row * oss;
 #pragma unroll
@@ -974,11 +979,10 @@ CGS_EXPORT int cgs_transpose_bf16(const void* x, void* y, int rows, int cols, lo
 static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel, 3 short-KV kernel, 4 D=64 r2
 CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
 
-CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
-                                  int D, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
-                                  long long ksh, long long vsb, long long vss, long long vsh, long long osb,
-                                  long long oss, long long osh, float scale, const void* key_mask, int causal,
-                                  hipStream_t stream) {
+static int flash_attn_impl(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, int D,
+                           long long qsb, long long qss, long long qsh, long long ksb, long long kss, long long ksh,
+                           long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
+                           float scale, const void* key_mask, int causal, float* lse, hipStream_t stream) {
   if (D % 8) return (int)hipErrorInvalidValue;
   int nqb = (Sq + ATT_QB - 1) / ATT_QB;
   long long nwg = (long long)nqb * B * H;
@@ -987,7 +991,7 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
   const bool al16 = ((qss | kss | vss | oss | qsb | ksb | vsb | osb | qsh | ksh | vsh | osh) & 7) == 0 &&
                     ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
                       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) & 15) == 0;
-  if (D == 64 && !key_mask && !causal && al16 && Sk > 0 && Sk <= 128 &&
+  if (D == 64 && !key_mask && !causal && al16 && Sk > 0 && Sk <= 128 && !lse &&
       (g_attn_variant == 0 || g_attn_variant == 3)) {
     const int nqb3 = (Sq + 127) / 128;
     const long long nwg3 = (long long)nqb3 * B * H;
@@ -1005,7 +1009,7 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
   }
   if (g_attn_variant == 3) return (int)hipErrorInvalidValue;
   if (D == WD_D) {
-    if (key_mask || causal || !al16 || Sk <= 0) return (int)hipErrorInvalidValue;
+    if (key_mask || causal || !al16 || Sk <= 0 || lse) return (int)hipErrorInvalidValue;
     const int nqb4 = (Sq + 31) / 32;
     const long long nwg4 = (long long)nqb4 * B * H;
     if (nwg4 > 0x7fffffff) return (int)hipErrorInvalidValue;
@@ -1014,7 +1018,7 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
         osb, oss, osh, sl2, nqb4);
     return (int)hipGetLastError();
   }
-  if (D == 64 && !key_mask && !causal && al16 && g_attn_variant == 4 && Sk > 0) {
+  if (D == 64 && !key_mask && !causal && al16 && g_attn_variant == 4 && Sk > 0 && !lse) {
     int nqb2 = (Sq + 255) / 256;
     long long nwg2 = (long long)nqb2 * B * H;
     if (nwg2 > 0x7fffffff) return (int)hipErrorInvalidValue;
@@ -1029,7 +1033,7 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
     if (nwg2 > 0x7fffffff) return (int)hipErrorInvalidValue;
     attn_fwd_d64_kernel<<<dim3((unsigned)nwg2), 512, 0, stream>>>(
         (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
-        osb, oss, osh, sl2, nqb2);
+        osb, oss, osh, sl2, nqb2, lse);
     return (int)hipGetLastError();
   }
   if (g_attn_variant == 2) return (int)hipErrorInvalidValue;
@@ -1037,7 +1041,7 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
 #define ATT_LAUNCH(DPV)                                                                                         \
   flash_fwd_kernel<DPV><<<grid, 256, 0, stream>>>((const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, B, H, Sq, \
                                                    Sk, D, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, oss,  \
-                                                   osh, sl2, (const signed char*)key_mask, causal, nqb)
+                                                   osh, sl2, (const signed char*)key_mask, causal, nqb, lse)
   if (D <= 32) ATT_LAUNCH(32);
   else if (D <= 64) ATT_LAUNCH(64);
   else if (D <= 96) ATT_LAUNCH(96);
@@ -1046,4 +1050,24 @@ CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, v
   else return (int)hipErrorInvalidValue;
 #undef ATT_LAUNCH
   return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
+                                  int D, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
+                                  long long ksh, long long vsb, long long vss, long long vsh, long long osb,
+                                  long long oss, long long osh, float scale, const void* key_mask, int causal,
+                                  hipStream_t stream) {
+  return flash_attn_impl(q, k, v, o, B, H, Sq, Sk, D, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, oss, osh, scale,
+                         key_mask, causal, nullptr, stream);
+}
+
+// Same, plus the per-(b, h, query) natural-log LSE of the scaled scores (fp32 [B, H, Sq]) for
+// merging partial results over K/V blocks (ring attention, parallel/sp.py). D = 64 or the generic kernel.
+CGS_EXPORT int cgs_flash_attn_fwd_lse(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
+                                      int Sq, int Sk, int D, long long qsb, long long qss, long long qsh, long long ksb,
+                                      long long kss, long long ksh, long long vsb, long long vss, long long vsh,
+                                      long long osb, long long oss, long long osh, float scale, hipStream_t stream) {
+  if (!lse) return (int)hipErrorInvalidValue;
+  return flash_attn_impl(q, k, v, o, B, H, Sq, Sk, D, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, oss, osh, scale,
+                         nullptr, 0, lse, stream);
 }

@@ -585,7 +585,9 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
       U = sp.t_full + tail * sp.S;
     }
   }
-  const int grid = (int)(U < num_cus() ? U : num_cus());
+  static const int grid_cap = getenv("CGS_V7_GRID") ? atoi(getenv("CGS_V7_GRID")) : 0;   // diagnostics only
+  int grid = (int)(U < num_cus() ? U : num_cus());
+  if (grid_cap > 0 && grid > grid_cap) grid = grid_cap;
   const bool ln = (epi & EPI_LNFOLD) != 0;
 #define CGS_V7L(GG, LNF)                                                                                            \
   gemm_bf16_nt_v7_kernel<GG, LNF><<<grid, ppk::THREADS, ppk::LDS, stream>>>(                                        \

@@ -319,6 +319,38 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     return attention_reference(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
 
 
+def attention_lse(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int):
+    """Unmasked attention plus the natural-log log-sum-exp of the scaled scores per (b, h, query):
+    ``(o [B, Sq, H*D] in q's dtype, lse fp32 [B, H, Sq])`` -- the partial result of one K/V block
+    that ring attention (parallel/sp.py) merges across blocks. Device: the flash kernels (D = 64
+    fast kernel, generic D <= 160) write the LSE from their running max / sum; else fp32 torch."""
+    B, Sq, HD = q.shape
+    Sk = k.shape[1]
+    D = HD // heads
+    be = backend_for("attention", q, "cgs_flash_attn_fwd_lse")
+    if (be == "hip" and D in _FLASH_HEAD_DIMS and q.dtype == torch.bfloat16 and k.dtype == q.dtype
+            and v.dtype == q.dtype and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1 and Sk > 0):
+        o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
+        lse = torch.empty((B, heads, Sq), device=q.device, dtype=torch.float32)
+        count("attention", "hip")
+        _check(_lib().cgs_flash_attn_fwd_lse(
+            q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), B, heads, Sq, Sk, D,
+            q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
+            o.stride(0), o.stride(1), D, 1.0 / math.sqrt(D), _stream()), "cgs_flash_attn_fwd_lse")
+        return o, lse
+    if q.device.type != "cpu":
+        vendor_fallback("attention", f"LSE form: dtype {q.dtype}, head dim {D}")
+    else:
+        count("attention", "torch")
+    qh = q.float().reshape(B, Sq, heads, D).transpose(1, 2)
+    kh = k.float().reshape(B, Sk, heads, D).transpose(1, 2)
+    vh = v.float().reshape(B, Sk, heads, D).transpose(1, 2)
+    s = (qh @ kh.transpose(-2, -1)) * (D ** -0.5)
+    lse = torch.logsumexp(s, dim=-1)
+    o = (torch.softmax(s, dim=-1) @ vh).transpose(1, 2).reshape(B, Sq, HD)
+    return o.to(q.dtype), lse
+
+
 EPI_F32OUT = 16
 # K22: one-head D=512 attention (KL-VAE mid block) through materialised scores (CGS_WIDE_ATTN=flash
 # keeps the flash kernel). S chunks are capped at 2^28 elements (1 GiB fp32).

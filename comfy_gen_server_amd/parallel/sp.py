@@ -61,17 +61,12 @@ def ulysses_attention(q, k, v, heads: int, group=None):
     return torch.stack(back, dim=2).reshape(B, Sl, HD)
 
 
-def _partial_attention(q, k, v, heads, scale):
-    """softmax-normalised partial attention of q against one K/V block + its log-sum-exp (fp32)."""
+def _partial_attention(q, k, v, heads):
+    """Partial attention of q against one K/V block: (o fp32 [B, Sq, H, D], lse fp32 [B, Sq, H, 1]).
+    The HIP flash kernels produce both in one pass (``ops.attention_lse``); the scores never exist."""
     B, Sq, HD = q.shape
-    D = HD // heads
-    qh = q.float().view(B, Sq, heads, D).transpose(1, 2)
-    kh = k.float().view(B, k.shape[1], heads, D).transpose(1, 2)
-    vh = v.float().view(B, v.shape[1], heads, D).transpose(1, 2)
-    s = (qh @ kh.transpose(-2, -1)) * scale
-    lse = torch.logsumexp(s, dim=-1, keepdim=True)        # [B, h, Sq, 1]
-    o = torch.softmax(s, dim=-1) @ vh                      # [B, h, Sq, D]
-    return o, lse
+    o, lse = ops.attention_lse(q, k, v, heads)
+    return o.float().view(B, Sq, heads, HD // heads), lse.transpose(1, 2).unsqueeze(-1)
 
 
 def ring_attention(q, k, v, heads: int, group=None):
@@ -79,8 +74,6 @@ def ring_attention(q, k, v, heads: int, group=None):
     if P == 1:
         return ops.attention(q, k, v, heads)
     B, Sl, HD = q.shape
-    D = HD // heads
-    scale = D ** -0.5
     ranks = dist.get_process_group_ranks(group) if group is not None else list(range(P))
     nxt, prv = ranks[(r + 1) % P], ranks[(r - 1) % P]
     kv = torch.cat([k, v], dim=-1).contiguous()
@@ -91,10 +84,10 @@ def ring_attention(q, k, v, heads: int, group=None):
             recv = torch.empty_like(kv)
             reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, kv, nxt, group),
                                            dist.P2POp(dist.irecv, recv, prv, group)])
-        o, lse = _partial_attention(q, kv[..., :HD], kv[..., HD:], heads, scale)
+        o, lse = _partial_attention(q, kv[..., :HD], kv[..., HD:], heads)
         if o_acc is None:
             o_acc, lse_acc = o, lse
-        else:
+        else:                                               # log-sum-exp merge of the two partials
             m = torch.maximum(lse_acc, lse)
             wa, wb = torch.exp(lse_acc - m), torch.exp(lse - m)
             o_acc = (o_acc * wa + o * wb) / (wa + wb)
@@ -103,7 +96,7 @@ def ring_attention(q, k, v, heads: int, group=None):
             req.wait()
         if step < P - 1:
             kv = recv
-    return o_acc.transpose(1, 2).reshape(B, Sl, HD).to(q.dtype)
+    return o_acc.reshape(B, Sl, HD).to(q.dtype)
 
 
 def shard_sequence(x, group=None, dim=1):

@@ -343,6 +343,32 @@ def test_attention_wide_materialised(cuda, B, S, chunk, monkeypatch):
     assert _rel(o[:, rows], ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,S,Sk,D", [(2, 10, 1024, 1024, 64), (1, 4, 300, 77, 64), (2, 5, 200, 333, 80),
+                                        (1, 2, 130, 64, 40)])
+def test_attention_lse_and_ring_merge(cuda, B, H, S, Sk, D):
+    """Flash kernels with the LSE output (ring attention partials): o and lse vs fp32 torch, and two
+    K/V halves merged by parallel/sp.py's log-sum-exp rule == attention over the whole K/V."""
+    from comfy_gen_server_amd.parallel import sp
+    torch.manual_seed(11)
+    q = torch.randn(B, S, H * D, device=cuda).to(torch.bfloat16)
+    k = torch.randn(B, Sk, H * D, device=cuda).to(torch.bfloat16)
+    v = torch.randn(B, Sk, H * D, device=cuda).to(torch.bfloat16)
+    o, lse = ops.attention_lse(q, k, v, H)
+    assert ops.stats().get(("attention", "hip"), 0) == 1
+    qh = q.float().view(B, S, H, D).transpose(1, 2)
+    kh = k.float().view(B, Sk, H, D).transpose(1, 2)
+    s = (qh @ kh.transpose(-1, -2)) * D ** -0.5
+    assert (lse - torch.logsumexp(s, -1)).abs().max().item() < 2e-2
+    assert _rel(o, core.attention_reference(q.float(), k.float(), v.float(), H)) < 2e-2
+    h = Sk // 2
+    o1, l1 = sp._partial_attention(q, k[:, :h], v[:, :h], H)
+    o2, l2 = sp._partial_attention(q, k[:, h:], v[:, h:], H)
+    m = torch.maximum(l1, l2)
+    wa, wb = torch.exp(l1 - m), torch.exp(l2 - m)
+    merged = ((o1 * wa + o2 * wb) / (wa + wb)).reshape(B, S, H * D)
+    assert _rel(merged, core.attention_reference(q.float(), k.float(), v.float(), H)) < 2e-2
+
+
 def test_softmax2_and_transpose_kernels(cuda):
     lib = core._lib()
     x = torch.randn(37, 5000, device=cuda) * 6
