@@ -145,6 +145,10 @@ KERNEL_SIGNATURES = {
     "cgs_v7_ws_bytes": [_I, _I, _I],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
     "cgs_conv2d_nhwc_v7ws": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P],
+    # K29 FreeU low-frequency filter: x, y, coef ws, B, C, H, W, x strides x4, y strides x4, t, scale, dtype
+    "cgs_fourier_filter": [_P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _I, _F, _I, _P],
+    # K30 ToMe matching: a, b, ws, vmax, imax(i64), B, Na, Nb, C, a strides (batch, row), b strides, dtype
+    "cgs_tome_match": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _I, _P],
     # K22 materialised wide-head attention: fp32 S -> bf16 P row softmax (log2 units) and a bf16 transpose
     "cgs_softmax2_f32_bf16": [_P, _P, _L, _I, _L, _L, _P],             # x(f32), y(bf16), rows, cols, ldx, ldy
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy

@@ -496,3 +496,231 @@ CGS_EXPORT int cgs_pooled_gather(const long long* ids, const void* x, void* out,
   CGS_DISPATCH_DT(dtype, pooled_gather_kernel, <<<B, 256, 0, stream>>>(ids, x, out, S, D));
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- K29: FreeU Fourier filter
+// Reference (comfy_extras/nodes_freelunch.py:6-23): fftn -> fftshift -> scale the 2t x 2t
+// low-frequency square [H/2 - t, H/2 + t) x [W/2 - t, W/2 + t) -> ifftshift -> ifftn -> real.
+// That square is the frequency set K = {-t .. t-1}^2, and the op is linear, so
+//   y = x + (scale - 1) * Re( (1/HW) sum_{k in K} X_k e^{+2 pi i k.p} ),  X_k = sum_p x_p e^{-2 pi i k.p}
+// -- exact, with (2t)^2 DFT coefficients per (b, c) instead of two full FFTs: pass 1 reduces the
+// coefficients (one wave per 64 channels x 4 pixel lanes), pass 2 applies them. Any strides (NCHW or
+// channels_last); t <= 4.
+namespace {
+constexpr int FF_MAXM = 64;
+
+template <int DT>
+__global__ __launch_bounds__(256) void fourier_coef_kernel(const u16* __restrict__ x, float* __restrict__ coef, int C,
+                                                           int H, int W, long long sb, long long sc, long long sy,
+                                                           long long sx, int t) {
+  __shared__ float red[4][64][2];
+  const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int n = 2 * t, nm = n * n;
+  const float ty = 6.283185307179586f / H, tx = 6.283185307179586f / W;
+  for (int m = 0; m < nm; ++m) {
+    const int ky = m / n - t, kx = m % n - t;
+    float re = 0.f, im = 0.f;
+    if (c < C) {
+      const u16* xb = x + b * sb + c * sc;
+      for (int p = sub; p < H * W; p += 4) {
+        const int py = p / W, px = p - py * W;
+        const float v = cvt_in<DT>(xb[py * sy + px * sx]);
+        float sn, cs;
+        // angle reduced mod 1 turn before sincos (exact integer phase)
+        const int ph_y = (ky * py) % H, ph_x = (kx * px) % W;
+        __sincosf(ty * ph_y + tx * ph_x, &sn, &cs);
+        re += v * cs;
+        im -= v * sn;
+      }
+    }
+    red[sub][threadIdx.x & 63][0] = re;
+    red[sub][threadIdx.x & 63][1] = im;
+    __syncthreads();
+    if (sub == 0 && c < C) {
+      const int l = threadIdx.x & 63;
+      const float r = (red[0][l][0] + red[1][l][0]) + (red[2][l][0] + red[3][l][0]);
+      const float i = (red[0][l][1] + red[1][l][1]) + (red[2][l][1] + red[3][l][1]);
+      float* o = coef + (((long long)b * C + c) * nm + m) * 2;
+      o[0] = r;
+      o[1] = i;
+    }
+    __syncthreads();
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void fourier_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y,
+                                                            const float* __restrict__ coef, int B, int C, int H, int W,
+                                                            long long sb, long long sc, long long sy, long long sx,
+                                                            long long ob, long long oc, long long oy, long long ox,
+                                                            int t, float gain) {
+  const long long total = (long long)B * C * H * W;
+  const int n = 2 * t, nm = n * n;
+  const float ty = 6.283185307179586f / H, tx = 6.283185307179586f / W;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    // channel fastest: coalesced for channels_last, and a wave shares (b, py, px)
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int px = (int)(r % W);
+    r /= W;
+    const int py = (int)(r % H);
+    const int b = (int)(r / H);
+    const float* cf = coef + ((long long)b * C + c) * nm * 2;
+    float acc = 0.f;
+    for (int m = 0; m < nm; ++m) {
+      const int ky = m / n - t, kx = m % n - t;
+      const int ph_y = (ky * py) % H, ph_x = (kx * px) % W;
+      float sn, cs;
+      __sincosf(ty * ph_y + tx * ph_x, &sn, &cs);
+      acc += cf[2 * m] * cs - cf[2 * m + 1] * sn;
+    }
+    const float v = cvt_in<DT>(x[b * sb + c * sc + py * sy + px * sx]);
+    y[b * ob + c * oc + py * oy + px * ox] = cvt_out<DT>(v + gain * acc);
+  }
+}
+}  // namespace
+
+CGS_EXPORT int cgs_fourier_filter(const void* x, void* y, float* coef, int B, int C, int H, int W, long long sb,
+                                  long long sc, long long sy, long long sx, long long ob, long long oc, long long oy,
+                                  long long ox, int t, float scale, int dtype, hipStream_t stream) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  if (t < 1 || (2 * t) * (2 * t) > FF_MAXM || 2 * t > H || 2 * t > W || dtype == CGS_F32) return (int)hipErrorInvalidValue;
+  dim3 g1((unsigned)((C + 63) / 64), (unsigned)B);
+  const float gain = (scale - 1.0f) / ((float)H * (float)W);
+  const long long total = (long long)B * C * H * W;
+  long long nb = (total + 255) / 256;
+  const int blocks = (int)(nb > 16384 ? 16384 : nb);
+  if (dtype == CGS_BF16) {
+    fourier_coef_kernel<CGS_BF16><<<g1, 256, 0, stream>>>((const u16*)x, coef, C, H, W, sb, sc, sy, sx, t);
+    fourier_apply_kernel<CGS_BF16><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, coef, B, C, H, W, sb, sc, sy,
+                                                                sx, ob, oc, oy, ox, t, gain);
+  } else {
+    fourier_coef_kernel<CGS_F16><<<g1, 256, 0, stream>>>((const u16*)x, coef, C, H, W, sb, sc, sy, sx, t);
+    fourier_apply_kernel<CGS_F16><<<blocks, 256, 0, stream>>>((const u16*)x, (u16*)y, coef, B, C, H, W, sb, sc, sy,
+                                                               sx, ob, oc, oy, ox, t, gain);
+  }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- K30: ToMe bipartite matching
+// Reference (comfy_extras/nodes_tomesd.py:22-160): cosine similarity of every src token a_i with
+// every dst token b_j, then (max_j, argmax_j) per src token. Fused here: 1/||row|| once per token
+// (pass 1), then 64 x 64 score tiles from LDS-staged k-chunks, 4 x 4 per thread in fp32, folded into a
+// running per-row (max, argmax) -- the [Na, Nb] score matrix never exists.
+namespace {
+template <int DT>
+__global__ __launch_bounds__(256) void row_inv_norm_kernel(const u16* __restrict__ x, float* __restrict__ out,
+                                                           long long rows, int C, long long ld) {
+  const long long r = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float v = cvt_in<DT>(x[r * ld + c]);
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s > 0.f ? rsqrtf(s) : 0.f;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void tome_match_kernel(const u16* __restrict__ a, const u16* __restrict__ b,
+                                                         const float* __restrict__ ia, const float* __restrict__ ib,
+                                                         float* __restrict__ vmax, long long* __restrict__ imax,
+                                                         int Na, int Nb, int C, long long sab, long long sa,
+                                                         long long sbb, long long sbr) {
+  __shared__ float As[32][65], Bs[32][65];
+  const int bt = blockIdx.y, r0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const u16* ab = a + bt * sab;
+  const u16* bb = b + bt * sbb;
+  float best[4], inva[4];
+  int bidx[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    best[i] = -INFINITY;
+    bidx[i] = 0;
+    const int r = r0 + ty * 4 + i;
+    inva[i] = r < Na ? ia[(long long)bt * Na + r] : 0.f;
+  }
+  for (int c0 = 0; c0 < Nb; c0 += 64) {
+    float acc[4][4] = {};
+    for (int k0 = 0; k0 < C; k0 += 32) {
+      // stage 64 rows x 32 k of A and B (transposed: [k][row])
+      for (int e = tid; e < 64 * 32; e += 256) {
+        const int row = e >> 5, k = e & 31;
+        const int ra = r0 + row, rb = c0 + row, kk = k0 + k;
+        As[k][row] = (ra < Na && kk < C) ? cvt_in<DT>(ab[ra * sa + kk]) : 0.f;
+        Bs[k][row] = (rb < Nb && kk < C) ? cvt_in<DT>(bb[rb * sbr + kk]) : 0.f;
+      }
+      __syncthreads();
+#pragma unroll 8
+      for (int k = 0; k < 32; ++k) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { av[i] = As[k][ty * 4 + i]; bv[i] = Bs[k][tx * 4 + i]; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = c0 + tx * 4 + j;
+      if (col >= Nb) continue;
+      const float invb = ib[(long long)bt * Nb + col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float s = acc[i][j] * inva[i] * invb;
+        if (s > best[i]) { best[i] = s; bidx[i] = col; }
+      }
+    }
+  }
+  // (max, argmax) over the 16 column lanes of each row group (lowest index on ties)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float ov = __shfl_xor(best[i], o, 64);
+      const int oi = __shfl_xor(bidx[i], o, 64);
+      if (ov > best[i] || (ov == best[i] && oi < bidx[i])) { best[i] = ov; bidx[i] = oi; }
+    }
+    const int r = r0 + ty * 4 + i;
+    if (tx == 0 && r < Na) {
+      vmax[(long long)bt * Na + r] = best[i];
+      imax[(long long)bt * Na + r] = bidx[i];
+    }
+  }
+}
+}  // namespace
+
+// a [B, Na, C] (row stride sa, batch stride sab), b [B, Nb, C]; ws: (B*Na + B*Nb) floats.
+CGS_EXPORT int cgs_tome_match(const void* a, const void* b, float* ws, float* vmax, long long* imax, int B, int Na,
+                              int Nb, int C, long long sab, long long sa, long long sbb, long long sbr, int dtype,
+                              hipStream_t stream) {
+  if (B <= 0 || Na <= 0) return 0;
+  if (Nb <= 0 || C <= 0 || dtype == CGS_F32) return (int)hipErrorInvalidValue;
+  float* ia = ws;
+  float* ib = ws + (long long)B * Na;
+  // row norms: rows of a batch are contiguous only per batch, so one launch per operand and batch stride
+  for (int bt = 0; bt < B; ++bt) {
+    const u16* ap = (const u16*)a + bt * sab;
+    const u16* bp = (const u16*)b + bt * sbb;
+    if (dtype == CGS_BF16) {
+      row_inv_norm_kernel<CGS_BF16><<<(unsigned)((Na + 3) / 4), 256, 0, stream>>>(ap, ia + (long long)bt * Na, Na, C, sa);
+      row_inv_norm_kernel<CGS_BF16><<<(unsigned)((Nb + 3) / 4), 256, 0, stream>>>(bp, ib + (long long)bt * Nb, Nb, C, sbr);
+    } else {
+      row_inv_norm_kernel<CGS_F16><<<(unsigned)((Na + 3) / 4), 256, 0, stream>>>(ap, ia + (long long)bt * Na, Na, C, sa);
+      row_inv_norm_kernel<CGS_F16><<<(unsigned)((Nb + 3) / 4), 256, 0, stream>>>(bp, ib + (long long)bt * Nb, Nb, C, sbr);
+    }
+  }
+  dim3 g((unsigned)((Na + 63) / 64), (unsigned)B);
+  if (dtype == CGS_BF16)
+    tome_match_kernel<CGS_BF16><<<g, 256, 0, stream>>>((const u16*)a, (const u16*)b, ia, ib, vmax, imax, Na, Nb, C, sab,
+                                                        sa, sbb, sbr);
+  else
+    tome_match_kernel<CGS_F16><<<g, 256, 0, stream>>>((const u16*)a, (const u16*)b, ia, ib, vmax, imax, Na, Nb, C, sab,
+                                                       sa, sbb, sbr);
+  return (int)hipGetLastError();
+}

@@ -15,6 +15,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from .. import ops
 from ..runtime import latent_formats
 from ..runtime.patcher import set_model_options_patch_replace
 from ..sampling import model_sampling as MS
@@ -320,14 +321,9 @@ class PerturbedAttentionGuidance:
 
 # ================================================================ block patches
 def fourier_filter(x, threshold, scale):
-    """Scale the low-frequency square (|f| < threshold around DC) of each channel by ``scale``."""
-    xf = torch.fft.fftshift(torch.fft.fftn(x.float(), dim=(-2, -1)), dim=(-2, -1))
-    B, C, H, W = xf.shape
-    mask = torch.ones((B, C, H, W), device=x.device)
-    ch, cw = H // 2, W // 2
-    mask[..., ch - threshold:ch + threshold, cw - threshold:cw + threshold] = scale
-    out = torch.fft.ifftn(torch.fft.ifftshift(xf * mask, dim=(-2, -1)), dim=(-2, -1)).real
-    return out.to(x.dtype)
+    """Scale the low-frequency square (|f| < threshold around DC) of each channel by ``scale``
+    (ops.fourier_filter: HIP DFT-coefficient kernels on the device, torch.fft on the CPU)."""
+    return ops.fourier_filter(x, threshold, scale)
 
 
 def _fourier_safe(hsp, s, cpu_devs):
@@ -335,7 +331,7 @@ def _fourier_safe(hsp, s, cpu_devs):
         try:
             return fourier_filter(hsp, 1, s)
         except Exception:
-            logging.warning("torch.fft unavailable on %s for FreeU, using the CPU", hsp.device)
+            logging.warning("FreeU Fourier filter failed on %s, using the CPU", hsp.device)
             cpu_devs.add(hsp.device)
     return fourier_filter(hsp.cpu(), 1, s).to(hsp.device)
 
@@ -550,11 +546,9 @@ def bipartite_soft_matching_random2d(metric, w, h, sx, sy, r, no_rand=False):
             C = x.shape[-1]
             return (torch.gather(x, 1, a_idx.expand(B, N - num_dst, C)),
                     torch.gather(x, 1, b_idx.expand(B, num_dst, C)))
-        mn = metric / metric.norm(dim=-1, keepdim=True)
-        a, b = split(mn)
-        scores = a @ b.transpose(-1, -2)
+        a, b = split(metric)
         r = min(a.shape[1], r)
-        node_max, node_idx = scores.max(dim=-1)
+        node_max, node_idx = ops.tome_match(a, b)     # fused cosine-similarity argmax (K30)
         edge = node_max.argsort(dim=-1, descending=True)[..., None]
         unm_idx, src_idx = edge[..., r:, :], edge[..., :r, :]
         dst_idx = torch.gather(node_idx[..., None], -2, src_idx)

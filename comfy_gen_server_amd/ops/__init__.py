@@ -20,5 +20,5 @@ from .core import (  # noqa: F401
     interpolate, fused_bias_act, upfirdn2d, upfirdn2d_reference, vq_nearest, grn_nhwc, softmax_rows,
     attention_with_probs, philox_randn, euler_ancestral_philox, brownian_increment, step_param, sampler_step_dev,
     step_advance, vae_out_u8, region_accumulate, region_normalize, clip_embed, pooled_gather,
-    layernorm_stats, lnfold_weights, linear_lnfold, lnfold_available,
+    layernorm_stats, lnfold_weights, linear_lnfold, lnfold_available, fourier_filter, tome_match,
 )

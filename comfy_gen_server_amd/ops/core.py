@@ -351,6 +351,61 @@ def attention_lse(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int)
     return o.to(q.dtype), lse
 
 
+def fourier_filter(x: torch.Tensor, threshold: int, scale: float) -> torch.Tensor:
+    """FreeU's Fourier filter (K29, comfy_extras/nodes_freelunch.py:6-23): scale the 2t x 2t
+    low-frequency square of every channel's centred spectrum by ``scale``. Device: the (2t)^2 DFT
+    coefficients it touches are reduced directly and the filtered image rebuilt as x + (scale - 1) x
+    their inverse transform (exact: the filter is linear and only those modes change); CPU / fp32 /
+    t > 4: torch.fft as the reference does."""
+    B, C, H, W = x.shape
+    t = int(threshold)
+    be = backend_for("fourier", x, "cgs_fourier_filter")
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and 1 <= t <= 4 and 2 * t <= min(H, W):
+        y = torch.empty_like(x)
+        coef = torch.empty((B, C, 4 * t * t, 2), device=x.device, dtype=torch.float32)
+        count("fourier", "hip")
+        _check(_lib().cgs_fourier_filter(x.data_ptr(), y.data_ptr(), coef.data_ptr(), B, C, H, W, *x.stride(),
+                                         *y.stride(), t, float(scale), _DT[x.dtype], _stream()), "cgs_fourier_filter")
+        return y
+    if x.device.type == "cpu":
+        count("fourier", "torch")
+    else:
+        vendor_fallback("fourier", f"dtype {x.dtype}, threshold {t}, {H}x{W}")
+    xf = torch.fft.fftshift(torch.fft.fftn(x.float(), dim=(-2, -1)), dim=(-2, -1))
+    mask = torch.ones((B, C, H, W), device=x.device)
+    ch, cw = H // 2, W // 2
+    mask[..., ch - t:ch + t, cw - t:cw + t] = scale
+    out = torch.fft.ifftn(torch.fft.ifftshift(xf * mask, dim=(-2, -1)), dim=(-2, -1)).real
+    return out.to(x.dtype)
+
+
+def tome_match(a: torch.Tensor, b: torch.Tensor):
+    """ToMe bipartite matching (K30, comfy_extras/nodes_tomesd.py:22-160): for every src token a_i
+    the most cosine-similar dst token, ``(max_j cos(a_i, b_j) fp32 [B, Na], argmax int64 [B, Na])``.
+    Device: one fused HIP kernel (row norms, 64x64 fp32 score tiles folded into a running argmax);
+    CPU: normalise + matmul + max as the reference does."""
+    B, Na, C = a.shape
+    Nb = b.shape[1]
+    be = backend_for("tome", a, "cgs_tome_match")
+    if (be == "hip" and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.stride(-1) == 1
+            and b.stride(-1) == 1 and Nb > 0):
+        ws = torch.empty(B * (Na + Nb), device=a.device, dtype=torch.float32)
+        vmax = torch.empty((B, Na), device=a.device, dtype=torch.float32)
+        imax = torch.empty((B, Na), device=a.device, dtype=torch.int64)
+        count("tome", "hip")
+        _check(_lib().cgs_tome_match(a.data_ptr(), b.data_ptr(), ws.data_ptr(), vmax.data_ptr(), imax.data_ptr(), B,
+                                     Na, Nb, C, a.stride(0), a.stride(1), b.stride(0), b.stride(1), _DT[a.dtype],
+                                     _stream()), "cgs_tome_match")
+        return vmax, imax
+    if a.device.type == "cpu":
+        count("tome", "torch")
+    else:
+        vendor_fallback("tome", f"dtype {a.dtype}")
+    an = a / a.norm(dim=-1, keepdim=True)
+    bn = b / b.norm(dim=-1, keepdim=True)
+    return (an @ bn.transpose(-1, -2)).max(dim=-1)
+
+
 EPI_F32OUT = 16
 # K22: one-head D=512 attention (KL-VAE mid block) through materialised scores (CGS_WIDE_ATTN=flash
 # keeps the flash kernel). S chunks are capped at 2^28 elements (1 GiB fp32).

@@ -161,3 +161,56 @@ def test_vae_out_u8_matches_reference(cuda):
     ref = (torch.clamp((x.float() + 1.0) / 2.0, 0.0, 1.0).movedim(1, -1) * 255.0 + 0.5).to(torch.uint8)
     assert ops.stats().get(("vae_u8", "hip"), 0) == 1
     assert y.shape == (2, 37, 53, 3) and torch.equal(y, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,t,cl", [((2, 1280, 32, 32), 1, True), ((2, 640, 64, 64), 1, False),
+                                        ((1, 96, 17, 24), 2, True), ((3, 64, 8, 8), 4, False)])
+def test_fourier_filter_vs_fft(cuda, shape, t, cl):
+    """K29: FreeU's low-frequency scaling from (2t)^2 DFT coefficients == the reference's
+    fftn -> fftshift -> mask -> ifftshift -> ifftn -> real (comfy_extras/nodes_freelunch.py:6-23)."""
+    from comfy_gen_server_amd import ops
+    from comfy_gen_server_amd.ops import dispatch
+    dispatch.reset_stats()
+    torch.manual_seed(3)
+    x = (torch.randn(*shape, device=cuda) + 0.3).to(torch.bfloat16)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = ops.fourier_filter(x, t, 0.2)
+    assert dispatch.stats().get(("fourier", "hip"), 0) == 1
+    B, C, H, W = shape
+    xf = torch.fft.fftshift(torch.fft.fftn(x.float(), dim=(-2, -1)), dim=(-2, -1))
+    mask = torch.ones_like(xf.real)
+    mask[..., H // 2 - t:H // 2 + t, W // 2 - t:W // 2 + t] = 0.2
+    ref = torch.fft.ifftn(torch.fft.ifftshift(xf * mask, dim=(-2, -1)), dim=(-2, -1)).real
+    assert (y.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+def test_fourier_filter_cpu_is_reference():
+    from comfy_gen_server_amd import ops
+    x = torch.randn(2, 8, 12, 10)
+    y = ops.fourier_filter(x, 1, 0.5)
+    xf = torch.fft.fftshift(torch.fft.fftn(x, dim=(-2, -1)), dim=(-2, -1))
+    xf[..., 5:7, 4:6] *= 0.5
+    ref = torch.fft.ifftn(torch.fft.ifftshift(xf, dim=(-2, -1)), dim=(-2, -1)).real
+    assert torch.allclose(y, ref, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,Na,Nb,C", [(2, 3072, 1024, 320), (3, 100, 37, 64), (1, 65, 200, 1280)])
+def test_tome_match_vs_reference(cuda, B, Na, Nb, C):
+    """K30: fused cosine-similarity argmax == normalise + matmul + max (comfy_extras/nodes_tomesd.py)."""
+    from comfy_gen_server_amd import ops
+    from comfy_gen_server_amd.ops import dispatch
+    dispatch.reset_stats()
+    torch.manual_seed(4)
+    a = torch.randn(B, Na, C, device=cuda).to(torch.bfloat16)
+    b = torch.randn(B, Nb, C, device=cuda).to(torch.bfloat16)
+    vmax, imax = ops.tome_match(a, b)
+    assert dispatch.stats().get(("tome", "hip"), 0) == 1
+    af, bf = a.float(), b.float()
+    s = (af / af.norm(dim=-1, keepdim=True)) @ (bf / bf.norm(dim=-1, keepdim=True)).transpose(-1, -2)
+    rv, ri = s.max(dim=-1)
+    assert (vmax - rv).abs().max().item() < 1e-4
+    picked = torch.gather(s, -1, imax[..., None])[..., 0]      # the chosen dst is (one of) the best
+    assert (picked - rv).abs().max().item() < 1e-4
