@@ -269,6 +269,23 @@ def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi, conv_variant):
     assert _rel(y, ref) < 1e-2
 
 
+# The SDXL VAE decoder's largest convs at 1024^2 (the bench runs 8 images; 1 here): 128 / 256 channels at
+# full resolution, the 256-channel upsample conv (nearest 2x fused into the gather) and the 512 -> 256 one.
+@pytest.mark.parametrize("Cin,H,Cout,up", [(128, 1024, 128, False), (256, 1024, 128, False), (256, 512, 256, True),
+                                           (512, 512, 256, False)])
+def test_conv2d_vae_production_shapes(cuda, Cin, H, Cout, up):
+    torch.manual_seed(1)
+    x = torch.randn(1, Cin, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 3, 3, device=cuda) / math.sqrt(Cin * 9)).to(torch.bfloat16)
+    b = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    xr = F.interpolate(x.float(), scale_factor=2.0, mode="nearest") if up else x.float()
+    ref = F.conv2d(xr, w.float(), b.float(), 1, 1)
+    y = ops.conv2d(x, w, b, 1, 1, weight_nhwc=w.permute(0, 2, 3, 1).contiguous(), upsample2x=up)
+    assert ops.stats().get(("conv", "hip"), 0) == 1 and ops.stats().get(("conv", "lib"), 0) == 0
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,C,H,W,Cout", [(2, 320, 8, 8, 320), (1, 640, 5, 7, 640), (2, 128, 16, 16, 128)])
 def test_conv2d_fused_upsample(cuda, N, C, H, W, Cout, conv_variant):
     torch.manual_seed(0)
