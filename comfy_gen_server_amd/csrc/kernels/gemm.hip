@@ -615,6 +615,100 @@ CGS_EXPORT long long cgs_v7_ws_bytes(int M, int N, int K) {
   return ppk::split_ws_bytes(T, K / ppk::BK, num_cus());
 }
 
+// ------------------------------------------------------------------------------------------------
+// Skinny GEMM (M <= 128): CLIP text-encoder layers at one prompt (M = 77), the ResBlock time-
+// embedding projections (M = UNet batch). A 256x256 tile per workgroup leaves ~15 CUs busy there and
+// runs each call at a few TF/s; these calls are weight-bandwidth bound instead. One workgroup per 16
+// output columns (N / 16 workgroups), all M rows as MR 16-row MFMA tiles (16x16x32 bf16), the K
+// range split over the 8 waves (K-steps interleaved), fragments loaded straight from global memory
+// (16 B per lane, next K-step's loads issued before this one's MFMAs), partial accumulators summed
+// through LDS, bias / residual epilogue. Needs K % 32 == 0 and 16-B aligned rows.
+constexpr int SK_WAVES = 8;
+
+template <int MR>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(const u16* __restrict__ A, const u16* __restrict__ W,
+                                                          u16* __restrict__ C, const u16* __restrict__ bias,
+                                                          const u16* __restrict__ R, int M, int N, int K, long long lda,
+                                                          long long ldw, long long ldc, long long ldr, int epi,
+                                                          float alpha) {
+  __shared__ f32x4 red[SK_WAVES][MR][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ncol = min(n0 + fr, N - 1);
+  const u16* wp = W + (long long)ncol * ldw + 8 * fq;
+  const u16* ap[MR];
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) ap[mr] = A + (long long)min(mr * 16 + fr, M - 1) * lda + 8 * fq;
+  f32x4 acc[MR];
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) acc[mr] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nks = K / 32;
+  int ks = wave;
+  if (ks < nks) {
+    bf16x8 a[MR], b;
+    b = *reinterpret_cast<const bf16x8*>(wp + ks * 32);
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr) a[mr] = *reinterpret_cast<const bf16x8*>(ap[mr] + ks * 32);
+    for (; ks < nks; ks += SK_WAVES) {
+      const int kn = ks + SK_WAVES < nks ? ks + SK_WAVES : ks;
+      const bf16x8 bn = *reinterpret_cast<const bf16x8*>(wp + kn * 32);
+      bf16x8 an[MR];
+#pragma unroll
+      for (int mr = 0; mr < MR; ++mr) an[mr] = *reinterpret_cast<const bf16x8*>(ap[mr] + kn * 32);
+#pragma unroll
+      for (int mr = 0; mr < MR; ++mr) acc[mr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mr], b, acc[mr], 0, 0, 0);
+      b = bn;
+#pragma unroll
+      for (int mr = 0; mr < MR; ++mr) a[mr] = an[mr];
+    }
+  }
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) red[wave][mr][lane] = acc[mr];
+  __syncthreads();
+  const int col = n0 + fr;
+  float bv = 0.f;
+  if ((epi & EPI_BIAS) && col < N) bv = bf2f(bias[col]);
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) {
+    if ((mr % SK_WAVES) != wave) continue;
+    f32x4 v = red[0][mr][lane];
+#pragma unroll
+    for (int w = 1; w < SK_WAVES; ++w) v += red[w][mr][lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = mr * 16 + fq * 4 + r;
+      if (row < M && col < N) {
+        float o = v[r] * alpha + bv;
+        if (epi & EPI_RESIDUAL) o += bf2f(R[(long long)row * ldr + col]);
+        C[(long long)row * ldc + col] = f2bf(o);
+      }
+    }
+  }
+}
+
+static int gemm_skinny_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                              int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                              hipStream_t stream) {
+  const unsigned g = (unsigned)((N + 15) / 16);
+  const int mr = (M + 15) / 16;
+#define CGS_SKINNY(MRV)                                                                                          \
+  gemm_skinny_kernel<MRV><<<g, 64 * SK_WAVES, 0, stream>>>((const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias,         \
+                                                 (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha)
+  switch (mr) {
+    case 1: CGS_SKINNY(1); break;
+    case 2: CGS_SKINNY(2); break;
+    case 3: CGS_SKINNY(3); break;
+    case 4: CGS_SKINNY(4); break;
+    case 5: CGS_SKINNY(5); break;
+    case 6: CGS_SKINNY(6); break;
+    case 7: CGS_SKINNY(7); break;
+    default: CGS_SKINNY(8); break;
+  }
+#undef CGS_SKINNY
+  return (int)hipGetLastError();
+}
+
 static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 waves), 4 = v3 (8 waves), 5 = v5 ping-pong
 
 CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -633,6 +727,10 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   bool v3_ok = (K % 32 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && (nout % 8 == 0) && (ldc % 8 == 0) &&
                (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
                ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
+  // skinny M (<= 128 rows): weight-bandwidth bound, one workgroup per 16 columns (variant 8, or auto)
+  if (M <= 128 && K % 32 == 0 && !(epi & (EPI_GEGLU | EPI_F32OUT | EPI_LNFOLD)) && (variant == -1 || variant == 8) &&
+      lda % 8 == 0 && ldw % 8 == 0 && (((uintptr_t)A | (uintptr_t)W) % 16 == 0))
+    return gemm_skinny_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (epi & EPI_F32OUT) {   // fp32 output: v7 only, plain / bias epilogue
     if ((epi & (EPI_GEGLU | EPI_RESIDUAL | EPI_LNFOLD)) || !v3_ok || K % 64 || K < 128 || ((uintptr_t)bias % 8) ||
         (long long)M * lda * 2 >= (1ll << 32) || (long long)N * ldw * 2 >= (1ll << 32))

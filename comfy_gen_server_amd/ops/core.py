@@ -116,7 +116,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             return y if r is None else y.add_(r)
 
         choice = "hip"
-        if M * N * K >= (1 << 27):
+        # M <= 128 (one prompt through CLIP, time-embedding projections): the skinny kernel ("hip" ->
+        # auto), weight-bandwidth bound; the big-tile kernels are not candidates there
+        if M * N * K >= (1 << 27) and (M > 128 or K % 32):
             cands = []
             if K % 64 == 0 and N % 8 == 0:
                 if K >= 128:
