@@ -149,13 +149,16 @@ KERNEL_SIGNATURES = {
     "cgs_fourier_filter": [_P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _I, _F, _I, _P],
     # K30 ToMe matching: a, b, ws, vmax, imax(i64), B, Na, Nb, C, a strides (batch, row), b strides, dtype
     "cgs_tome_match": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _I, _P],
+    # K28 v2 GRN (vectorised, optional fused pre-GELU): x, gamma, beta, y, ws, N, HW, C, pre_gelu, dtype
+    "cgs_grn_nhwc_v2": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "cgs_grn_slices": [_I, _I, _I],
     # K22 materialised wide-head attention: fp32 S -> bf16 P row softmax (log2 units) and a bf16 transpose
     "cgs_softmax2_f32_bf16": [_P, _P, _L, _I, _L, _L, _P],             # x(f32), y(bf16), rows, cols, ldx, ldy
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
             "cgs_attn_set_variant": None}
 

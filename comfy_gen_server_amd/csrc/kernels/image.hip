@@ -232,6 +232,99 @@ __global__ void __launch_bounds__(256) grn_apply_kernel(const void* x, const flo
 }
 
 
+// K28 v2 (bf16 / fp16, C % 8 == 0): 16-B vectors, no atomics (per-row-slice partials, so no zero-fill
+// pass), and an optional fused pre-GELU (Cascade's ChannelMLP is Linear -> GELU -> GRN: the GELU is
+// recomputed in the two reads instead of being written and re-read).
+//   pass 1: block = (512 channels, row slice, n), 4 row groups x 64 channel chunks -> part[n][c][slice]
+//   pass 2: per n (1024 threads, a channel's S partials are contiguous: float4 reads),
+//           g_c = sqrt(sum over slices), nx_c = g_c / (mean_c g + 1e-6)
+//   pass 3: y = beta + a * (1 + gamma * nx), a = x or gelu(x)
+template <int DT, bool GELU>
+__global__ void __launch_bounds__(256) grn2_sumsq_kernel(const u16* __restrict__ x, float* __restrict__ part, int HW,
+                                                         int C, int rows_per, int S) {
+  __shared__ float red[4][64][8];
+  const int n = blockIdx.z, sl = blockIdx.y;
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  const int nchunk = C >> 3;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (ch < nchunk) {
+    const int r0 = sl * rows_per, r1 = min(HW, r0 + rows_per);
+    const u16* xb = x + (size_t)n * HW * C + ch * 8;
+    for (int r = r0 + rg; r < r1; r += 4) {
+      const s16x8 v = *reinterpret_cast<const s16x8*>(xb + (size_t)r * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float f = cvt_in<DT>((u16)v[j]);
+        if (GELU) f = gelu_f(f);
+        acc[j] += f * f;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][lane][j] = acc[j];
+  __syncthreads();
+  if (rg == 0 && ch < nchunk) {
+    float* o = part + ((size_t)n * C + ch * 8) * S + sl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o[(size_t)j * S] = (red[0][lane][j] + red[1][lane][j]) + (red[2][lane][j] + red[3][lane][j]);
+  }
+}
+
+__global__ void __launch_bounds__(1024) grn2_finalize_kernel(const float* __restrict__ part, float* __restrict__ nx,
+                                                             int C, int S) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  float sum = 0.f;
+  for (int c = threadIdx.x; c < C; c += 1024) {
+    const float4* p = reinterpret_cast<const float4*>(part + ((size_t)n * C + c) * S);
+    float ss = 0.f;
+    for (int q = 0; q < S / 4; ++q) {
+      const float4 v = p[q];
+      ss += (v.x + v.y) + (v.z + v.w);
+    }
+    const float g = sqrtf(ss);
+    nx[(size_t)n * C + c] = g;
+    sum += g;
+  }
+  sum = wave_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w];
+  const float inv = 1.f / (tot / (float)C + 1e-6f);
+  for (int c = threadIdx.x; c < C; c += 1024) nx[(size_t)n * C + c] *= inv;
+}
+
+template <int DT, bool GELU>
+__global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__ x, const float* __restrict__ nx,
+                                                         const u16* __restrict__ gamma, const u16* __restrict__ beta,
+                                                         u16* __restrict__ y, long long chunks, int HW, int C) {
+  const int cpr = C >> 3;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < chunks; i += (long long)gridDim.x * 256) {
+    const long long row = i / cpr;
+    const int c0 = (int)(i - row * cpr) * 8;
+    const int n = (int)(row / HW);
+    const s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
+    const s16x8 gm = *reinterpret_cast<const s16x8*>(gamma + c0);
+    const s16x8 bt = *reinterpret_cast<const s16x8*>(beta + c0);
+    const float4* np = reinterpret_cast<const float4*>(nx + (size_t)n * C + c0);
+    const float4 n0 = np[0], n1 = np[1];
+    const float nv[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+    s16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = cvt_in<DT>((u16)v[j]);
+      if (GELU) f = gelu_f(f);
+      o[j] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j]) + f * (1.f + cvt_in<DT>((u16)gm[j]) * nv[j]));
+    }
+    reinterpret_cast<s16x8*>(y)[i] = o;
+  }
+}
+
+
 // ---------------------------------------------------------------------------------------------
 // K17 / K24: weighted accumulate of a piece into a region of an fp32 [B, C, Ho, Wo] accumulator
 // pair (reference comfy/samplers.py:205-228 area/mask conds; comfy/utils.py tiled_scale feather):
@@ -722,5 +815,43 @@ CGS_EXPORT int cgs_tome_match(const void* a, const void* b, float* ws, float* vm
   else
     tome_match_kernel<CGS_F16><<<g, 256, 0, stream>>>((const u16*)a, (const u16*)b, ia, ib, vmax, imax, Na, Nb, C, sab,
                                                        sa, sbb, sbr);
+  return (int)hipGetLastError();
+}
+
+// K28 v2 launcher: ws >= N * (S + 1) * C floats with S = cgs_grn_slices(N, HW, C).
+CGS_EXPORT int cgs_grn_slices(int N, int HW, int C) {
+  // ~512 pass-1 blocks, a multiple of 4 slices (pass 2 reads each channel's partials as float4s)
+  const int cb = (C / 8 + 63) / 64;
+  int s = (512 + N * cb - 1) / (N * cb);
+  const int smax = (HW + 15) / 16;               // >= 16 rows per slice
+  if (s > smax) s = smax;
+  s = (s + 3) & ~3;
+  return s < 4 ? 4 : s;
+}
+
+CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* beta, void* y, float* ws, int N, int HW,
+                               int C, int pre_gelu, int dtype, hipStream_t stream) {
+  if (N <= 0 || HW <= 0) return 0;
+  if (C % 8 || dtype == CGS_F32 || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15))
+    return (int)hipErrorInvalidValue;
+  const int S = cgs_grn_slices(N, HW, C);
+  const int rows_per = (HW + S - 1) / S;
+  float* part = ws;
+  float* nx = ws + (size_t)N * S * C;
+  dim3 g1((unsigned)((C / 8 + 63) / 64), (unsigned)S, (unsigned)N);
+  const long long chunks = (long long)N * HW * (C / 8);
+  long long nb = (chunks + 255) / 256;
+  const int blocks = (int)(nb > 16384 ? 16384 : nb);
+#define CGS_GRN2(DTV, GV)                                                                                        \
+  grn2_sumsq_kernel<DTV, GV><<<g1, 256, 0, stream>>>((const u16*)x, part, HW, C, rows_per, S);                  \
+  grn2_finalize_kernel<<<N, 1024, 0, stream>>>(part, nx, C, S);                                                  \
+  grn2_apply_kernel<DTV, GV><<<blocks, 256, 0, stream>>>((const u16*)x, nx, (const u16*)gamma, (const u16*)beta, \
+                                                         (u16*)y, chunks, HW, C)
+  if (dtype == CGS_BF16) {
+    if (pre_gelu) { CGS_GRN2(CGS_BF16, true); } else { CGS_GRN2(CGS_BF16, false); }
+  } else {
+    if (pre_gelu) { CGS_GRN2(CGS_F16, true); } else { CGS_GRN2(CGS_F16, false); }
+  }
+#undef CGS_GRN2
   return (int)hipGetLastError();
 }

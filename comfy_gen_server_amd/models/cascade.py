@@ -92,7 +92,8 @@ class _ChannelMLP(nn.Sequential):
                          Linear(c_hidden, c_out, dtype=dtype, device=device))
 
     def forward(self, x, residual=None):
-        h = self[2](F.gelu(self[0](x)))
+        grn = self[2]
+        h = ops.grn_nhwc(self[0](x), _cast(grn.gamma, x), _cast(grn.beta, x), pre_gelu=True)
         return self[4](h, residual=residual)
 
 

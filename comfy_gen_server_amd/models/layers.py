@@ -40,8 +40,23 @@ def bump_weights_epoch():
     WEIGHTS_EPOCH += 1
 
 
-def invalidate_all(module: nn.Module):
+def stamp_epoch(module: nn.Module) -> int:
+    """Bump the global epoch and record it on every submodule of ``module``: captured graphs key on
+    ``module_epoch`` of the model they hold pointers into, so patching / moving one model (Cascade
+    Stage B) does not retire the plans of another (Stage C)."""
     bump_weights_epoch()
+    for m in module.modules():
+        m.__dict__["_cgs_epoch"] = WEIGHTS_EPOCH
+    return WEIGHTS_EPOCH
+
+
+def module_epoch(module) -> int:
+    """Weight epoch of ``module``'s tree (0 until it is first patched / moved)."""
+    return module.__dict__.get("_cgs_epoch", 0) if module is not None else 0
+
+
+def invalidate_all(module: nn.Module):
+    stamp_epoch(module)
     for m in module.modules():
         if isinstance(m, DerivedMixin):
             m.invalidate_derived()

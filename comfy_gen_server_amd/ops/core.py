@@ -1098,11 +1098,26 @@ def vq_nearest(z: torch.Tensor, codebook: torch.Tensor):
     return codebook[idx].to(z.dtype), idx
 
 
-def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor) -> torch.Tensor:
+def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, pre_gelu: bool = False) -> torch.Tensor:
     """ConvNeXt-V2 GlobalResponseNorm on NHWC [N, H, W, C] (K28, Cascade ``common.py:77-87``):
-    beta + x * (1 + gamma * ||x||_HW / mean_C ||x||_HW)."""
+    beta + a * (1 + gamma * ||a||_HW / mean_C ||a||_HW), a = x, or gelu(x) with ``pre_gelu`` (the
+    Linear -> GELU -> GRN of Cascade's ChannelMLP: the GELU is fused into both reads of x)."""
     N, H, W, C = x.shape
     be = backend_for("grn", x, "cgs_grn_nhwc")
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0 and \
+            _native.has_kernel("cgs_grn_nhwc_v2"):
+        count("grn", "hip")
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        S = int(_lib().cgs_grn_slices(N, H * W, C))
+        ws = torch.empty(N * (S + 1) * C, device=x.device, dtype=torch.float32)
+        g = gamma.to(x.dtype).reshape(-1).contiguous()
+        b = beta.to(x.dtype).reshape(-1).contiguous()
+        _check(_lib().cgs_grn_nhwc_v2(xc.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(), ws.data_ptr(), N,
+                                      H * W, C, 1 if pre_gelu else 0, _DT[x.dtype], _stream()), "cgs_grn_nhwc_v2")
+        return y
+    if pre_gelu:
+        x = F.gelu(x)
     if be == "hip" and x.dtype in _DT:
         count("grn", "hip")
         xc = x.contiguous()

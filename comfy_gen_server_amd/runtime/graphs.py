@@ -13,8 +13,9 @@ Plan lifecycle:
   * later calls: copy the inputs into the static buffers, replay, clone the output.
 A plan is only graphed when nothing dynamic can reach the forward: no ControlNet residuals, no
 ``transformer_options`` patches / replacements (their Python hooks run per step), CUDA tensors.
-Weight patching (LoRA merge / unpatch) bumps ``models.layers.WEIGHTS_EPOCH`` which retires every
-captured plan (the graph holds raw pointers to the old weight buffers).
+Weight patching (LoRA merge / unpatch) or a device move stamps a new epoch on that model's module
+tree (``models.layers.stamp_epoch``), which retires the plans captured over it (the graph holds raw
+pointers to the old weight buffers); other models' plans stay (Cascade Stage C / B alternate).
 Disable with ``CGS_GRAPHS=0``.
 """
 from __future__ import annotations
@@ -75,7 +76,7 @@ class GraphedForward:
 
     def _key(self, x, timesteps, context, y, kw):
         from ..models import layers
-        return (layers.WEIGHTS_EPOCH, _sig(x), _sig(timesteps), _sig(context), _sig(y),
+        return (layers.module_epoch(self.module), _sig(x), _sig(timesteps), _sig(context), _sig(y),
                 tuple(sorted((k, _sig(v)) for k, v in kw.items())))
 
     def _eager(self, x, timesteps, context, y, control, to, kw):
@@ -113,7 +114,7 @@ class GraphedForward:
         from ..models import layers
         with _lock:
             # plans captured under an older weight epoch hold stale pointers: drop them
-            for k in [k for k in self.plans if k[0] != layers.WEIGHTS_EPOCH]:
+            for k in [k for k in self.plans if k[0] != layers.module_epoch(self.module)]:
                 del self.plans[k]
             if len(self.plans) >= self.MAX_PLANS:
                 self.plans.pop(next(iter(self.plans)))

@@ -351,8 +351,8 @@ class ModelPatcher:
                 self.model.to(device_to)             # (anything the arena does not hold)
             else:
                 self.model.to(device_to)
-            from ..models.layers import bump_weights_epoch
-            bump_weights_epoch()
+            from ..models.layers import stamp_epoch
+            stamp_epoch(self.model)
         if patch_weights and (force or getattr(self.model, "current_patches_uuid", None) != self.patches_uuid):
             # restore weights that have a backup but are no longer patched
             for k in list(self.backup.keys()):

@@ -141,16 +141,17 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
         xin = torch.empty((x.shape[0] * batched,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
         hints = [cn.prepare_hint(xin, batched) for cn in chain]
     from ..models import layers
-    key = (layers.WEIGHTS_EPOCH, tuple(x.shape), use_uncond, float(guider.cfg),
+    epoch = layers.module_epoch(model)
+    key = (epoch, tuple(x.shape), use_uncond, float(guider.cfg),
            tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in cond.items())),
-           tuple((id(cn.control_model), float(cn.strength), bool(cn.global_average_pooling), tuple(h.shape), h.dtype)
-                 for cn, h in zip(chain, hints)))
+           tuple((id(cn.control_model), layers.module_epoch(cn.control_model), float(cn.strength),
+                  bool(cn.global_average_pooling), tuple(h.shape), h.dtype) for cn, h in zip(chain, hints)))
     plans = model.__dict__.setdefault("_step_graph_plans", {})
     plan = plans.get(key)
     if plan is None:
         plan = _new_plan(x, cond, hints)
         with _lock:
-            for k in [k for k in plans if k[0] != layers.WEIGHTS_EPOCH]:
+            for k in [k for k in plans if k[0] != epoch]:
                 del plans[k]
             plans[key] = plan
     for pat in sorted(set(patterns)):

@@ -115,6 +115,23 @@ def test_vq_nearest_gpu(cuda, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 24, 24, 8192), (4, 64, 64, 1536), (1, 5, 7, 64)])
+@pytest.mark.parametrize("pre_gelu", [False, True])
+def test_grn_v2_gpu(cuda, shape, pre_gelu):
+    """K28 v2: vectorised GRN (per-slice partials, no atomics) with the optional fused pre-GELU of
+    Cascade's Linear -> GELU -> GRN, vs fp32 torch."""
+    N, H, W, C = shape
+    x, g, b = torch.randn(*shape), torch.randn(C) * 0.5, torch.randn(C) * 0.1
+    ops.reset_stats()
+    y = ops.grn_nhwc(x.to(cuda, torch.bfloat16), g.to(cuda, torch.bfloat16), b.to(cuda, torch.bfloat16),
+                     pre_gelu=pre_gelu).float().cpu()
+    assert ops.stats().get(("grn", "hip"), 0) == 1
+    xr = x.to(torch.bfloat16).float()
+    ref = _ref_grn(F.gelu(xr) if pre_gelu else xr, g.to(torch.bfloat16), b.to(torch.bfloat16))
+    assert ((y - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_grn_gpu(cuda, dtype):
     x, g, b = torch.randn(2, 24, 24, 2048), torch.randn(2048) * 0.5, torch.randn(2048) * 0.1
