@@ -392,6 +392,39 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
   mc::tile<BN, NW>(al, W, ldw, M, N, K, tm * mc::BM, tn * BN, e, smem);
 }
 
+// v8: the same main loop on 128 x 128 tiles (4 waves of 64 x 64), two workgroups per CU, for the
+// short-M / short-N shapes whose 256-row grids leave most CUs idle. K % 32 == 0, 16-B aligned rows.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v8_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
+  DenseA al{A, lda, M, {}};
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
+  mc::tile<128, 4, DenseA, 128>(al, W, ldw, M, N, K, tm * 128, tn * 128, e, smem);
+}
+
+static int gemm_v8_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream) {
+  using Cf = mc::Cfg<128, 4, 128>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + 127) / 128;
+  const long long nwg = (long long)((M + 127) / 128) * tiles_n;
+  if (nwg > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  gemm_bf16_nt_v8_kernel<<<(unsigned)nwg, 256, Cf::LDS, stream>>>((const u16*)A, (const u16*)W, (u16*)C,
+                                                                   (const u16*)bias, (const u16*)R, M, N, K, lda, ldw,
+                                                                   ldc, ldr, epi, alpha, tiles_n, g_tile_group);
+  return (int)hipGetLastError();
+}
+
 template <int BN, int NW>
 static void gemm_v3_go(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                        long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
@@ -727,8 +760,8 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   bool v3_ok = (K % 32 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && (nout % 8 == 0) && (ldc % 8 == 0) &&
                (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
                ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
-  // skinny M (<= 128 rows): weight-bandwidth bound, one workgroup per 16 columns (variant 8, or auto)
-  if (M <= 128 && K % 32 == 0 && !(epi & (EPI_GEGLU | EPI_F32OUT | EPI_LNFOLD)) && (variant == -1 || variant == 8) &&
+  // skinny M (<= 128 rows): weight-bandwidth bound, one workgroup per 16 columns (variant 9, or auto)
+  if (M <= 128 && K % 32 == 0 && !(epi & (EPI_GEGLU | EPI_F32OUT | EPI_LNFOLD)) && (variant == -1 || variant == 9) &&
       lda % 8 == 0 && ldw % 8 == 0 && (((uintptr_t)A | (uintptr_t)W) % 16 == 0))
     return gemm_skinny_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (epi & EPI_F32OUT) {   // fp32 output: v7 only, plain / bias epilogue
@@ -742,6 +775,7 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&
       ((uintptr_t)bias % 8 == 0) && (long long)M * lda * 2 < (1ll << 32) && (long long)N * ldw * 2 < (1ll << 32))
     return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
+  if (v3_ok && variant == 8) return gemm_v8_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && variant == 5)
     return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && (variant >= 3 || variant == -1)) {

@@ -42,23 +42,29 @@ constexpr int BM = 256;
 constexpr int BK = 32;
 constexpr int STAGES = 4;
 
-// NW = waves per block: 4 (2x2 grid, one wave per SIMD, 128 x BN/2 per wave) or 8 (2x4 grid, two
-// waves per SIMD, 128 x BN/4 per wave: the partner wave hides LDS latency, barriers and VMEM issue).
-template <int BN, int NW = 4>
+// NW = waves per block: 4 (2x2 grid, one wave per SIMD, BMV/2 x BN/2 per wave) or 8 (2x4 grid, two
+// waves per SIMD, BMV/2 x BN/4 per wave: the partner wave hides LDS latency, barriers and VMEM issue).
+// BMV = tile rows: 256, or 128 for the small-M "v8" form (128 x 128 tiles, 64 KiB of LDS -> two
+// workgroups per CU: 4x the tiles of a 256 x 256 grid where M or N is short -- SDXL at batch 1,
+// Cascade's 24^2 / 32^2 token grids -- and one workgroup's epilogue overlaps the other's main loop).
+template <int BN, int NW = 4, int BMV = BM>
 struct Cfg {
   static constexpr int THREADS = 64 * NW;
   static constexpr int WCOLS = NW / 2;                  // wave grid is 2 x WCOLS
-  static constexpr int A_BYTES = BM * BK * 2;           // 16 KiB
+  static constexpr int TM = BMV;                        // tile rows
+  static constexpr int WROWS = BMV / 2;                 // wave tile rows
+  static constexpr int A_BYTES = BMV * BK * 2;          // 16 KiB at 256 rows
   static constexpr int B_BYTES = BN * BK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int LDS = STAGES * STAGE;
-  static constexpr int A_PIECES = BM / 16 / NW;         // LDS-DMA pieces (16 rows) per wave
+  static constexpr int A_PIECES = BMV / 16 / NW;        // LDS-DMA pieces (16 rows) per wave
   static constexpr int B_PIECES = BN / 16 / NW;
   static constexpr int PER_STAGE = A_PIECES + B_PIECES; // LDS-DMA instructions per wave per stage
   static constexpr int WN = BN / WCOLS;                 // wave tile cols
-  static constexpr int NI = 4;                          // 32-row MFMA tiles per wave
+  static constexpr int NI = WROWS / 32;                 // 32-row MFMA tiles per wave
   static constexpr int NJ = WN / 32;                    // 32-col MFMA tiles per wave
-  static_assert(B_PIECES >= 1 && NJ >= 1, "tile too narrow for this wave count");
+  static_assert(A_PIECES >= 1 && B_PIECES >= 1 && NJ >= 1 && NI >= 1, "tile too narrow for this wave count");
+  static_assert(NW * WROWS * WN * 2 <= LDS, "epilogue regions must fit the stage ring");
 };
 
 struct Epi {
@@ -90,14 +96,14 @@ __device__ __forceinline__ int src_chunk(int lane) { return (lane & 3) ^ ((lane 
 // Main loop + epilogue for one 256 x BN output tile.
 //   AL: loader with  __device__ void setup(int p, int row)  (p = this wave's A piece 0..3, row =
 //       global output row, may be >= M) and  __device__ const void* src(int p, int k0) const.
-template <int BN, int NW, class AL>
+template <int BN, int NW, class AL, int BMV = BM>
 __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K, int m0,
                                      int n0, const Epi& e, unsigned char* smem) {
-  using C = Cfg<BN, NW>;
+  using C = Cfg<BN, NW, BMV>;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wave / C::WCOLS) * 128;
+  const int wm = (wave / C::WCOLS) * C::WROWS;
   const int wn = (wave % C::WCOLS) * C::WN;
   const int prow = piece_row(lane);
   const int sch = src_chunk(lane);
@@ -196,7 +202,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
 
   // ---- epilogue, staged through LDS so global traffic is 16-B vectors.
   // 32x32 C layout: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
-  // Each wave owns a 128 x OW bf16 region (OW = WN, or WN/2 for GEGLU); 16-B chunk ch of row r is
+  // Each wave owns a WROWS x OW bf16 region (OW = WN, or WN/2 for GEGLU); 16-B chunk ch of row r is
   // stored at ch ^ (r & (CPR - 1)) so the column-wise fragment writes and row-wise reads are
   // conflict-free without padding (the 4 regions fill exactly the 4-stage ring).
   wait_vmcnt<0>();   // the clamped tail DMAs target slots the epilogue reuses
@@ -205,7 +211,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   const int OW = geglu ? C::WN / 2 : C::WN;
   const int CPR = OW / 8;               // 16-B chunks per row
   const int pitch = OW * 2;
-  unsigned char* region = smem + wave * (128 * C::WN * 2);
+  unsigned char* region = smem + wave * (C::WROWS * C::WN * 2);
   const int ecol = lane & 31;
   const int erow = 4 * fhalf;
   if (geglu) {
@@ -258,7 +264,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   const int gcol0 = geglu ? (n0 + wn) / 2 : n0 + wn;
   const int Nout = geglu ? N / 2 : N;
   const int ch = lane % CPR;
-  for (int rr = lane / CPR; rr < 128; rr += rows_per_it) {
+  for (int rr = lane / CPR; rr < C::WROWS; rr += rows_per_it) {
     const int grow = m0 + wm + rr;
     const int gcol = gcol0 + 8 * ch;
     s16x8 v = *reinterpret_cast<const s16x8*>(region + rr * pitch + 16 * (ch ^ (rr & (CPR - 1))));

@@ -127,6 +127,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
                 cands.append(("v6", lambda: run_hip(6)))
             if K % 32 == 0 and N % 8 == 0:
                 cands.append(("v4", lambda: run_hip(4)))
+                cands.append(("v8", lambda: run_hip(8)))      # 128 x 128 tiles (short M / N grids)
             cands.append(("hip", lambda: run_hip(-1)))
             if _LIB_GEMM:     # vendor GEMM only as an explicit opt-in (CGS_GEMM_LIB=1)
                 cands.append(("lib", run_lib))
@@ -135,7 +136,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")     # explicit opt-in (CGS_GEMM_LIB=1)
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4}.get(choice, -2)
+        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N)
     if be == "torch":
         count("gemm", "torch")

@@ -170,7 +170,7 @@ def test_attention_d64_variants(cuda, attn_variant, B, H, Sq, Sk, spike):
     assert _rel(o, ref) < 2e-2
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160", "v7ppk"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8], ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160", "v7ppk", "v8t128"])
 def gemm_variant(request):
     lib = _native.load_kernels()
     lib.cgs_gemm_set_variant(request.param)
