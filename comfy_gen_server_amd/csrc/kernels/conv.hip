@@ -258,6 +258,34 @@ static void conv_v3_go(ConvArgs& a, hipStream_t stream) {
   conv_nhwc_v3_kernel<BN, NW><<<(unsigned)nwg, 64 * NW, mc::Cfg<BN, NW>::LDS, stream>>>(a);
 }
 
+// v8: the v3 main loop on 128 x 128 tiles (two workgroups per CU) for short grids -- the level-2
+// convs at UNet batch 2 (M = 2048) and Cascade's small token grids. Cin % 32 == 0 (v3 gather).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v8_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
+  ConvGatherA al;
+  al.a = &a;
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  mc::tile<128, 4, ConvGatherA, 128>(al, a.w, K, M, a.Cout, K, tm * 128, tn * 128, e, smem);
+}
+
+static void conv_v8_go(ConvArgs& a, hipStream_t stream) {
+  using Cf = mc::Cfg<128, 4, 128>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = (a.Cout + 127) / 128;
+  const long long nwg = (long long)((M + 127) / 128) * a.tiles_n;
+  conv_nhwc_v8_kernel<<<(unsigned)nwg, 256, Cf::LDS, stream>>>(a);
+}
+
 // v5: ping-pong schedule (mfma_pp.h), 256 x 256 x 64 tiles; Cin % 64 == 0 (one tap per K-tile).
 struct ConvGatherA8 {
   const ConvArgs* a;
@@ -560,6 +588,10 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream, void* ws
   if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
       ((uintptr_t)a.bias % 8) == 0) {
     conv_v6_go(a, stream);
+    return (int)hipGetLastError();
+  }
+  if (variant == 8) {
+    conv_v8_go(a, stream);
     return (int)hipGetLastError();
   }
   const int M = a.N * a.Ho * a.Wo;

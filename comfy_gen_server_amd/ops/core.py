@@ -629,12 +629,14 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         M = N * Ho * Wo
         if M * Cout * Cin * kh * kw >= (1 << 27):
             cands = [("v4", lambda: run(4))]
+            if Cout % 8 == 0:
+                cands.append(("v8", lambda: run(8)))      # 128 x 128 tiles (short grids)
             if Cin % 64 == 0:
                 cands += [("v7", lambda: run(7)), ("v5", lambda: run(5)), ("v6", lambda: run(6)),
                           ("v2", lambda: run(2))]
             choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None))
                                      + ((("dual", C1),) if x2c is not None else ()), cands, default="auto")
-            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7, "auto": -2}[choice]
+            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7, "v8": 8, "auto": -2}[choice]
         return run(variant)
     if upsample2x:
         x = upsample_nearest2x(x)

@@ -237,7 +237,7 @@ def test_elementwise(cuda):
     assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
 
 
-@pytest.fixture(params=[2, 3, 4, 5, 6, 7], ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160", "cv7ppk"])
+@pytest.fixture(params=[2, 3, 4, 5, 6, 7, 8], ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160", "cv7ppk", "cv8t128"])
 def conv_variant(request):
     lib = _native.load_kernels()
     lib.cgs_conv_set_variant(request.param)
