@@ -80,6 +80,9 @@ KERNEL_SIGNATURES = {
                            _L, _L, _L,                  # v strides
                            _L, _L, _L,                  # o strides
                            _F, _P, _I, _P],             # scale, key_mask(int8 [B,Sk] or null), causal, stream
+    # per-call kernel variant (op-layer autotune): ..., scale, variant, stream
+    "cgs_flash_attn_fwd_v": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _F,
+                             _I, _P],
     # same + fp32 LSE [B, H, Sq] out (ring attention merge): q,k,v,o,lse, B,H,Sq,Sk,D, 12 strides, scale
     "cgs_flash_attn_fwd_lse": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L,
                                _F, _P],

@@ -1052,6 +1052,20 @@ static int flash_attn_impl(const void* q, const void* k, const void* v, void* o,
   return (int)hipGetLastError();
 }
 
+// Per-call kernel choice for the op-layer autotuner (variant as in cgs_attn_set_variant; the process
+// setting is restored before returning).
+CGS_EXPORT int cgs_flash_attn_fwd_v(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
+                                    int D, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
+                                    long long ksh, long long vsb, long long vss, long long vsh, long long osb,
+                                    long long oss, long long osh, float scale, int variant, hipStream_t stream) {
+  const int saved = g_attn_variant;
+  g_attn_variant = variant;
+  const int rc = flash_attn_impl(q, k, v, o, B, H, Sq, Sk, D, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, oss, osh,
+                                 scale, nullptr, 0, nullptr, stream);
+  g_attn_variant = saved;
+  return rc;
+}
+
 CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
                                   int D, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
                                   long long ksh, long long vsb, long long vss, long long vsh, long long osb,

@@ -302,6 +302,21 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
             count("attention", "hip")
             return _attention_wide_mat(q, k, v)
         choice = "hip"
+        # D = 64 self-attention whose 256-query blocks leave CUs idle (batch 1-2 at level 2: B*H*Sq/256
+        # < 256 workgroups): the generic kernel's 128-query blocks are a measured alternative
+        if (kp is None and not causal and D == 64 and Sk > 128 and B * heads * ((Sq + 255) // 256) < 256
+                and B * heads * Sq * Sk >= (1 << 22) and _native.has_kernel("cgs_flash_attn_fwd_v")):
+            def run_v(var):
+                o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
+                _check(_lib().cgs_flash_attn_fwd_v(
+                    q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, heads, Sq, Sk, D,
+                    q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
+                    o.stride(0), o.stride(1), D, 1.0 / math.sqrt(D), var, _stream()), "cgs_flash_attn_fwd_v")
+                return o
+            sel = autotune.choose(("attention_grid", B, heads, Sq, Sk, D),
+                                  [("d64", lambda: run_v(0)), ("generic", lambda: run_v(1))], default="d64")
+            count("attention", "hip")
+            return run_v(0 if sel == "d64" else 1)
         # The vendor SDPA is a tuning candidate only on explicit request: the hot path is the
         # hand-written kernel (K02/K03), never an SDPA fallback.
         if kp is None and _ATTN_ALLOW_LIB and B * heads * Sq * Sk >= (1 << 22):
