@@ -155,6 +155,8 @@ KERNEL_SIGNATURES = {
     # K28 v2 GRN (vectorised, optional fused pre-GELU): x, gamma, beta, y, ws, N, HW, C, pre_gelu, dtype
     "cgs_grn_nhwc_v2": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "cgs_grn_slices": [_I, _I, _I],
+    # K05 batched fp32-MFMA GEMM: A, B, C, batch, M, N, K, A strides (b, m, k), B strides (b, k, n), C (b, m), alpha, dta, dtb
+    "cgs_bgemm_f32": [_P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _F, _I, _I, _P],
     # K22 materialised wide-head attention: fp32 S -> bf16 P row softmax (log2 units) and a bf16 transpose
     "cgs_softmax2_f32_bf16": [_P, _P, _L, _I, _L, _L, _P],             # x(f32), y(bf16), rows, cols, ldx, ldy
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy

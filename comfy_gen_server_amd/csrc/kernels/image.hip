@@ -855,3 +855,76 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
 #undef CGS_GRN2
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- K05: probability-output attention
+// SAG / PAG read the attention map itself (comfy_extras/nodes_sag.py, reference fp32 bmm + softmax),
+// so it is materialised: S = scale * Q K^T and O = P V as batched fp32 GEMMs on the f32-input MFMA
+// (v_mfma_f32_16x16x4_f32: exact fp32 products, the reference's precision), P by the row softmax
+// (K05 softmax_rows). C[b] = alpha * A[b] . B[b] with A(m, k) = A + b*sab + m*sam + k*sak and
+// B(k, n) = B + b*sbb + k*sbk + n*sbn (any strides: B = K^T for the scores, B = V for PV);
+// 64 x 64 tiles, 4 waves of 32 x 32, k-chunks of 16 staged through LDS as fp32.
+namespace {
+template <int DTA, int DTB>
+__global__ __launch_bounds__(256) void bgemm_f32_kernel(const void* __restrict__ A, const void* __restrict__ Bm,
+                                                        float* __restrict__ C, int M, int N, int K, long long sab,
+                                                        long long sam, long long sak, long long sbb, long long sbk,
+                                                        long long sbn, long long scb, long long scm, float alpha) {
+  __shared__ float As[64][17], Bs[64][17];   // As[m][k], Bs[n][k]
+  const int bt = blockIdx.z, m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int e = tid; e < 64 * 16; e += 256) {
+      const int r = e >> 4, kk = e & 15, k = k0 + kk;
+      const int m = m0 + r, n = n0 + r;
+      As[r][kk] = (m < M && k < K) ? ldv<DTA>(A, bt * sab + m * sam + k * sak) : 0.f;
+      Bs[r][kk] = (n < N && k < K) ? ldv<DTB>(Bm, bt * sbb + k * sbk + n * sbn) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kk = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float a = As[wm + 16 * i + (lane & 15)][kk];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[wn + 16 * j + (lane & 15)][kk], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + 16 * i + (lane >> 4) * 4 + r, n = n0 + wn + 16 * j + (lane & 15);
+        if (m < M && n < N) C[bt * scb + (long long)m * scm + n] = acc[i][j][r] * alpha;
+      }
+}
+}  // namespace
+
+// dta / dtb: CgsDType of A / B (fp32, bf16 or fp16); C fp32 with row stride scm.
+CGS_EXPORT int cgs_bgemm_f32(const void* A, const void* B, float* C, int batch, int M, int N, int K, long long sab,
+                             long long sam, long long sak, long long sbb, long long sbk, long long sbn, long long scb,
+                             long long scm, float alpha, int dta, int dtb, hipStream_t stream) {
+  if (batch <= 0 || M <= 0 || N <= 0) return 0;
+  if (K <= 0 || batch > 65535 || (M + 63) / 64 > 65535) return (int)hipErrorInvalidValue;
+  dim3 g((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)batch);
+#define CGS_BG(TA, TB) bgemm_f32_kernel<TA, TB><<<g, 256, 0, stream>>>(A, B, C, M, N, K, sab, sam, sak, sbb, sbk, sbn, scb, scm, alpha)
+  if (dta == CGS_BF16 && dtb == CGS_BF16) CGS_BG(CGS_BF16, CGS_BF16);
+  else if (dta == CGS_F32 && dtb == CGS_BF16) CGS_BG(CGS_F32, CGS_BF16);
+  else if (dta == CGS_F16 && dtb == CGS_F16) CGS_BG(CGS_F16, CGS_F16);
+  else if (dta == CGS_F32 && dtb == CGS_F16) CGS_BG(CGS_F32, CGS_F16);
+  else if (dta == CGS_F32 && dtb == CGS_F32) CGS_BG(CGS_F32, CGS_F32);
+  else return (int)hipErrorInvalidValue;
+#undef CGS_BG
+  return (int)hipGetLastError();
+}

@@ -1166,10 +1166,34 @@ def softmax_rows(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
 
 
 def attention_with_probs(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int):
-    """Attention that also returns the probabilities [(b*heads), Sq, Sk] in fp32 (K05). Scores and
-    the PV product are fp32 batched GEMMs (hipBLASLt); the softmax writing P is the HIP kernel."""
+    """Attention that also returns the probabilities [(b*heads), Sq, Sk] in fp32 (K05: SAG / PAG read
+    the map). Device: scores and PV as batched fp32-MFMA GEMMs straight from the strided per-head
+    views (``cgs_bgemm_f32``: exact fp32 products, the reference's fp32 bmm precision), the softmax
+    writing P in place (``cgs_softmax_rows``); CPU: fp32 torch."""
     b, sq, hd = q.shape
     d = hd // heads
+    sk = k.shape[1]
+    if (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16) and k.dtype == q.dtype and v.dtype == q.dtype
+            and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1
+            and backend_for("attention", q, "cgs_bgemm_f32") == "hip"
+            and backend_for("softmax", q, "cgs_softmax_rows") == "hip"):
+        lib, st, dt = _lib(), _stream(), _DT[q.dtype]
+        bh = b * heads
+        p = torch.empty((bh, sq, sk), device=q.device, dtype=torch.float32)
+        # batch index = b * heads + h: per-head base = b*stride(0) + h*d  (sab covers h via the loop)
+        for bi in range(b):
+            _check(lib.cgs_bgemm_f32(q[bi].data_ptr(), k[bi].data_ptr(), p[bi * heads].data_ptr(), heads, sq, sk, d,
+                                     d, q.stride(1), 1, d, 1, k.stride(1), sq * sk, sk, 1.0, dt, dt, st),
+                   "cgs_bgemm_f32")
+        count("softmax", "hip")
+        _check(lib.cgs_softmax_rows(p.data_ptr(), p.data_ptr(), bh * sq, sk, float(d ** -0.5), 0, st),
+               "cgs_softmax_rows")
+        o = torch.empty((b, sq, hd), device=q.device, dtype=torch.float32)
+        for bi in range(b):
+            _check(lib.cgs_bgemm_f32(p[bi * heads].data_ptr(), v[bi].data_ptr(), o[bi].data_ptr(), heads, sq, d, sk,
+                                     sq * sk, sk, 1, d, v.stride(1), 1, d, hd, 1.0, 0, dt, st), "cgs_bgemm_f32")
+        count("attention", "hip")
+        return o.to(q.dtype), p
     qh = q.reshape(b, sq, heads, d).permute(0, 2, 1, 3).reshape(b * heads, sq, d).float()
     kh = k.reshape(b, -1, heads, d).permute(0, 2, 1, 3).reshape(b * heads, -1, d).float()
     vh = v.reshape(b, -1, heads, d).permute(0, 2, 1, 3).reshape(b * heads, -1, d).float()

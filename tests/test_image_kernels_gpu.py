@@ -161,6 +161,30 @@ def test_softmax_rows_and_attention_probs_gpu(cuda, dtype):
     assert torch.allclose(o.cpu(), attention_reference(q, k, v, 4), atol=1e-4)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,heads,sq,sk,d", [(2, 5, 300, 77, 64), (1, 10, 1024, 1024, 64), (3, 2, 65, 130, 40)])
+def test_attention_probs_bf16_mfma_gpu(cuda, b, heads, sq, sk, d):
+    """K05 device path: fp32-MFMA batched GEMMs over the strided per-head views (q from a fused QKV)
+    + in-place HIP softmax, vs the fp32 reference of the same bf16 inputs."""
+    torch.manual_seed(6)
+    qkv = torch.randn(b, sq, 3 * heads * d).to(torch.bfloat16)
+    hd = heads * d
+    q = qkv[..., :hd]
+    k = torch.randn(b, sk, hd).to(torch.bfloat16)
+    v = torch.randn(b, sk, hd).to(torch.bfloat16)
+    ops.reset_stats()
+    o, p = ops.attention_with_probs(q.to(cuda), k.to(cuda), v.to(cuda), heads)
+    st = ops.stats()
+    assert st.get(("attention", "hip"), 0) == 1 and st.get(("softmax", "hip"), 0) == 1, st
+    qh = q.float().reshape(b, sq, heads, d).transpose(1, 2).reshape(b * heads, sq, d)
+    kh = k.float().reshape(b, sk, heads, d).transpose(1, 2).reshape(b * heads, sk, d)
+    pref = torch.softmax(qh @ kh.transpose(1, 2) * d ** -0.5, -1)
+    assert (p.cpu() - pref).abs().max().item() < 1e-4
+    from comfy_gen_server_amd.ops.core import attention_reference
+    oref = attention_reference(q.float(), k.float(), v.float(), heads)
+    assert ((o.float().cpu() - oref).norm() / oref.norm()).item() < 1e-2
+
+
 def test_attention_probs_cpu():
     q, k, v = (torch.randn(1, 16, 2 * 8) for _ in range(3))
     o, p = ops.attention_with_probs(q, k, v, 2)
