@@ -22,9 +22,9 @@ tests() { step 900 pytest python -u -m pytest tests/ -m gpu -x -q --timeout 300 
 smoke() { step 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"; }
 bench() { step 600 bench python -u bench.py ${BENCH_ARGS:---profile-ops}; }
 prof() {
-  step 600 prof rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag} -o run -- \
+  step 600 prof rocprofv3 --kernel-trace --stats -d /tmp/prof_${tag} -o run -- \
       python3 bench.py --steps ${PROF_STEPS:-2} --warmup 1 ${BENCH_ARGS:-} || return $?
-  db=$(find gpurun_out/prof_${tag} -name "*results.db" | head -n1)
+  db=$(find /tmp/prof_${tag} -name "*results.db" | head -n1)
   [ -n "$db" ] && python -m comfy_gen_server_amd.tools.rocprof_summary "$db" "gpurun_out/${tag}_prof.md" --top 60 ${PROF_TAIL:+--tail-s $PROF_TAIL}
   return 0
 }
