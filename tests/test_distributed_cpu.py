@@ -315,7 +315,8 @@ if lp.Q > 1:
         assert st[mode] > 0, st
 d = (got - ref).abs().max().item()
 print("layout", lay, "G", lp.G, "Q", lp.Q, "maxdiff", d, "sp", None if lp.sp is None else lp.sp.stats, flush=True)
-assert d < 1e-4, d
+# the batch split changes CPU BLAS blocking (reduction order): fp32 round-off, scaled to the latent
+assert d < 2e-5 * max(1.0, ref.abs().max().item()) + 2e-4, d
 c.shutdown()
 '''
 
