@@ -602,8 +602,120 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream, void* ws
   return (int)hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Narrow-output conv (Cout <= 16): the UNet's conv_out (320 -> 4 latent channels, once per
+// denoiser step) and the VAE decoder's conv_out (128 -> 3 at full image resolution). A 128/256-wide
+// N tile wastes > 95 % of its MFMA columns and LDS traffic on these (they ran at ~1.7 ms per UNet
+// step and ~10 ms per decode on v2). Here one wave owns SN_MB x 16 output pixels x 16 output
+// channels: per 32-channel K step it issues SN_MB v_mfma_f32_16x16x32_bf16 whose A fragments are
+// 16-B NHWC vectors loaded straight from global (lane l: pixel row l & 15, channels 8 (l >> 4) ..
+// +7 -- the MFMA's own A layout, so no LDS) and whose B fragment is the same slice of the filter
+// row of output channel l & 15 (the whole filter is a few 10s of KB and stays in L1/L2). No LDS,
+// no barriers, 4 waves per workgroup and >= 1000 workgroups on the production shapes.
+// Pixel mapping: a workgroup (4 waves) owns a 16 x 16 output patch of one image; wave w covers
+// rows 4w .. 4w+3, one 16-pixel MFMA block per row (lane & 15 = x). The K loop runs channel-chunk
+// outer, tap inner, so while a workgroup is on one 32-channel chunk it touches only its 18 x 18 x
+// 64-B input halo (~21 KB): the nine taps' re-reads are L1 hits and HBM/L2 see ~one pass.
+#define SN_MB 4
+template <int KS>   // KS = kh = kw when 1 or 3 (taps unrolled), 0 = runtime kh / kw
+__global__ __launch_bounds__(256) void conv_nhwc_smalln_kernel(ConvArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tiles_x = (a.Wo + 15) >> 4, tiles_y = (a.Ho + 15) >> 4;
+  const int bid = blockIdx.x;
+  const int n = bid / (tiles_x * tiles_y);
+  const int trem = bid - n * tiles_x * tiles_y;
+  const int ty = trem / tiles_x, tx = trem - ty * tiles_x;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int kh = KS ? KS : a.kh, kw = KS ? KS : a.kw;
+  const bool up = (a.flags & CONV_UP2X) != 0;
+  const int Hin = up ? 2 * a.H : a.H, Win = up ? 2 * a.W : a.W;
+  const int ox = tx * 16 + fr;
+  const int px = ox * a.stride - a.pad;
+  int py[SN_MB];
+  bool pv[SN_MB];
+#pragma unroll
+  for (int b = 0; b < SN_MB; ++b) {
+    const int oy = ty * 16 + wave * SN_MB + b;
+    pv[b] = oy < a.Ho && ox < a.Wo;
+    py[b] = oy * a.stride - a.pad;
+  }
+  const bool cv = fr < a.Cout;
+  const int C2 = a.Cin - a.C1;
+  const u16* wrow = a.w + (long long)(cv ? fr : 0) * kh * kw * a.Cin + 8 * fq;
+  f32x4 acc[SN_MB];
+#pragma unroll
+  for (int b = 0; b < SN_MB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long long img = (long long)n * a.H;
+  for (int c = 0; c < a.Cin; c += 32) {
+    const bool second = c >= a.C1;
+    const u16* src = second ? a.in2 : a.in;
+    const int cs = second ? C2 : a.C1;
+    const int cb = (second ? c - a.C1 : c) + 8 * fq;
+    // (measured: hoisting all nine taps' loads ahead of the MFMAs -- 45 in flight, 256 VGPRs, one wave
+    // per SIMD -- was slower on the VAE shape, 287 -> 336 us; the per-tap loop below keeps two waves)
+    {
+#pragma unroll
+      for (int ky = 0; ky < kh; ++ky) {
+#pragma unroll
+        for (int kx = 0; kx < kw; ++kx) {
+          // loads are unconditional (padding taps / unused columns read the zero page): a predicated
+          // load compiles to a branch per lane group and serialises every tap behind vmcnt(0)
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(cv ? (const void*)(wrow + (ky * kw + kx) * a.Cin + c)
+                                                                   : (const void*)(g_conv_zero_page + 16 * fq));
+          int ix = px + kx;
+          const bool okx = ix >= 0 && ix < Win;
+          if (up) ix >>= 1;
+          bf16x8 af[SN_MB];
+#pragma unroll
+          for (int b = 0; b < SN_MB; ++b) {
+            int iy = py[b] + ky;
+            const bool ok = pv[b] && okx && iy >= 0 && iy < Hin;
+            if (up) iy >>= 1;
+            af[b] = *reinterpret_cast<const bf16x8*>(ok ? (const void*)(src + ((img + iy) * a.W + ix) * cs + cb)
+                                                        : (const void*)(g_conv_zero_page + 16 * fq));
+          }
+#pragma unroll
+          for (int b = 0; b < SN_MB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[b], bfr, acc[b], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // C/D layout: acc[b][r] = (pixel row 4 (lane >> 4) + r of block b, output channel lane & 15). Block b is
+  // image row oy_b; its 16 MFMA rows are the 16 x positions tx*16 .. +15.
+  if (!cv) return;
+  const float bv = (a.flags & EPI_BIAS) ? bf2f(a.bias[fr]) : 0.f;
+#pragma unroll
+  for (int b = 0; b < SN_MB; ++b) {
+    const int oy = ty * 16 + wave * SN_MB + b;
+    if (oy >= a.Ho) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int x = tx * 16 + fq * 4 + r;
+      if (x < a.Wo) {
+        const long long row = ((long long)n * a.Ho + oy) * a.Wo + x;
+        float v = acc[b][r] + bv;
+        if (a.flags & EPI_RESIDUAL) v += bf2f(a.res[row * a.Cout + fr]);
+        a.out[row * a.Cout + fr] = f2bf(v);
+      }
+    }
+  }
+}
+
+static int conv_smalln_launch(const ConvArgs& a, hipStream_t stream) {
+  const long long nwg = (long long)a.N * ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16);
+  if (nwg > 0x7fffffffLL || nwg < 1) return (int)hipErrorInvalidValue;
+  if (a.kh == 3 && a.kw == 3) conv_nhwc_smalln_kernel<3><<<(unsigned)nwg, 256, 0, stream>>>(a);
+  else if (a.kh == 1 && a.kw == 1) conv_nhwc_smalln_kernel<1><<<(unsigned)nwg, 256, 0, stream>>>(a);
+  else conv_nhwc_smalln_kernel<0><<<(unsigned)nwg, 256, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// variant 12 = the narrow-output kernel above (default for Cout <= 16); variant 2 keeps the
+// 256-row v2 tile for A/B comparisons.
 static int conv_launch(ConvArgs& a, hipStream_t stream, int variant = -2, void* ws = nullptr, long long ws_bytes = 0) {
   if (variant == -2) variant = g_conv_variant;
+  if (a.Cout <= 16 && (variant != 2 || a.Cin % 64 || (a.in2 && a.C1 % 64))) return conv_smalln_launch(a, stream);
   // v3 needs Cout % 8 == 0 for the 16-B epilogue stores (SD/SDXL/VAE convs: all but the 3/4-channel
   // heads, which take v2).
   if (variant != 2 && a.Cout % 8 == 0) return conv_v3_launch(a, variant, stream, ws, ws_bytes);
@@ -631,7 +743,7 @@ static int conv_launch(ConvArgs& a, hipStream_t stream, int variant = -2, void* 
 CGS_EXPORT int cgs_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* res, void* out, int N, int H,
                                int W, int Cin, int Cout, int kh, int kw, int stride, int pad, int Ho, int Wo,
                                hipStream_t stream) {
-  if (Cin % 32 || Cout < 1 || (Cout % 8 && Cin % 64)) return (int)hipErrorInvalidValue;
+  if (Cin % 32 || Cout < 1 || (Cout % 8 && Cout > 16 && Cin % 64)) return (int)hipErrorInvalidValue;
   ConvArgs a{(const u16*)x, nullptr, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W, Cin, Cin,
              Cout, kh, kw, stride, pad, Ho, Wo, (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0), 0, 1};
   return conv_launch(a, stream);
@@ -642,7 +754,7 @@ CGS_EXPORT int cgs_conv2d_nhwc(const void* x, const void* w, const void* bias, c
 CGS_EXPORT int cgs_conv2d_nhwc_ex(const void* x, const void* x2, int C1, const void* w, const void* bias,
                                   const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
                                   int stride, int pad, int Ho, int Wo, int flags, hipStream_t stream) {
-  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && (Cin % 64 || (x2 && C1 % 64))))
+  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && Cout > 16 && (Cin % 64 || (x2 && C1 % 64))))
     return (int)hipErrorInvalidValue;
   ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
              Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
@@ -654,7 +766,7 @@ CGS_EXPORT int cgs_conv2d_nhwc_ex(const void* x, const void* x2, int C1, const v
 CGS_EXPORT int cgs_conv2d_nhwc_v(const void* x, const void* x2, int C1, const void* w, const void* bias,
                                  const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
                                  int stride, int pad, int Ho, int Wo, int flags, int variant, hipStream_t stream) {
-  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && (Cin % 64 || (x2 && C1 % 64))))
+  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && Cout > 16 && (Cin % 64 || (x2 && C1 % 64))))
     return (int)hipErrorInvalidValue;
   ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
              Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
@@ -667,7 +779,7 @@ CGS_EXPORT int cgs_conv2d_nhwc_v7ws(const void* x, const void* x2, int C1, const
                                     const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
                                     int stride, int pad, int Ho, int Wo, int flags, void* ws, long long ws_bytes,
                                     hipStream_t stream) {
-  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && (Cin % 64 || (x2 && C1 % 64))))
+  if (Cin % 32 || (x2 && (C1 % 32)) || Cout < 1 || (Cout % 8 && Cout > 16 && (Cin % 64 || (x2 && C1 % 64))))
     return (int)hipErrorInvalidValue;
   ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
              Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,

@@ -611,7 +611,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         x = torch.cat([x, x2], dim=1)
         x2 = None
     if (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
-            and x.dim() == 4 and x.shape[1] % 32 == 0 and (Cout % 8 == 0 or x.shape[1] % 64 == 0)):
+            and x.dim() == 4 and x.shape[1] % 32 == 0 and (Cout % 8 == 0 or Cout <= 16 or x.shape[1] % 64 == 0)):
         count("conv", "hip")
         N, C1, H, W = x.shape
         Cin = C1 + (0 if x2 is None else x2.shape[1])
@@ -642,7 +642,8 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
 
         variant = -2            # process-wide override (cgs_conv_set_variant), default auto
         M = N * Ho * Wo
-        if M * Cout * Cin * kh * kw >= (1 << 27):
+        # Cout <= 16 (UNet / VAE conv_out): the narrow-output kernel, no tuning (csrc conv_launch)
+        if M * Cout * Cin * kh * kw >= (1 << 27) and Cout > 16:
             cands = [("v4", lambda: run(4))]
             if Cout % 8 == 0:
                 cands.append(("v8", lambda: run(8)))      # 128 x 128 tiles (short grids)

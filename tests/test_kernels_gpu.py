@@ -710,3 +710,63 @@ def test_attention_underfilled_grid_autotuned(cuda, monkeypatch):
                                         q.stride(1), D, ov.stride(0), ov.stride(1), D, D ** -0.5, var,
                                         core._stream()) == 0
         assert _rel(ov, ref) < 2e-2
+
+
+# Narrow-output convs (Cout <= 16: UNet conv_out 320 -> 4, VAE conv_out 128 -> 3): the dedicated
+# kernel (conv_nhwc_smalln_kernel) for every variant but an explicit v2; includes Cin % 64 != 0,
+# stride 2, the fused 2x upsample, a residual and the dual-source (skip-concat) input.
+@pytest.mark.parametrize("N,Cin,H,W,Cout,k,s,up,res", [(2, 320, 128, 128, 4, 3, 1, False, False),
+                                                       (1, 128, 1024, 1024, 3, 3, 1, False, False),
+                                                       (3, 96, 13, 11, 3, 3, 1, False, True),
+                                                       (2, 32, 9, 17, 16, 3, 2, False, False),
+                                                       (1, 64, 10, 6, 8, 1, 1, False, True),
+                                                       (2, 160, 7, 9, 5, 3, 1, True, False)])
+def test_conv2d_narrow_output(cuda, N, Cin, H, W, Cout, k, s, up, res):
+    torch.manual_seed(3)
+    p = k // 2
+    x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, k, k, device=cuda) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
+    b = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    xr = F.interpolate(x.float(), scale_factor=2.0, mode="nearest") if up else x.float()
+    ref = F.conv2d(xr, w.float(), b.float(), s, p)
+    r = None
+    if res:
+        r = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        ref = ref + r.float()
+    wn = w.permute(0, 2, 3, 1).contiguous()
+    y = ops.conv2d(x, w, b, s, p, residual=r, weight_nhwc=wn, upsample2x=up)
+    assert ops.stats().get(("conv", "hip"), 0) == 1 and ops.stats().get(("conv", "lib"), 0) == 0
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+    if H >= 128 and Cin % 64 == 0:      # production shape: time it against the 256-row v2 tile
+        lib = _native.load_kernels()
+
+        def t(variant):
+            lib.cgs_conv_set_variant(variant)
+            try:
+                for _ in range(2):
+                    ops.conv2d(x, w, b, s, p, weight_nhwc=wn)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    ops.conv2d(x, w, b, s, p, weight_nhwc=wn)
+                e1.record()
+                torch.cuda.synchronize()
+                return e0.elapsed_time(e1) / 5
+            finally:
+                lib.cgs_conv_set_variant(-1)
+        t_new, t_v2 = t(-1), t(2)
+        print(f"narrow conv N={N} Cin={Cin} {H}x{W} Cout={Cout}: smalln {t_new * 1e3:.1f} us, v2 {t_v2 * 1e3:.1f} us")
+        assert t_new < t_v2
+
+
+def test_conv2d_narrow_output_dual_source(cuda):
+    torch.manual_seed(4)
+    a = torch.randn(2, 128, 12, 10, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b2 = torch.randn(2, 64, 12, 10, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(16, 192, 3, 3, device=cuda) / math.sqrt(192 * 9)).to(torch.bfloat16)
+    bias = torch.randn(16, device=cuda).to(torch.bfloat16)
+    ref = F.conv2d(torch.cat([a, b2], 1).float(), w.float(), bias.float(), 1, 1)
+    y = ops.conv2d(a, w, bias, 1, 1, weight_nhwc=w.permute(0, 2, 3, 1).contiguous(), x2=b2)
+    assert ops.stats().get(("conv", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
