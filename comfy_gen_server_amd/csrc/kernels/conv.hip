@@ -647,22 +647,21 @@ __global__ __launch_bounds__(256) void conv_nhwc_smalln_kernel(ConvArgs a) {
 #pragma unroll
   for (int b = 0; b < SN_MB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const long long img = (long long)n * a.H;
+  const bf16x8 zero = {};
   for (int c = 0; c < a.Cin; c += 32) {
     const bool second = c >= a.C1;
     const u16* src = second ? a.in2 : a.in;
     const int cs = second ? C2 : a.C1;
     const int cb = (second ? c - a.C1 : c) + 8 * fq;
-    // (measured: hoisting all nine taps' loads ahead of the MFMAs -- 45 in flight, 256 VGPRs, one wave
-    // per SIMD -- was slower on the VAE shape, 287 -> 336 us; the per-tap loop below keeps two waves)
+    // Measured on the VAE 1024^2 shape (one image): this per-tap loop with predicated loads 287 us;
+    // unconditional zero-page loads 337 us; all nine taps' loads hoisted ahead of the MFMAs (45 in
+    // flight, 256 VGPRs, one wave per SIMD) 336 us; the 256-row v2 tile 443 us.
     {
 #pragma unroll
       for (int ky = 0; ky < kh; ++ky) {
 #pragma unroll
         for (int kx = 0; kx < kw; ++kx) {
-          // loads are unconditional (padding taps / unused columns read the zero page): a predicated
-          // load compiles to a branch per lane group and serialises every tap behind vmcnt(0)
-          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(cv ? (const void*)(wrow + (ky * kw + kx) * a.Cin + c)
-                                                                   : (const void*)(g_conv_zero_page + 16 * fq));
+          const bf16x8 bfr = cv ? *reinterpret_cast<const bf16x8*>(wrow + (ky * kw + kx) * a.Cin + c) : zero;
           int ix = px + kx;
           const bool okx = ix >= 0 && ix < Win;
           if (up) ix >>= 1;
@@ -672,8 +671,7 @@ __global__ __launch_bounds__(256) void conv_nhwc_smalln_kernel(ConvArgs a) {
             int iy = py[b] + ky;
             const bool ok = pv[b] && okx && iy >= 0 && iy < Hin;
             if (up) iy >>= 1;
-            af[b] = *reinterpret_cast<const bf16x8*>(ok ? (const void*)(src + ((img + iy) * a.W + ix) * cs + cb)
-                                                        : (const void*)(g_conv_zero_page + 16 * fq));
+            af[b] = ok ? *reinterpret_cast<const bf16x8*>(src + ((img + iy) * a.W + ix) * cs + cb) : zero;
           }
 #pragma unroll
           for (int b = 0; b < SN_MB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[b], bfr, acc[b], 0, 0, 0);

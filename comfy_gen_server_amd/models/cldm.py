@@ -47,7 +47,31 @@ class ControlNet(UNetModel):
                 h = ops.silu(h)
         return h
 
-    def forward(self, x, hint, timesteps, context, y=None, transformer_options=None, **kwargs):
+    def _zero(self, conv, h, scale, res):
+        """One zero conv with the ControlNet merge fused into its epilogue (K15):
+        ``scale * conv(h) + res`` -- ``res`` is the chained previous ControlNet's residual for the same
+        injection point (controlnet.py:92-138 control_merge). On the device the strength is folded into
+        a scaled copy of the 1x1 weights/bias (one slot, recomputed when the strength changes) and
+        ``res`` is the conv kernel's residual epilogue, so the residual leaves the kernel merged."""
+        if res is not None:
+            res = res.to(h.dtype)
+        if scale == 1.0:
+            return conv(h, residual=res)
+        if h.is_cuda and conv.weight.dtype == h.dtype and conv.weight.device == h.device:
+            d = conv.__dict__.setdefault("_derived", {})
+            ent = d.get("w_scaled")
+            if ent is None or ent[0] != scale:
+                w = (conv.weight.float() * scale).to(h.dtype)
+                b = None if conv.bias is None else (conv.bias.float() * scale).to(h.dtype)
+                ent = d["w_scaled"] = (scale, w, b, w.permute(0, 2, 3, 1).contiguous())
+            return ops.conv2d(h, ent[1], ent[2], conv.stride, conv.padding, residual=res, weight_nhwc=ent[3])
+        y = conv(h) * scale
+        return y if res is None else y + res
+
+    def forward(self, x, hint, timesteps, context, y=None, transformer_options=None, zero_scale=None,
+                zero_residuals=None, **kwargs):
+        """Returns the zero-conv residuals (input blocks in order, then the middle block). With
+        ``zero_scale`` / ``zero_residuals`` set, each is already ``strength * out + previous``."""
         to = dict(transformer_options or {})
         to.pop("patches", None)
         to.pop("patches_replace", None)
@@ -74,8 +98,14 @@ class ControlNet(UNetModel):
             if guided is not None:
                 h = h + guided
                 guided = None
-            outs.append(zc[0](h))
+            outs.append(self._emit(zc[0], h, len(outs), zero_scale, zero_residuals))
         to["block"] = ("middle", 0)
         h = self.middle_block(h, emb_silu, context, to)
-        outs.append(self.middle_block_out[0](h))
+        outs.append(self._emit(self.middle_block_out[0], h, len(outs), zero_scale, zero_residuals))
         return outs
+
+    def _emit(self, conv, h, i, scale, residuals):
+        if scale is None and residuals is None:
+            return conv(h)
+        return self._zero(conv, h, 1.0 if scale is None else float(scale),
+                          None if residuals is None else residuals[i])

@@ -186,9 +186,38 @@ class ControlNet(ControlBase):
         ms = self.model_sampling_current
         timestep = ms.timestep(t)
         x_in = ms.calculate_input(t, x_noisy)
+        fused = self._fusable(x_noisy, prev)
+        if fused is not None:
+            # K15: strength and the chained net's residuals are applied inside the zero convs'
+            # epilogues; residuals stay in the control model's dtype (the UNet's), no fp32 round trip
+            control = self.control_model(x=x_in.to(dtype), hint=self.cond_hint, timesteps=timestep.float(),
+                                         context=context.to(dtype), y=y, zero_scale=self.strength,
+                                         zero_residuals=fused)
+            return {"input": [] if prev is None else list(prev["input"]), "middle": control[-1:],
+                    "output": control[:-1]}
         control = self.control_model(x=x_in.to(dtype), hint=self.cond_hint, timesteps=timestep.float(),
                                      context=context.to(dtype), y=y)
         return self.control_merge(None, control, prev, x_noisy.dtype)
+
+    def _fusable(self, x_noisy, prev):
+        """Residual list for the fused merge (None entries where there is no previous residual), or
+        None when the merge must run unfused: CPU, global-average pooling, CGS_CN_FUSE=0, or a chained
+        net whose residual lists / batch sizes do not line up one-to-one with this net's outputs."""
+        import os
+        from ..models.cldm import ControlNet as _CN
+        if not x_noisy.is_cuda or self.global_average_pooling or os.environ.get("CGS_CN_FUSE", "1") == "0" \
+                or not isinstance(self.control_model, _CN):
+            return None
+        n_out = len(self.control_model.zero_convs)
+        if prev is None:
+            return [None] * (n_out + 1)
+        po, pm = list(prev.get("output", [])), list(prev.get("middle", []))
+        if len(po) != n_out or len(pm) != 1:
+            return None
+        res = po + pm
+        if any(r is not None and r.shape[0] != x_noisy.shape[0] for r in res):
+            return None
+        return res
 
     def copy(self):
         c = ControlNet(None, global_average_pooling=self.global_average_pooling, load_device=self.load_device,

@@ -228,3 +228,50 @@ def test_step_graph_static_kv_new_prompt_per_job(cuda, monkeypatch):
     for a, b in zip(res["0"], res["1"]):
         err = (a - b).abs().max().item()
         assert err < 2e-2 * (a.abs().max().item() + 1), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strength", [1.0, 0.7])
+def test_controlnet_fused_merge_matches_unfused(cuda, monkeypatch, strength):
+    """K15: strength and the chained net's residuals applied in the zero convs' epilogues (scaled 1x1
+    weights + residual epilogue) give the same control dict as the unfused merge (x * strength, cast,
+    then + previous)."""
+    import copy
+    from comfy_gen_server_amd.models.cldm import ControlNet as CN
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    from comfy_gen_server_amd.runtime import controlnet as rcn
+    from comfy_gen_server_amd.tools.synth import TINY_UNET, build_pipeline
+    from comfy_gen_server_amd import ops
+    with torch.inference_mode():
+        patcher, _, _ = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        cfg = copy.deepcopy(TINY_UNET)
+        cfg.update(num_heads=2, num_head_channels=-1)
+        nets = []
+        for seed in (7, 8):
+            cm = CN(hint_channels=3, dtype=torch.bfloat16, device=cuda, **cfg)
+            init_random_fast_(cm, seed=seed)
+            c = rcn.ControlNet(cm, load_device=cuda)
+            c.cond_hint_original = torch.rand(1, 3, 64, 64)
+            c.strength = strength if seed == 7 else 0.5
+            c.model_sampling_current = patcher.model.model_sampling
+            nets.append(c)
+        nets[0].previous_controlnet = nets[1]
+        x = torch.randn(2, 4, 8, 8, device=cuda)
+        t = torch.tensor([5.0, 5.0], device=cuda)
+        cond = {"c_crossattn": torch.randn(2, 7, cfg["context_dim"], device=cuda, dtype=torch.bfloat16)}
+        if cfg.get("adm_in_channels"):
+            cond["y"] = torch.randn(2, cfg["adm_in_channels"], device=cuda)
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_CN_FUSE", mode)
+            for n in nets:
+                n.cond_hint = None
+            res[mode] = nets[0].get_control(x, t, cond, 1)
+        torch.cuda.synchronize()
+    assert ops.stats().get(("conv", "hip"), 0) > 0
+    for key in ("middle", "output"):
+        assert len(res["0"][key]) == len(res["1"][key]) > 0
+        for a, b in zip(res["0"][key], res["1"][key]):
+            assert b.dtype == torch.bfloat16
+            err = (a.float() - b.float()).abs().max().item()
+            assert err < 2e-2 * (a.float().abs().max().item() + 1e-3), (key, err)
