@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import Conv2d, DerivedMixin, LayerNorm, Linear
+from .layers import Conv2d, DerivedMixin, LayerNorm, Linear, module_epoch
 
 
 # ------------------------------------------------------------------------------------------------
@@ -37,6 +37,11 @@ def _cast(w, x):
 def _pw(conv, x, residual=None):
     """1x1 conv on an NHWC tensor as a GEMM over the channel dim."""
     w = _cast(conv.weight, x).reshape(conv.out_channels, conv.in_channels)
+    if x.is_cuda and conv.in_channels % 32:
+        # narrow K (Stage A's 4-channel latent in): zero-pad K to 32 so the HIP GEMM takes it
+        kp = (conv.in_channels + 31) // 32 * 32
+        w = F.pad(w, (0, kp - conv.in_channels))
+        x = F.pad(x, (0, kp - conv.in_channels))
     return ops.linear(x, w, _cast(conv.bias, x), residual=residual)
 
 
@@ -570,7 +575,20 @@ class StageA(nn.Module):
         b = _cast(mod.bias, x)
         xn = x.permute(0, 3, 1, 2)
         if isinstance(mod, nn.ConvTranspose2d):
-            y = F.conv_transpose2d(xn, w, b, mod.stride, mod.padding)
+            pw = None
+            if xn.is_cuda and w is mod.weight:       # phase weights cached per weight version (K09 form)
+                key = (w.data_ptr(), module_epoch(mod))     # epoch: bumped on every weight patch
+                ent = mod.__dict__.get("_cgs_ct_phase")
+                if ent is None or ent[0] != key:
+                    ent = mod.__dict__["_cgs_ct_phase"] = (key, ops.conv_transpose_phase_weights(w))
+                pw = ent[1]
+            y = ops.conv_transpose2d(xn, w, b, mod.stride, mod.padding, phase_weights=pw)
+        elif xn.is_cuda and w is mod.weight:
+            ent = mod.__dict__.get("_cgs_w_nhwc")
+            key = (w.data_ptr(), module_epoch(mod))
+            if ent is None or ent[0] != key:
+                ent = mod.__dict__["_cgs_w_nhwc"] = (key, w.permute(0, 2, 3, 1).contiguous())
+            y = ops.conv2d(xn, w, b, mod.stride, mod.padding, weight_nhwc=ent[1])
         else:
             y = F.conv2d(xn, w, b, mod.stride, mod.padding)
         return _to_nhwc(y)

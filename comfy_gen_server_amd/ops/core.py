@@ -670,6 +670,52 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
     return y
 
 
+# ConvTranspose2d(k=4, s=2, p=1) as four sub-pixel phases: output pixel (2y + py, 2x + px) sums the
+# 2 x 2 input neighbourhood starting at (y - 1 + py, x - 1 + px) through kernel taps _CT_TAPS[py] x
+# _CT_TAPS[px] (tap k of the transposed conv reaches output 2i - 1 + k).
+_CT_TAPS = ((3, 1), (2, 0))
+
+
+def conv_transpose_phase_weights(weight: torch.Tensor):
+    """[Cin, Cout, 4, 4] ConvTranspose2d weight -> four ([Cout, Cin, 2, 2], NHWC copy) phase convs."""
+    out = []
+    for py in range(2):
+        for px in range(2):
+            wp = weight[:, :, list(_CT_TAPS[py])][:, :, :, list(_CT_TAPS[px])].permute(1, 0, 2, 3).contiguous()
+            out.append((wp, wp.permute(0, 2, 3, 1).contiguous()))
+    return out
+
+
+def conv_transpose2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
+                     phase_weights=None) -> torch.Tensor:
+    """ConvTranspose2d (Stable Cascade Stage A decoder's 4x4 / stride-2 upsampler, cascade.py).
+
+    Device path for k = 4, s = 2, p = 1: four 2 x 2 convs (one per output sub-pixel phase, pad 1, on
+    the NHWC implicit-GEMM conv kernel) written into the interleaved output -- the overlap-add of
+    the transposed conv is never formed and no library kernel runs (MIOpen's backward-data conv
+    took ~180 ms per call on this shape). ``phase_weights``: cached conv_transpose_phase_weights()."""
+    s = stride[0] if isinstance(stride, (tuple, list)) else stride
+    p = padding[0] if isinstance(padding, (tuple, list)) else padding
+    Cin, Cout, kh, kw = weight.shape
+    be = backend_for("conv", x, "cgs_conv2d_nhwc")
+    if (be == "hip" and x.dim() == 4 and x.dtype == torch.bfloat16 and weight.dtype == x.dtype and kh == kw == 4
+            and s == 2 and p == 1 and Cin % 32 == 0 and (Cout % 8 == 0 or Cout <= 16)):
+        N, _, H, W = x.shape
+        pw = phase_weights if phase_weights is not None else conv_transpose_phase_weights(weight)
+        out = torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+        for i, (wp, wn) in enumerate(pw):
+            py, px = divmod(i, 2)
+            y = conv2d(x, wp, bias, 1, 1, weight_nhwc=wn)          # [N, Cout, H + 1, W + 1]
+            out[:, :, py::2, px::2] = y[:, :, py:py + H, px:px + W]
+        return out
+    if be == "torch":
+        count("conv", "torch")
+        y = F.conv_transpose2d(x.float(), weight.float(), None if bias is None else bias.float(), s, p)
+        return y.to(x.dtype)
+    vendor_fallback("conv", f"conv_transpose2d k={kh}x{kw} s={s} p={p} dtype {x.dtype}")
+    return F.conv_transpose2d(x, weight, bias, s, p)
+
+
 def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
     be = backend_for("upsample", x, "cgs_upsample_nearest2x_nhwc")
     if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16):

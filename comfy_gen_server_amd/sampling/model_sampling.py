@@ -240,7 +240,9 @@ class StableCascadeSampling(ModelSamplingDiscrete):
     def timestep(self, sigma):
         var = 1 / ((sigma * sigma) + 1)
         var = var.clamp(0, 1.0)
-        s, min_var = self.cosine_s.to(var.device), self._init_alpha_cumprod.to(var.device)
+        # host scalars (fp32 values, applied in var's dtype): no H2D copy, so a captured step graph
+        # (sampling/step_graph.py) can hold this -- a .to(device) here made every Cascade capture fail
+        s, min_var = float(self.cosine_s), float(self._init_alpha_cumprod)
         t = (((var * min_var) ** 0.5).acos() / (torch.pi * 0.5)) * (1 + s) - s
         return t
 
