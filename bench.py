@@ -165,6 +165,8 @@ def main():
         if _dp.STAGE_TIMES:
             res["stage_seconds"] = {k: [round(x, 3) for x in v] for k, v in _dp.STAGE_TIMES.items()}
         res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
+        from comfy_gen_server_amd.sampling import step_graph as _sg
+        res["step_graph"] = dict(_sg.stats)      # capture / replay / capture_failed counts
         print(json.dumps(res), flush=True)
     comm.shutdown()
 

@@ -258,6 +258,7 @@ def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
             body("use")
         torch.cuda.synchronize()
     except Exception as e:  # capture-unsafe op in the step: this plan stays eager
+        stats["capture_failed"] = stats.get("capture_failed", 0) + 1
         logging.warning("step hipGraph capture failed (%s); sampling stays eager", e,
                         exc_info=os.environ.get("CGS_GRAPH_DEBUG", "0") == "1")
         try:

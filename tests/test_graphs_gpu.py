@@ -275,3 +275,39 @@ def test_controlnet_fused_merge_matches_unfused(cuda, monkeypatch, strength):
             assert b.dtype == torch.bfloat16
             err = (a.float() - b.float()).abs().max().item()
             assert err < 2e-2 * (a.float().abs().max().item() + 1e-3), (key, err)
+
+
+@pytest.mark.gpu
+def test_cascade_stage_c_step_graph_captures(cuda, monkeypatch):
+    """Stable Cascade Stage C sampling captures its Euler-a steps into hipGraphs (a host->device copy in
+    the Cascade timestep used to abort every capture silently) and replays the eager result."""
+    from comfy_gen_server_amd.graph import registry
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    from comfy_gen_server_amd.runtime import families
+    from comfy_gen_server_amd.runtime.patcher import ModelPatcher
+    from comfy_gen_server_amd.sampling import step_graph
+    registry.init_nodes(custom_nodes=False)
+    NM = registry.NODE_CLASS_MAPPINGS
+    cfg = dict(c_in=16, c_out=16, c_r=64, c_cond=64, c_hidden=[64, 64], nhead=[2, 2], blocks=[[1, 1], [1, 1]],
+               block_repeat=[[1, 1], [2, 1]], level_config=["CTA", "CTA"], c_clip_text=64, c_clip_text_pooled=64,
+               c_clip_img=768, c_clip_seq=2, switch_level=[False], stable_cascade_stage="c")
+    model = families.Stable_Cascade_C(cfg).get_model({})
+    model.diffusion_model.to(device=cuda, dtype=torch.bfloat16)
+    init_random_fast_(model.diffusion_model, seed=10)
+    patcher = ModelPatcher(model, load_device=cuda, offload_device=cuda)
+    g = torch.Generator().manual_seed(0)
+    pos = [[torch.randn(1, 7, 64, generator=g), {"pooled_output": torch.randn(1, 64, generator=g)}]]
+    neg = [[torch.zeros(1, 7, 64), {"pooled_output": torch.zeros(1, 64)}]]
+    lat_c, _ = NM["StableCascade_EmptyLatentImage"]().generate(512, 512, 42, 2)
+    res = {}
+    with torch.inference_mode():
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_GRAPHS", mode)
+            before = dict(step_graph.stats)
+            res[mode] = NM["KSampler"]().sample(patcher, 3, 5, 4.0, "euler_ancestral", "simple", pos, neg, lat_c,
+                                                1.0)[0]["samples"].float()
+        torch.cuda.synchronize()
+    assert step_graph.stats.get("capture_failed", 0) == before.get("capture_failed", 0)
+    assert step_graph.stats["capture"] > before.get("capture", 0) and step_graph.stats["replay"] > before["replay"]
+    err = (res["0"] - res["1"]).abs().max().item()
+    assert err < 2e-2 * (res["0"].abs().max().item() + 1), err
