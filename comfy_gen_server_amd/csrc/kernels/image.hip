@@ -254,10 +254,11 @@ __global__ void __launch_bounds__(256) grn2_sumsq_kernel(const u16* __restrict__
     for (int r = r0 + rg; r < r1; r += 4) {
       const s16x8 v = *reinterpret_cast<const s16x8*>(xb + (size_t)r * C);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float f = cvt_in<DT>((u16)v[j]);
-        if (GELU) f = gelu_f(f);
-        acc[j] += f * f;
+      for (int j = 0; j < 8; j += 2) {
+        f32x2_t f = {cvt_in<DT>((u16)v[j]), cvt_in<DT>((u16)v[j + 1])};
+        if (GELU) f = gelu_fast2(f);     // A&S 7.1.26 erf (|err| <= 1.5e-7): erff made GRN ALU-bound
+        acc[j] += f.x * f.x;
+        acc[j + 1] += f.y * f.y;
       }
     }
   }
@@ -302,11 +303,13 @@ template <int DT, bool GELU>
 __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__ x, const float* __restrict__ nx,
                                                          const u16* __restrict__ gamma, const u16* __restrict__ beta,
                                                          u16* __restrict__ y, long long chunks, int HW, int C) {
-  const int cpr = C >> 3;
+  const unsigned cpr = (unsigned)C >> 3;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < chunks; i += (long long)gridDim.x * 256) {
-    const long long row = i / cpr;
-    const int c0 = (int)(i - row * cpr) * 8;
-    const int n = (int)(row / HW);
+    // 32-bit index math (chunks < 2^32, checked by the launcher): 64-bit divisions cost ~10x
+    const unsigned iu = (unsigned)i;
+    const unsigned row = iu / cpr;
+    const int c0 = (int)(iu - row * cpr) * 8;
+    const int n = (int)(row / (unsigned)HW);
     const s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
     const s16x8 gm = *reinterpret_cast<const s16x8*>(gamma + c0);
     const s16x8 bt = *reinterpret_cast<const s16x8*>(beta + c0);
@@ -315,10 +318,11 @@ __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__
     const float nv[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
     s16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float f = cvt_in<DT>((u16)v[j]);
-      if (GELU) f = gelu_f(f);
-      o[j] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j]) + f * (1.f + cvt_in<DT>((u16)gm[j]) * nv[j]));
+    for (int j = 0; j < 8; j += 2) {
+      f32x2_t f = {cvt_in<DT>((u16)v[j]), cvt_in<DT>((u16)v[j + 1])};
+      if (GELU) f = gelu_fast2(f);
+      o[j] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j]) + f.x * (1.f + cvt_in<DT>((u16)gm[j]) * nv[j]));
+      o[j + 1] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j + 1]) + f.y * (1.f + cvt_in<DT>((u16)gm[j + 1]) * nv[j + 1]));
     }
     reinterpret_cast<s16x8*>(y)[i] = o;
   }
@@ -840,6 +844,7 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
   float* nx = ws + (size_t)N * S * C;
   dim3 g1((unsigned)((C / 8 + 63) / 64), (unsigned)S, (unsigned)N);
   const long long chunks = (long long)N * HW * (C / 8);
+  if (chunks >= (1LL << 32)) return (int)hipErrorInvalidValue;
   long long nb = (chunks + 255) / 256;
   const int blocks = (int)(nb > 16384 ? 16384 : nb);
 #define CGS_GRN2(DTV, GV)                                                                                        \

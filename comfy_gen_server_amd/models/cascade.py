@@ -178,8 +178,8 @@ class TimestepBlock(nn.Module):
     def forward(self, x, t):
         t = t.chunk(len(self.conds) + 1, dim=1)
         ab = self.mapper(t[0])
-        for i, name in enumerate(self.conds):
-            ab = ab + getattr(self, f"mapper_{name}")(t[i + 1])
+        for i, name in enumerate(self.conds):      # the sum rides the GEMMs' residual epilogue
+            ab = getattr(self, f"mapper_{name}")(t[i + 1], residual=ab)
         a, b = ab[:, None, None, :].chunk(2, dim=-1)
         return torch.addcmul(b, x, 1 + a)
 

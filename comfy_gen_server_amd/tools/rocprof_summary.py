@@ -17,6 +17,7 @@ def short_name(name: str, width: int = 90) -> str:
     if n.startswith("_ZN"):   # mangled (CK / Tensile): keep the readable identifier chunks
         parts = re.findall(r"\d+([A-Za-z_][A-Za-z0-9_]*)", n[:400])
         n = "::".join(p for p in parts[:6] if len(p) > 2)
+    n = n.replace("(anonymous namespace)", "anon")
     n = re.sub(r"\(.*", "", n)
     return n if len(n) <= width else n[: width - 3] + "..."
 
