@@ -121,14 +121,19 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     if n < 1 or n > CAPACITY:
         return None
     cond = _conditioning(guider, lists, x, s[0])
-    if cond is None or any(not isinstance(v, torch.Tensor) or not v.is_cuda for v in cond.values()):
+    # device tensors, or host scalars that are constant over the run (SVD's num_video_frames): those are
+    # part of the plan key and baked into the captured graph
+    if cond is None or any(not (isinstance(v, torch.Tensor) and v.is_cuda) and
+                           not (isinstance(v, (int, float, bool)) and not isinstance(v, torch.Tensor))
+                           for v in cond.values()):
         return None
     model = guider.inner_model
     # floating conds in the model's compute dtype up front: apply_model's .to(dtype) is then the
     # identity, so the UNet sees the plan's static tensors themselves (static K/V keys on them)
     try:
         mdt = model.manual_cast_dtype or model.get_dtype()
-        cond = {k: (v.to(mdt) if v.is_floating_point() and k in ("c_crossattn", "y") else v) for k, v in cond.items()}
+        cond = {k: (v.to(mdt) if torch.is_tensor(v) and v.is_floating_point() and k in ("c_crossattn", "y") else v)
+                for k, v in cond.items()}
     except Exception:
         pass
     chain = _chain(ctrl)
@@ -143,7 +148,8 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     from ..models import layers
     epoch = layers.module_epoch(model)
     key = (epoch, tuple(x.shape), use_uncond, float(guider.cfg),
-           tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in cond.items())),
+           tuple(sorted((k, tuple(v.shape), v.dtype) if torch.is_tensor(v) else (k, "scalar", v)
+                        for k, v in cond.items())),
            tuple((id(cn.control_model), layers.module_epoch(cn.control_model), float(cn.strength),
                   bool(cn.global_average_pooling), tuple(h.shape), h.dtype) for cn, h in zip(chain, hints)))
     plans = model.__dict__.setdefault("_step_graph_plans", {})
@@ -175,7 +181,8 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     plan.meta.copy_(torch.tensor([0, int(extra_args["seed"]) & 0x7FFFFFFFFFFFFFFF, index0], dtype=torch.int64))
     plan.x.copy_(x)
     for k, v in cond.items():
-        plan.cond[k].copy_(v)
+        if torch.is_tensor(v):
+            plan.cond[k].copy_(v)
     if plan.kv_sources:
         # the run's constant context -> every cross-attention K/V once per job (the captured steps
         # read the buffers instead of recomputing them each step)
@@ -202,9 +209,10 @@ def _new_plan(x, cond, hints):
     p.meta = torch.zeros(3, device=dev, dtype=torch.int64)
     p.sig = torch.empty(x.shape[0], device=dev, dtype=torch.float32)
     p.den = torch.empty_like(p.x)
-    p.cond = {k: v.detach().clone() for k, v in cond.items()}
+    p.cond = {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in cond.items()}
     # static cross-attention K/V over the plan's context buffers (CGS_STATIC_KV=0 disables)
-    p.kv_sources = frozenset(id(v) for v in p.cond.values()) if os.environ.get("CGS_STATIC_KV", "1") != "0" \
+    p.kv_sources = frozenset(id(v) for v in p.cond.values() if torch.is_tensor(v)) \
+        if os.environ.get("CGS_STATIC_KV", "1") != "0" \
         else frozenset()
     p.hints = list(hints)           # the first job's prepared hint tensors become the static inputs
     p.graphs = {}

@@ -55,3 +55,38 @@ def test_temporal_vae_device_matches_cpu(cuda):
         md.load_state_dict(m.state_dict())
         out = md(z.to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last))
     assert _rel(out.cpu(), ref) < 3e-2
+
+
+def test_svd_sampling_step_graph(cuda, monkeypatch):
+    """SVD img2vid (tiny, random init) sampled with Euler through the captured step graph: no capture
+    failure (no silent eager fallback) and graph replay == eager."""
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    from comfy_gen_server_amd.runtime import families
+    from comfy_gen_server_amd.runtime.patcher import ModelPatcher
+    from comfy_gen_server_amd.sampling import sample as S, step_graph
+    small = dict(CFG, model_channels=64, num_res_blocks=[1, 1], channel_mult=[1, 2], transformer_depth=[1, 1],
+                 transformer_depth_output=[1, 1, 1, 1], num_head_channels=16, context_dim=64, adm_in_channels=768)
+    mc = families.SVD_img2vid(small)
+    mc.set_inference_dtype(torch.bfloat16)
+    model = mc.get_model({})
+    model.diffusion_model.to(device=cuda, dtype=torch.bfloat16)
+    init_random_fast_(model.diffusion_model, seed=2)
+    patcher = ModelPatcher(model, load_device=cuda, offload_device=cuda)
+    g = torch.Generator().manual_seed(0)
+    extra = dict(motion_bucket_id=127, fps=6, augmentation_level=0.0)
+    pos = [[torch.randn(1, 1, 64, generator=g), dict(extra, concat_latent_image=torch.randn(1, 4, 8, 8, generator=g))]]
+    neg = [[torch.zeros(1, 1, 64), dict(extra, concat_latent_image=torch.zeros(1, 4, 8, 8))]]
+    latent = torch.zeros(3, 4, 8, 8)
+    res = {}
+    with torch.inference_mode():
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_GRAPHS", mode)
+            before = dict(step_graph.stats)
+            noise = S.prepare_noise(latent, 3)
+            res[mode] = S.sample(patcher, noise, 4, 2.5, "euler", "karras", pos, neg, latent, seed=3).float()
+        torch.cuda.synchronize()
+    assert step_graph.stats.get("capture_failed", 0) == before.get("capture_failed", 0), step_graph.stats
+    assert step_graph.stats["replay"] > before["replay"], step_graph.stats    # the video UNet is captured too
+    err = (res["0"] - res["1"]).abs().max().item()
+    assert err < 2e-2 * (res["0"].abs().max().item() + 1), err
+    print("svd step graph", {k: step_graph.stats[k] - before.get(k, 0) for k in step_graph.stats})
