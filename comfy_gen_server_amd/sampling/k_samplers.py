@@ -301,6 +301,9 @@ def sample_dpmpp_sde(model, x, sigmas, extra_args=None, callback=None, disable=N
 @torch.no_grad()
 def sample_dpmpp_2m(model, x, sigmas, extra_args=None, callback=None, disable=None):
     extra_args = {} if extra_args is None else extra_args
+    r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "dpmpp_2m")
+    if r is not None:
+        return r
     s = _f(sigmas)
     s_in = _s_in(x)
     old = None

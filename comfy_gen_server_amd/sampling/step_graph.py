@@ -30,6 +30,7 @@ disables it.
 from __future__ import annotations
 
 import logging
+import math
 import os
 import threading
 
@@ -45,7 +46,8 @@ stats = {"capture": 0, "replay": 0, "jobs": 0}
 
 
 class _Plan:
-    __slots__ = ("graphs", "x", "params", "meta", "sig", "den", "cond", "hints", "pool", "kv_sources")
+    __slots__ = ("graphs", "x", "params", "meta", "sig", "den", "cond", "hints", "pool", "kv_sources", "kind",
+                 "old", "w")
 
 
 def _ancestral(s0, s1, eta):
@@ -147,7 +149,7 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
         hints = [cn.prepare_hint(xin, batched) for cn in chain]
     from ..models import layers
     epoch = layers.module_epoch(model)
-    key = (epoch, tuple(x.shape), use_uncond, float(guider.cfg),
+    key = (epoch, kind == "dpmpp_2m", tuple(x.shape), use_uncond, float(guider.cfg),
            tuple(sorted((k, tuple(v.shape), v.dtype) if torch.is_tensor(v) else (k, "scalar", v)
                         for k, v in cond.items())),
            tuple((id(cn.control_model), layers.module_epoch(cn.control_model), float(cn.strength),
@@ -156,6 +158,7 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     plan = plans.get(key)
     if plan is None:
         plan = _new_plan(x, cond, hints)
+        plan.kind = "dpmpp_2m" if kind == "dpmpp_2m" else "euler"
         with _lock:
             for k in [k for k in plans if k[0] != epoch]:
                 del plans[k]
@@ -170,6 +173,17 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     # per-job inputs
     rows = []
     for i in range(n):
+        if kind == "dpmpp_2m":
+            # DPM++ 2M (k_samplers.sample_dpmpp_2m) is the Euler update x' = (s'/s) x + (1 - s'/s) d applied
+            # to d = den + w (den - den_prev), w = 1 / (2 r) with r = h_last / h (0 on the first and last
+            # steps); column 3 carries w (no noise: sigma_up = 0)
+            w = 0.0
+            if i > 0 and s[i + 1] > 0:
+                h = math.log(s[i]) - math.log(s[i + 1])
+                h_last = math.log(s[i - 1]) - math.log(s[i])
+                w = 1.0 / (2.0 * (h_last / h))
+            rows.append((s[i], s[i + 1], 0.0, w))
+            continue
         if kind == "euler_ancestral":
             down, up = _ancestral(s[i], s[i + 1], eta)
             if s[i + 1] <= 0:
@@ -180,6 +194,8 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     plan.params[:n].copy_(torch.tensor(rows, dtype=torch.float32))
     plan.meta.copy_(torch.tensor([0, int(extra_args["seed"]) & 0x7FFFFFFFFFFFFFFF, index0], dtype=torch.int64))
     plan.x.copy_(x)
+    if plan.old is not None:
+        plan.old.zero_()
     for k, v in cond.items():
         if torch.is_tensor(v):
             plan.cond[k].copy_(v)
@@ -217,6 +233,9 @@ def _new_plan(x, cond, hints):
     p.hints = list(hints)           # the first job's prepared hint tensors become the static inputs
     p.graphs = {}
     p.pool = None
+    p.kind = "euler"
+    p.old = torch.zeros_like(p.x)          # DPM++ 2M: previous step's denoised
+    p.w = torch.zeros(1, device=dev, dtype=torch.float32)
     return p
 
 
@@ -243,7 +262,17 @@ def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
         if chain:
             control = chain[0].get_control(xin, tin, p.cond, 2 if use_uncond else 1)
         out = model.apply_model(xin, tin, control=control, transformer_options=t, **p.cond)
-        if use_uncond:
+        if p.kind == "dpmpp_2m":
+            if use_uncond:
+                oc, ou = out.chunk(2)
+                p.den.copy_(ops.cfg_combine(oc.float().contiguous(), ou.float().contiguous(), cfg))
+            else:
+                p.den.copy_(out)
+            ops.step_param(p.w, p.params, p.meta, 3)
+            d = torch.addcmul(p.den, p.w, p.den - p.old)
+            ops.sampler_step_dev(p.x, d, None, None, 1.0, p.params, p.meta)
+            p.old.copy_(p.den)
+        elif use_uncond:
             oc, ou = out.chunk(2)
             ops.sampler_step_dev(p.x, oc.contiguous(), ou.contiguous(), p.den, cfg, p.params, p.meta)
         else:

@@ -73,7 +73,7 @@ def test_graphs_cpu_is_eager():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sampler", ["euler_ancestral", "euler"])
+@pytest.mark.parametrize("sampler", ["euler_ancestral", "euler", "dpmpp_2m"])
 def test_step_graph_matches_eager_loop(cuda, monkeypatch, sampler):
     """One captured graph per sampler step (UNet(cond||uncond) + CFG + Euler(-a) + in-register noise,
     every scalar from a device table) reproduces the eager Python loop, for two jobs through the
@@ -84,6 +84,7 @@ def test_step_graph_matches_eager_loop(cuda, monkeypatch, sampler):
     with torch.inference_mode():
         patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
         res = {}
+        before = dict(step_graph.stats)
         for mode in ("0", "1"):
             monkeypatch.setenv("CGS_GRAPHS", mode)
             outs = []
@@ -92,7 +93,8 @@ def test_step_graph_matches_eager_loop(cuda, monkeypatch, sampler):
                 outs.append(generate_local(patcher, clip, vae, job, off, 3, decode=False).float())
             res[mode] = outs
         torch.cuda.synchronize()
-    assert step_graph.stats["capture"] >= 1 and step_graph.stats["replay"] >= 12
+    assert step_graph.stats["capture"] - before["capture"] >= 1
+    assert step_graph.stats["replay"] - before["replay"] >= 12 and step_graph.stats["jobs"] - before["jobs"] == 2
     for a, b in zip(res["0"], res["1"]):
         err = (a - b).abs().max().item()
         assert err < 2e-2 * (a.abs().max().item() + 1), err
