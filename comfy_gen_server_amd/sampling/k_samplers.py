@@ -507,6 +507,10 @@ def sample_ddpm(model, x, sigmas, extra_args=None, callback=None, disable=None, 
 @torch.no_grad()
 def sample_lcm(model, x, sigmas, extra_args=None, callback=None, disable=None, noise_sampler=None):
     extra_args = {} if extra_args is None else extra_args
+    if noise_sampler is None:
+        r = step_graph.try_sample(model, x, sigmas, extra_args, callback, "lcm")
+        if r is not None:
+            return r
     ns = _noise_sampler(x, extra_args, noise_sampler)
     s = _f(sigmas)
     s_in = _s_in(x)

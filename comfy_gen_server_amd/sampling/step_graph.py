@@ -184,6 +184,11 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
                 w = 1.0 / (2.0 * (h_last / h))
             rows.append((s[i], s[i + 1], 0.0, w))
             continue
+        if kind == "lcm":
+            # LCM (k_samplers.sample_lcm): x' = den + s' * noise == the Euler-a kernel with sigma_down = 0,
+            # sigma_up = s', s_noise = 1 (same per-step noise stream as the eager loop)
+            rows.append((s[i], 0.0, s[i + 1], 1.0))
+            continue
         if kind == "euler_ancestral":
             down, up = _ancestral(s[i], s[i + 1], eta)
             if s[i + 1] <= 0:

@@ -73,7 +73,7 @@ def test_graphs_cpu_is_eager():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sampler", ["euler_ancestral", "euler", "dpmpp_2m"])
+@pytest.mark.parametrize("sampler", ["euler_ancestral", "euler", "dpmpp_2m", "lcm"])
 def test_step_graph_matches_eager_loop(cuda, monkeypatch, sampler):
     """One captured graph per sampler step (UNet(cond||uncond) + CFG + Euler(-a) + in-register noise,
     every scalar from a device table) reproduces the eager Python loop, for two jobs through the
