@@ -99,10 +99,8 @@ def main():
         log(f"step {i}: {time.perf_counter() - ts:.2f}s")
         return r
 
-    # pipelined serving is on for one GPU; with N ranks the image all-gather would run on the side
-    # stream concurrently with the next job's broadcast, which only CGS_DP_PIPELINE_MULTI=1 enables
-    # (the 1-GPU A/B gain is < 1 %, not worth an unexercised collective ordering at N > 1).
-    args.pipeline = args.pipeline and (N == 1 or os.environ.get("CGS_DP_PIPELINE_MULTI", "0") == "1")
+    # pipelined serving at every N: the job broadcast travels on the Gloo control group, so the image
+    # gather (side stream) is the only RCCL collective in the loop (dp.run_many docstring)
     if args.pipeline and args.warmup:
         jobs = (Job(**{**job.__dict__, "seed": 1000 + i}) for i in range(args.warmup))
         with torch.inference_mode():
@@ -183,8 +181,32 @@ def _spawn_ranks(n: int) -> int:
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    return max((abs(rc) for rc in rcs), default=0)
+    return _watch(procs)
+
+
+def _watch(procs, poll_s: float = 0.2, grace_s: float = 10.0) -> int:
+    """Wait for every rank; on the FIRST non-zero exit terminate the survivors (they would otherwise
+    block in a collective until the communicator timeout) and return that exit code."""
+    import time as _t
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = _t.time() + grace_s
+            for p in procs:
+                while p.poll() is None and _t.time() < deadline:
+                    _t.sleep(0.05)
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+            print(f"bench.py: rank exited with {bad[0]}; stopped the other ranks", file=sys.stderr, flush=True)
+            return abs(bad[0]) or 1
+        if all(rc == 0 for rc in rcs):
+            return 0
+        _t.sleep(poll_s)
 
 
 if __name__ == "__main__":

@@ -96,6 +96,8 @@ class PromptServer:
         self._last_node_id = None
         self.output_map = OutputMap(self)
         self.metrics = {"prompts_total": 0, "prompts_failed": 0, "images_total": 0, "execution_seconds_total": 0.0}
+        self.interrupt_hooks = []
+        self.cluster = None
         middlewares = [cache_control]
         if enable_cors_header:
             middlewares.append(create_cors_middleware(enable_cors_header))
@@ -450,6 +452,8 @@ class PromptServer:
         @routes.post("/interrupt")
         async def post_interrupt(request):
             dm.interrupt_current_processing()
+            for h in self.interrupt_hooks:         # multi-rank serving: forward to busy ranks
+                h()
             return web.Response(status=200)
 
         @routes.post("/free")

@@ -56,6 +56,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--auto-launch", action="store_true")
     p.add_argument("--disable-auto-launch", action="store_true")
     p.add_argument("--cuda-device", type=int, default=None, metavar="DEVICE_ID")
+    p.add_argument("--gpus", type=int, default=1, metavar="N",
+                   help="serve one API from N GPU ranks (rank 0: server + coordinator; sched/cluster.py)")
     cm = p.add_mutually_exclusive_group()
     cm.add_argument("--cuda-malloc", action="store_true")
     cm.add_argument("--disable-cuda-malloc", action="store_true")

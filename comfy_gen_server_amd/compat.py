@@ -125,7 +125,10 @@ class _Facade(types.ModuleType):
             raise AttributeError(attr)
         extra = self.__dict__["_extra"]
         if extra is None:
-            extra = self.__dict__["_extra"] = _extras(self)
+            from . import compat_names
+            extra = dict(compat_names.extra_names(self.__name__))
+            extra.update(_extras(self))
+            self.__dict__["_extra"] = extra
         if attr in extra:
             return extra[attr]
         for src in self.__dict__["_sources"]:
@@ -171,7 +174,10 @@ class _Loader(importlib.abc.Loader):
     def create_module(self, spec):
         name = spec.name
         if name in DIRECT:
-            return importlib.import_module(f"{_PKG}.{DIRECT[name]}")
+            mod = importlib.import_module(f"{_PKG}.{DIRECT[name]}")
+            from . import compat_names
+            compat_names.inject(name, mod)     # reference-named extras on our module itself
+            return mod
         if name in FACADES:
             return _Facade(name, FACADES[name])
         if name.startswith("comfy_extras.nodes_"):

@@ -577,6 +577,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   ppk::run<GG, LN, DenseA32, F32>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m, sp);
 }
 
+// Timing-probe bits of the v7 loop (ppk::run): CGS_V7_SPLIT_DBG at first use, cgs_v7_set_dbg() after.
+static int g_v7_dbg = -1;
+static int v7_dbg() {
+  if (g_v7_dbg < 0) g_v7_dbg = getenv("CGS_V7_SPLIT_DBG") ? atoi(getenv("CGS_V7_SPLIT_DBG")) : 0;
+  return g_v7_dbg;
+}
+CGS_EXPORT void cgs_v7_set_dbg(int d) { g_v7_dbg = d; }
+
 // ws (may be null): split-K tail workspace of >= cgs_v7_ws_bytes(M, N, K) bytes; without it the
 // tail round runs whole tiles.
 static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
@@ -600,7 +608,7 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
   const int tiles_n = (N + ppk::BN - 1) / ppk::BN;
   const int tiles_m = (M + ppk::BM - 1) / ppk::BM;
   const long long T = (long long)tiles_m * tiles_n;
-  ppk::Split sp{0, 1, nullptr, nullptr, 0};
+  ppk::Split sp{0, 1, nullptr, nullptr, v7_dbg()};
   long long U = T;
   if (ws && ws_bytes >= ppk::split_ws_bytes(T, K / ppk::BK, num_cus())) {
     sp.S = ppk::split_plan(T, K / ppk::BK, num_cus(), sp.t_full);
@@ -608,9 +616,7 @@ static int gemm_v7_launch(const void* A, const void* W, void* C, const void* bia
       const long long tail = T - sp.t_full;
       sp.part = (float4*)ws;
       sp.cnt = (int*)((char*)ws + tail * sp.S * 32ll * ppk::THREADS * 16);
-      static const int dbg = getenv("CGS_V7_SPLIT_DBG") ? atoi(getenv("CGS_V7_SPLIT_DBG")) : 0;
-      sp.dbg = dbg;
-      if (!(dbg & 2)) {
+      if (!(sp.dbg & 2)) {
         ppk::zero_counters_kernel<<<1, 256, 0, stream>>>(sp.cnt, (int)tail);
         hipError_t err = hipGetLastError();
         if (err != hipSuccess) return (int)err;

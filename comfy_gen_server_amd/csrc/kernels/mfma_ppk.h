@@ -20,6 +20,13 @@
 //     large as the operand reads). Straight from registers (the LDS keeps prefetching), bias from
 //     scalar loads (no vmcnt drain of the in-flight DMAs), GEGLU pairs in-lane, residual via 16-B
 //     loads;
+//   * output stores leave in full 128-B lines: one dwordx4 store instruction = 8 rows x 128 B (the
+//     MFMA layout gives a lane 16 B of 16 different rows per instruction = 16 half lines). The
+//     accumulators pass through the 32 KiB LDS staging area (wave-local for plain outputs; for GEGLU,
+//     whose wave slice is only 64 B wide, the two waves of a column pair exchange halves behind a
+//     barrier). Measured on MI355X (tools/probes/store_probe.hip): one CU writes a 128 KiB tile at
+//     99 GB/s this way vs 35 GB/s with half lines; with every CU storing at once both meet the
+//     chip's ~5.7 TB/s write limit, which is why the workgroups are also de-synchronised;
 //   * the epilogue's stores sit in the vmcnt order between two DMA stages: the waits of the next
 //     K-tile allow STORES more outstanding ops (a full tile issues every store; a partial tile keeps
 //     the plain counts, which over-wait and are therefore safe);
@@ -44,7 +51,10 @@ using pp::BK;
 using pp::THREADS;
 using pp::PART;
 using pp::BUF;
-using pp::LDS;
+// LDS: the two 64 KiB operand buffers + a 32 KiB epilogue staging area (row-major transposes so the
+// output leaves in full 128-B lines, below) = all 160 KiB of the CU
+constexpr int STG = 32768;
+constexpr int LDS = pp::LDS + STG;
 using pp::P_A0;
 using pp::P_A1;
 using pp::P_B0;
@@ -109,6 +119,15 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   const int G = gridDim.x;
   const int u0 = xcd_remap(blockIdx.x, G);
   if (u0 >= U) return;
+  // timing probes (CGS_V7_SPLIT_DBG / cgs_v7_set_dbg): bit 8 = no epilogue stores, bit 32 = round-2
+  // half-line stores; bits 8.. = start delay unit D:
+  // workgroup b waits (b & 1) x D (bit 16 clear) or (b & 3) x D (bit 16 set) x 8128 cycles
+  const bool nostore = (sp.dbg & 8) != 0;
+  const bool legacy = (sp.dbg & 32) != 0;     // probe: half-line register stores (round-2 epilogue)
+  if (sp.dbg >> 8) {
+    const int steps = ((sp.dbg & 16) ? (blockIdx.x & 3) : (blockIdx.x & 1)) * (sp.dbg >> 8);
+    for (int i = 0; i < steps; ++i) __builtin_amdgcn_s_sleep(127);
+  }
 
   // unit -> (tile origin, K range, partial slot or -1)
   auto unit = [&](int u, int& m0, int& n0, int& kb, int& ke, int& slot) {
@@ -293,6 +312,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
     }
     if constexpr (GG) {
+     if (legacy) {
       const int Nout = N >> 1;
       const int ocol = (n0 >> 1) + wc * 32 + 8 * fq;   // 8 output columns of this lane
 #pragma unroll
@@ -311,8 +331,51 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             const f32x2_t o23 = (f32x2_t{a[2], a[3]} * e.alpha + f32x2_t{ba.z, ba.w}) * g23;
             h[nq] = pack4_bf16(o01.x, o01.y, o23.x, o23.y);
           }
-          if (row < M && ocol < Nout) store16(e.C + (long long)row * e.ldc + ocol, h[0], h[1], e.flags);
+          if (row < M && ocol < Nout && !nostore) store16(e.C + (long long)row * e.ldc + ocol, h[0], h[1], e.flags);
         }
+     } else {
+      // The wave's output slice is 128 rows x 32 columns (64 B). Waves wc = 2p, 2p + 1 (same group,
+      // so the group's barriers order their exchange) own adjacent 64-B halves of the same rows:
+      // per 64-row round both write their halves into the pair's 8 KiB region ([64 rows][128 B], 16-B
+      // chunk c of row r at c ^ (r & 7)), then each stores 32 whole rows.
+      const int Nout = N >> 1;
+      unsigned char* reg = smem + pp::LDS + (wr * 2 + (wc >> 1)) * 8192;
+      const int half = wc & 1;
+      const int gcol = (n0 >> 1) + (wc >> 1) * 64 + 8 * (lane & 7);
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq) {
+        if (mq) {
+          pp::wait_lgkm0();
+          pp::barrier();           // WAR: the pair read round 0 before round 1 overwrites it
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint2 h[2];
+#pragma unroll
+          for (int nq = 0; nq < 2; ++nq) {
+            const f32x4 a = acc[mq * 4 + i][nq * 2 + 0], g = acc[mq * 4 + i][nq * 2 + 1];
+            const float4 ba = bv[nq][0], bg = bv[nq][1];
+            const f32x2_t g01 = gelu_fast2(f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y});
+            const f32x2_t g23 = gelu_fast2(f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w});
+            const f32x2_t o01 = (f32x2_t{a[0], a[1]} * e.alpha + f32x2_t{ba.x, ba.y}) * g01;
+            const f32x2_t o23 = (f32x2_t{a[2], a[3]} * e.alpha + f32x2_t{ba.z, ba.w}) * g23;
+            h[nq] = pack4_bf16(o01.x, o01.y, o23.x, o23.y);
+          }
+          const int r = 16 * i + fr;
+          *reinterpret_cast<u32x4_t*>(reg + r * 128 + 16 * ((half * 4 + fq) ^ (r & 7))) =
+              u32x4_t{h[0].x, h[0].y, h[1].x, h[1].y};
+        }
+        pp::wait_lgkm0();
+        pp::barrier();             // RAW: the partner's half is in the region
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int r = half * 32 + 8 * t + (lane >> 3);
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(reg + r * 128 + 16 * ((lane & 7) ^ (r & 7)));
+          const int row = m0 + wr * 128 + mq * 64 + r;
+          if (row < M && gcol < Nout && !nostore) *reinterpret_cast<u32x4_t*>(e.C + (long long)row * e.ldc + gcol) = v;
+        }
+      }
+     }
     } else if constexpr (F32 && !HR) {
       // fp32 output (materialised attention scores): two 16-B stores per (row, nq) -- 32 per lane
       // per tile, so the caller keeps the plain vmcnt windows (stores_pending stays false)
@@ -337,8 +400,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             }
           }
         }
-    } else {
-      // residual words: all 16 loads issued before the first store (one wait, one drain)
+    } else if (legacy) {
       uint4 rw[2][4][2];
       if constexpr (HR) {
 #pragma unroll
@@ -377,8 +439,67 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
               h[j] = pack4_bf16(v0, v1, v2, v3);
             }
             const int col = ncw + nq * 32 + 8 * fq;
-            if (row < M && col < N) store16(e.C + (long long)row * e.ldc + col, h[0], h[1], e.flags);
+            if (row < M && col < N && !nostore) store16(e.C + (long long)row * e.ldc + col, h[0], h[1], e.flags);
           }
+        }
+    } else {
+      // The wave's slice is 128 rows x 64 columns = 128-B rows: per 16-row block i, the lane's two
+      // 16-B chunks (nq = 0, 1) of row fr go to the wave's 2 KiB staging block ([16 rows][128 B], chunk
+      // c of row r at c ^ (r & 7): conflict-free b128 writes and reads), then come back as two full
+      // 8-row x 128-B store instructions (lane -> row lane >> 3, chunk lane & 7). The residual is read
+      // in that output layout (16 loads issued before the first store) and added to the rounded
+      // GEMM output in fp32 -- the reference's bf16 linear + bf16 residual add.
+      unsigned char* stg = smem + pp::LDS + wave * 2048;
+      const int sr = lane >> 3, sc = lane & 7;
+      const int gcol = ncw + 8 * sc;
+      uint4 rw[2][4][2];
+      if constexpr (HR) {
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              int row = m0 + wr * 128 + mq * 64 + 16 * i + 8 * hh + sr;
+              row = row < M ? row : M - 1;
+              const int col = gcol < N ? gcol : N - 8;
+              rw[mq][i][hh] = *reinterpret_cast<const uint4*>(e.R + (long long)row * e.ldr + col);
+            }
+      }
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int nq = 0; nq < 2; ++nq) {
+            uint2 h[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f32x4 v = acc[mq * 4 + i][nq * 2 + j];
+              const float4 b = bv[nq][j];
+              h[j] = pack4_bf16(v[0] * e.alpha + b.x, v[1] * e.alpha + b.y, v[2] * e.alpha + b.z,
+                                v[3] * e.alpha + b.w);
+            }
+            *reinterpret_cast<u32x4_t*>(stg + fr * 128 + 16 * ((nq * 4 + fq) ^ (fr & 7))) =
+                u32x4_t{h[0].x, h[0].y, h[1].x, h[1].y};
+          }
+          asm volatile("" ::: "memory");     // the wave's chunk writes precede its row reads (LDS in order)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int r = 8 * hh + sr;
+            u32x4_t v = *reinterpret_cast<const u32x4_t*>(stg + r * 128 + 16 * (sc ^ (r & 7)));
+            if constexpr (HR) {
+              const uint4 rq = rw[mq][i][hh];
+              const float4 a0 = unpack4_bf16(uint2{v[0], v[1]}), a1 = unpack4_bf16(uint2{v[2], v[3]});
+              const float4 r0 = unpack4_bf16(uint2{rq.x, rq.y}), r1 = unpack4_bf16(uint2{rq.z, rq.w});
+              const uint2 p0 = pack4_bf16(a0.x + r0.x, a0.y + r0.y, a0.z + r0.z, a0.w + r0.w);
+              const uint2 p1 = pack4_bf16(a1.x + r1.x, a1.y + r1.y, a1.z + r1.z, a1.w + r1.w);
+              v = u32x4_t{p0.x, p0.y, p1.x, p1.y};
+            }
+            const int row = m0 + wr * 128 + mq * 64 + 16 * i + r;
+            if (row < M && gcol < N && !nostore) *reinterpret_cast<u32x4_t*>(e.C + (long long)row * e.ldc + gcol) = v;
+          }
+          asm volatile("" ::: "memory");     // this block's reads precede the next block's writes
         }
     }
   };
@@ -399,7 +520,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       else epilogue_t(m0, n0, F{}, F{});
     }
   };
-  __shared__ int last_flag;
+  int& last_flag = *reinterpret_cast<int*>(smem + pp::LDS);   // staging area is idle in the split epilogue
   // split unit: publish the fp32 partial; the tile's last arriver reduces and runs the epilogue
   auto split_epilogue = [&](int m0, int n0, int slot) {
     float4* mine = sp.part + (size_t)slot * (32 * THREADS);
@@ -428,7 +549,9 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
     }
     __syncthreads();
-    if (!last_flag) return;
+    const bool last = last_flag;
+    __syncthreads();               // every wave has read the flag before the epilogue reuses its LDS word
+    if (!last) return;
     const int r0 = tile * S;
     for (int r = 0; r < S; ++r) {
       if (r0 + r == slot || (sp.dbg & 4)) continue;

@@ -161,8 +161,9 @@ class _NullServer:
 
 
 class PromptExecutor:
-    def __init__(self, server=None):
+    def __init__(self, server=None, node_hook=None):
         self.server = server or _NullServer()
+        self.node_hook = node_hook      # sched.spmd.SPMD for batch-sharded multi-rank prompts
         self.reset()
 
     def reset(self):
@@ -203,9 +204,16 @@ class PromptExecutor:
                 obj = class_def()
                 self.object_storage[(unique_id, class_type)] = obj
             t0 = time.perf_counter()
+            hook = self.node_hook
+            run_inputs = input_data_all if hook is None else hook.before(class_type, class_def, input_data_all)
             with telemetry.span(f"node:{class_type}:{unique_id}"):
                 telemetry.maybe_fault("node", class_type)
-                output_data, output_ui = get_output_data(obj, input_data_all)
+                if run_inputs is None:          # SPMD: output node, runs on rank 0 only
+                    output_data, output_ui = [], {}
+                else:
+                    output_data, output_ui = get_output_data(obj, run_inputs)
+                    if hook is not None:
+                        output_data = hook.after(class_type, run_inputs, output_data)
             dt = time.perf_counter() - t0
             self.node_timings[unique_id] = (class_type, dt)
             telemetry.record_node(class_type, dt)

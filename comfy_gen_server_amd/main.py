@@ -6,8 +6,9 @@ sentinel, ``/free`` flags, periodic model cleanup + GC at most every 10 s), ``hi
 (progress events + binary preview frames + interrupt check on every sampler tick), temp cleanup,
 and the asyncio loop running the server and its publish loop.
 
-MI355X specifics: one server process per GPU (``--cuda-device`` / LOCAL_RANK picks it; put a load
-balancer in front for a whole node, or use ``parallel.dp`` for one job split over the node), the
+MI355X specifics: ``--gpus N`` serves the whole node from one API (``sched/cluster.py``: rank 0 runs the
+server and a coordinator; independent prompts go to idle ranks, a prompt's image batch is split over
+all ranks), or one server process per GPU (``--cuda-device`` / LOCAL_RANK) behind a balancer; the
 per-shape kernel autotuner (``--no-autotune``, ``--tune-file``) and the HBM residency budget.
 
 Run: ``python -m comfy_gen_server_amd.main --listen 0.0.0.0 --port 8188`` (or ``python main.py``).
@@ -45,6 +46,9 @@ def apply_args(args):
     from .runtime import device as dm
     from .utils import folder_paths
 
+    if os.environ.get("CGS_REGISTER_TINY") == "1":     # tests: the tiny synthetic family's checkpoints load
+        from .tools.synth import register_tiny_family
+        register_tiny_family()
     if args.cpu:
         dm.set_cpu_mode(True)
     elif args.cuda_device is not None:
@@ -172,9 +176,41 @@ def build_server(args, loop):
     return server, q
 
 
+def _cluster_start(args, argv):
+    """``--gpus N``: rank 0 starts ranks 1..N-1 (same flags) before any device use, then every rank
+    joins the process group (RCCL + Gloo control; Gloo only with ``--cpu``)."""
+    from .sched import cluster
+    role = os.environ.get("CGS_SCHED_ROLE", "coordinator")
+    listener = procs = None
+    if role != "worker":
+        import sys as _sys
+        listener, procs = cluster.launch(args.gpus, list(argv) if argv is not None else _sys.argv[1:])
+    from .parallel.comm import init_from_env
+    comm = init_from_env(backend="gloo" if args.cpu else None)
+    return role, comm, listener, procs
+
+
+def _worker_rank_main(args, comm):
+    from .graph import registry
+    from .sched import cluster
+    apply_args(args)
+    registry.init_nodes(custom_nodes=not args.disable_custom_nodes,
+                        custom_dirs=list(itertools.chain.from_iterable(args.custom_nodes_directory))
+                        if args.custom_nodes_directory else None)
+    addr, key = cluster.worker_address()
+    cluster.worker_main(comm, addr, key)
+    comm.shutdown()
+    return 0
+
+
 def main(argv=None):
     cli_args.enable_args_parsing()
     args = cli_args.parse(argv)
+    cluster_state = None
+    if getattr(args, "gpus", 1) > 1:
+        cluster_state = _cluster_start(args, argv)
+        if cluster_state[0] == "worker":
+            return _worker_rank_main(args, cluster_state[1])
     from .runtime import alloc_policy
     logging.info("HBM allocator: %s", alloc_policy.configure(args))   # before any device allocation
     from .graph import registry
@@ -186,7 +222,16 @@ def main(argv=None):
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
     server, q = build_server(args, loop)
-    threading.Thread(target=prompt_worker, daemon=True, args=(q, server)).start()
+    coord = None
+    if cluster_state is not None:
+        from .sched.cluster import Coordinator
+        _, comm, listener, procs = cluster_state
+        coord = Coordinator(q, server, comm, listener)
+        server.cluster = coord
+        threading.Thread(target=coord.run_forever, daemon=True).start()
+        logging.info("serving on %d ranks (single prompts on idle ranks, batches split across all)", comm.world)
+    else:
+        threading.Thread(target=prompt_worker, daemon=True, args=(q, server)).start()
     grpc_srv = None
     if args.grpc_port is not None:
         from .api.grpc_service import start_grpc_server
@@ -205,6 +250,13 @@ def main(argv=None):
         logging.info("Stopped server")
     if grpc_srv is not None:
         grpc_srv.stop(grace=1.0)
+    if coord is not None:
+        coord.shutdown()
+        for p in cluster_state[3] or []:
+            try:
+                p.wait(timeout=30)
+            except Exception:
+                p.kill()
     cleanup_temp()
     return 0
 

@@ -470,7 +470,8 @@ class UNetModel(nn.Module):
             hsp = _apply_control(hsp, control, "output")
             for p in patches.get("output_block_patch", []):
                 h, hsp = p(h, hsp, to)
-            if x.is_cuda and _SKIPCAT() and h.shape[1] % 64 == 0 and hsp.shape[1] % 64 == 0 and h.dtype == hsp.dtype:
+            if (x.is_cuda and _SKIPCAT() and h.shape[1] % 64 == 0 and hsp.shape[1] % 64 == 0
+                    and h.dtype == hsp.dtype == torch.bfloat16):
                 h = SkipCat(h, hsp)          # consumed by the block's ResBlock without a concat
             else:
                 h = torch.cat([h, hsp], dim=1)

@@ -673,20 +673,26 @@ class SetLatentNoiseMask:
 # ================================================================ sampling
 def common_ksampler(model, seed, steps, cfg, sampler_name, scheduler, positive, negative, latent, denoise=1.0,
                     disable_noise=False, start_step=None, last_step=None, force_full_denoise=False):
-    latent_image = latent["samples"]
+    """``nodes.py:1420-1439``. In an SPMD prompt (``sched/spmd.py``) this rank samples only its slice
+    of the batch; noise is keyed by the images' global batch indices, so the shards together equal
+    the one-GPU batch."""
+    from ..sched import spmd
+    local, batch_inds, shard = spmd.shard_latent(latent)
+    latent_image = local["samples"]
     if disable_noise:
         noise = torch.zeros(latent_image.size(), dtype=torch.float32, layout=latent_image.layout, device="cpu")
     else:
-        batch_inds = latent.get("batch_index")
         noise = S.prepare_noise(latent_image, seed, batch_inds)
-    noise_mask = latent.get("noise_mask")
+    noise_mask = local.get("noise_mask")
     callback = NH.prepare_callback(model, steps)
     samples = S.sample(model, noise, steps, cfg, sampler_name, scheduler, positive, negative, latent_image,
                        denoise=denoise, disable_noise=disable_noise, start_step=start_step, last_step=last_step,
                        force_full_denoise=force_full_denoise, noise_mask=noise_mask, callback=callback, seed=seed,
-                       noise_inds=latent.get("batch_index"))
+                       noise_inds=batch_inds)
     out = latent.copy()
     out["samples"] = samples
+    if shard is not None:
+        out["dp_shard"] = shard
     return (out,)
 
 
@@ -1179,6 +1185,30 @@ class SaveImage:
         names = save_png_batch(images, full_output_folder, filename, counter, metadata, self.compress_level)
         results = [{"filename": n, "subfolder": subfolder, "type": self.type} for n in names]
         return {"ui": {"images": results}}
+
+
+def save_image_to_respective_path(prefix_append, output_dir, images, filename_prefix, prompt, extra_pnginfo,
+                                  compress_level, type, results):
+    """Save ``images`` as PNGs under ``output_dir`` and append their ``{filename, subfolder, type}``
+    records to ``results`` (the reference's shared SaveImage body, ``nodes.py:1630``; ``%batch_num%``
+    in the prefix is replaced per image)."""
+    from ..utils.imageio import save_png_batch
+    filename_prefix += prefix_append
+    full_output_folder, filename, counter, subfolder, filename_prefix = folder_paths.get_save_image_path(
+        filename_prefix, output_dir, images[0].shape[1], images[0].shape[0])
+    metadata = None
+    if not NH.args_disable_metadata():
+        metadata = {}
+        if prompt is not None:
+            metadata["prompt"] = json.dumps(prompt)
+        if extra_pnginfo is not None:
+            for x in extra_pnginfo:
+                metadata[x] = json.dumps(extra_pnginfo[x])
+    for b in range(images.shape[0]):
+        name = filename.replace("%batch_num%", str(b))
+        names = save_png_batch(images[b:b + 1], full_output_folder, name, counter, metadata, compress_level)
+        results.extend({"filename": n, "subfolder": subfolder, "type": type} for n in names)
+    return results
 
 
 class PreviewImage(SaveImage):

@@ -605,13 +605,16 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
         padding = padding[0]
     be = backend_for("conv", x, "cgs_conv2d_nhwc")
     Cout, Cin_g, kh, kw = weight.shape
-    dual_ok = x2 is None or (x.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0 and x2.dtype == x.dtype
+    cin_total = x.shape[1] + (0 if x2 is None else x2.shape[1])
+    hip_ok = (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
+              and x.dim() == 4 and cin_total % 32 == 0 and (Cout % 8 == 0 or Cout <= 16 or cin_total % 64 == 0))
+    dual_ok = x2 is None or (hip_ok and x.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0 and x2.dtype == x.dtype
                              and not upsample2x and Cout % 8 == 0)
-    if x2 is not None and (be != "hip" or not dual_ok):
-        x = torch.cat([x, x2], dim=1)
+    if x2 is not None and not dual_ok:
+        # every path other than the dual-source HIP loader convolves the materialised concat
+        x = torch.cat([x, x2.to(x.dtype)], dim=1)
         x2 = None
-    if (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
-            and x.dim() == 4 and x.shape[1] % 32 == 0 and (Cout % 8 == 0 or Cout <= 16 or x.shape[1] % 64 == 0)):
+    if hip_ok:
         count("conv", "hip")
         N, C1, H, W = x.shape
         Cin = C1 + (0 if x2 is None else x2.shape[1])

@@ -2,8 +2,11 @@
 on ROCm), Gloo on the CPU for tests. The reference has no collective call sites (SURVEY §2.6);
 the new ones are:
 
-  R1 job broadcast      ``broadcast_object`` (workflow JSON / seeds / prompts, rank 0 -> all)
-  R2 result gather      ``all_gather_uint8`` images / latents into rank 0's output
+  R1 job broadcast      ``broadcast_object`` (workflow JSON / seeds / prompts, rank 0 -> all) -- on the
+                        Gloo CONTROL group (host memory), so the RCCL communicator only ever carries
+                        device tensors and its collectives stay in one order on one stream
+  R2 result gather      ``gather`` of uint8 images / latents to rank 0 only (``all_gather`` where every
+                        rank needs the batch, e.g. latents feeding a replicated node)
   R3 weight broadcast   ``broadcast_module`` — bucketed (256 MB default) in-place broadcast of every
                         parameter from rank 0 so only one rank reads a checkpoint from disk
   R6 control            ``barrier`` / ``heartbeat`` (all-reduce of a liveness counter)
@@ -27,6 +30,7 @@ class Comm:
         self.local_rank = 0
         self.backend = None
         self.device = torch.device("cpu")
+        self.ctrl = None      # Gloo group for host-side control traffic (None: the default group)
 
     degraded = False   # set by the DP engine after a rank failure: the process group is unusable
 
@@ -42,11 +46,25 @@ class Comm:
                 dist.barrier()
 
     def broadcast_object(self, obj, src=0):
+        """R1 over the Gloo control group: no device sync, no RCCL op on the issuing stream."""
         if not self.enabled:
             return obj
         lst = [obj if self.rank == src else None]
-        dist.broadcast_object_list(lst, src=src, device=self.device if self.backend == "nccl" else None)
+        dist.broadcast_object_list(lst, src=src, group=self.ctrl)
         return lst[0]
+
+    def send_object(self, obj, dst):
+        dist.send_object_list([obj], dst=dst, group=self.ctrl)
+
+    def recv_object(self, src=None):
+        """Receive one object (from ``src``, or from any rank); returns (obj, source rank)."""
+        lst = [None]
+        r = dist.recv_object_list(lst, src=src, group=self.ctrl)
+        return lst[0], (src if src is not None else r)
+
+    def ctrl_barrier(self):
+        if self.enabled:
+            dist.barrier(group=self.ctrl)
 
     def broadcast_tensor(self, t, src=0):
         if self.enabled:
@@ -89,11 +107,25 @@ class Comm:
         dist.all_gather_into_tensor(out, t)
         return out
 
+    def gather(self, t, dst=0):
+        """R2: ``t`` of every rank (same shape) concatenated along dim 0 on ``dst``; None elsewhere.
+        One RCCL gather: each rank's shard crosses one xGMI link once (an all-gather would ship the
+        whole batch to every rank, world-1 times the bytes)."""
+        if not self.enabled:
+            return t
+        t = t.contiguous()
+        if self.rank == dst:
+            parts = [torch.empty_like(t) for _ in range(self.world)]
+            dist.gather(t, gather_list=parts, dst=dst)
+            return torch.cat(parts)
+        dist.gather(t, dst=dst)
+        return None
+
     def all_reduce_max(self, x: float) -> float:
         if not self.enabled:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl)
         return float(t.item())
 
     def heartbeat_fault_site(self):
@@ -187,6 +219,8 @@ def init_from_env(backend=None, timeout_s=600) -> Comm:
         if c.backend == "nccl":
             kw["device_id"] = c.device
         dist.init_process_group(**kw)
+        if c.backend == "nccl":
+            c.ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
     elif dist.is_initialized():
         c.backend = dist.get_backend()
     return c

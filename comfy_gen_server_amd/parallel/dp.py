@@ -5,7 +5,7 @@ Rank 0 owns the job and broadcasts it (R1); each rank generates its slice of the
 reference's per-index noise replay (``prepare_noise`` with ``batch_index`` = the image's global
 index) for the initial latent, and the per-step ancestral/SDE noise keyed by the same global index
 (``sampling/rng.py``), so a DP run is identical to a single-GPU run of the whole batch; the decoded
-uint8 images are all-gathered (R2) so rank 0 can encode/save them.
+uint8 images are gathered to rank 0 (R2), which encodes/saves them.
 
 Everything per rank is the standard single-GPU path (CLIP -> CFGGuider/KSampler -> VAE), so the
 DP engine scales whatever the kernels deliver on one GPU.
@@ -133,10 +133,10 @@ class DataParallelGenerator:
                 return None
             return generate_local(self.patcher, self.clip, self.vae, job, 0, job.batch, decode="uint8")
         job = c.broadcast_object(job)
+        c.heartbeat_fault_site()
         offset, local = self._shard(job, c.rank)
         u8 = generate_local(self.patcher, self.clip, self.vae, job, offset, local, decode="uint8")
         if gather and c.enabled and fault_tolerant:
-            c.heartbeat_fault_site()
             rid, dead = c.liveness_round(float(os.environ.get("CGS_DP_LIVENESS_TIMEOUT", "30")))
             if dead:
                 return self._recover(job, u8, dead, rid)
@@ -145,6 +145,7 @@ class DataParallelGenerator:
         return u8
 
     def _gather_plain(self, job, u8):
+        """Shards -> rank 0 (None on the other ranks)."""
         c = self.comm
         if not c.enabled:
             return u8
@@ -153,7 +154,9 @@ class DataParallelGenerator:
         if rem:
             pad = torch.zeros((per + 1 - local,) + tuple(u8.shape[1:]), dtype=u8.dtype, device=u8.device)
             u8 = torch.cat([u8, pad])
-        allimgs = c.all_gather(u8.to(c.device))
+        allimgs = c.gather(u8.to(c.device), dst=0)
+        if allimgs is None:
+            return None
         if rem:
             keep = []
             for r in range(c.world):
@@ -172,7 +175,13 @@ class DataParallelGenerator:
         VAE's low-occupancy phases (small-spatial convs, GroupNorm reductions, the one-workgroup-
         per-CU mid attention) and the host gaps between jobs are filled with UNet work. Results come
         out one job late, in order, with the main stream made to wait for them. The liveness /
-        recovery protocol of ``run(fault_tolerant=True)`` is not used on this path."""
+        recovery protocol of ``run(fault_tolerant=True)`` is not used on this path.
+
+        Multi-rank ordering: the job broadcast goes over the Gloo control group (host), so the ONLY
+        RCCL collective inside the loop is the image gather, always issued on the side stream --
+        one communicator, one stream, the same order on every rank. Anything issued on the main
+        stream after the loop (barrier, timing reduce) follows ``_collect``'s wait on the last
+        gather's event."""
         c = self.comm
         if pipeline is None:
             pipeline = os.environ.get("CGS_DP_PIPELINE", "0") == "1"
@@ -181,6 +190,7 @@ class DataParallelGenerator:
         pending = None
         for job in jobs:
             job = c.broadcast_object(job)
+            c.heartbeat_fault_site()
             offset, local = self._shard(job, c.rank)
             if side is None:
                 u8 = generate_local(self.patcher, self.clip, self.vae, job, offset, local, decode="uint8")
@@ -206,7 +216,8 @@ class DataParallelGenerator:
     def _collect(out, done):
         cur = torch.cuda.current_stream()
         cur.wait_event(done)
-        out.record_stream(cur)
+        if out is not None and out.is_cuda:      # gloo gathers return host tensors (no stream to record)
+            out.record_stream(cur)
         return out
 
     def _recover(self, job, u8, dead, rid):

@@ -93,13 +93,15 @@ class WeightArena:
         with self.lock:
             table = self.blocks.setdefault(id(module), {})
             seen: dict[int, torch.Tensor] = {}
-            new = []
+            new = []          # (name, tensor, original data) of blocks allocated by this call
+            tied = []         # (tensor, original data) of tied weights redirected onto those blocks
             try:
                 for name, t in list(module.named_parameters(recurse=True)) + list(module.named_buffers(recurse=True)):
                     if t is None or name in table:
                         continue
                     key = t.data_ptr() if t.numel() else id(t)
                     if key in seen:                         # tied weights: one block, same view
+                        tied.append((t, t.data))
                         t.data = seen[key]
                         continue
                     nbytes = t.numel() * t.element_size()
@@ -114,6 +116,8 @@ class WeightArena:
                     table[name] = off
                     placed += nbytes
             except ArenaFull:
+                for t, orig in tied:                       # never leave a view of a freed block behind
+                    t.data = orig
                 for name, t, orig in new:
                     t.data = orig
                     self.alloc.free(table.pop(name))

@@ -239,6 +239,43 @@ class ControlNet(ControlBase):
         super().cleanup()
 
 
+class ControlLoraOps:
+    """Layer namespace whose Linear / Conv2d hold a low-rank ``up`` / ``down`` pair next to the weight
+    and apply ``weight + up @ down`` per call (``comfy/controlnet.py:207``; custom nodes build
+    Control-LoRA-style modules with it). ``ControlLora`` below merges the deltas once at load
+    instead, so the per-step forward runs the plain fused kernels."""
+
+    class Linear(torch.nn.Module):
+        def __init__(self, in_features, out_features, bias=True, device=None, dtype=None):
+            super().__init__()
+            self.in_features, self.out_features = in_features, out_features
+            self.weight = self.bias = self.up = self.down = None
+
+        def forward(self, input):
+            w = self.weight.to(input.device, input.dtype)
+            if self.up is not None:
+                w = w + torch.mm(self.up.flatten(1).float(), self.down.flatten(1).float()).reshape(w.shape).to(w.dtype)
+            b = None if self.bias is None else self.bias.to(input.device, input.dtype)
+            from .. import ops
+            return ops.linear(input, w, b)
+
+    class Conv2d(torch.nn.Module):
+        def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, groups=1,
+                     bias=True, padding_mode="zeros", device=None, dtype=None):
+            super().__init__()
+            self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, kernel_size
+            self.stride, self.padding, self.dilation, self.groups = stride, padding, dilation, groups
+            self.transposed, self.output_padding, self.padding_mode = False, 0, padding_mode
+            self.weight = self.bias = self.up = self.down = None
+
+        def forward(self, input):
+            w = self.weight.to(input.device, input.dtype)
+            if self.up is not None:
+                w = w + torch.mm(self.up.flatten(1).float(), self.down.flatten(1).float()).reshape(w.shape).to(w.dtype)
+            b = None if self.bias is None else self.bias.to(input.device, input.dtype)
+            return torch.nn.functional.conv2d(input, w, b, self.stride, self.padding, self.dilation, self.groups)
+
+
 class ControlLora(ControlNet):
     """Control-LoRA: a ControlNet whose encoder weights are the base UNet's plus low-rank deltas
     (``*.up`` / ``*.down``), with full hint block / zero convs / norms in the file."""

@@ -329,24 +329,27 @@ class InterruptProcessingException(Exception):
     pass
 
 
-_interrupt_lock = threading.RLock()
-_interrupt = False
+interrupt_processing_mutex = threading.RLock()
+interrupt_processing = False
 
 
 def interrupt_current_processing(value=True):
-    global _interrupt
-    with _interrupt_lock:
-        _interrupt = value
+    global interrupt_processing
+    with interrupt_processing_mutex:
+        interrupt_processing = value
 
 
 def processing_interrupted():
-    with _interrupt_lock:
-        return _interrupt
+    with interrupt_processing_mutex:
+        return interrupt_processing
 
 
 def throw_exception_if_processing_interrupted():
-    global _interrupt
-    with _interrupt_lock:
-        if _interrupt:
-            _interrupt = False
+    global interrupt_processing
+    from ..sched import spmd
+    if spmd.active() is not None:      # SPMD prompts stop only where every rank agrees (spmd.SPMD.before)
+        return
+    with interrupt_processing_mutex:
+        if interrupt_processing:
+            interrupt_processing = False
             raise InterruptProcessingException()

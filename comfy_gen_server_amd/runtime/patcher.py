@@ -52,13 +52,13 @@ def _f(t, like):
     return None if t is None else t.to(device=like.device, dtype=torch.float32)
 
 
-def calculate_weight(patches, weight, key):
+def calculate_weight(patches, weight, key, base_dtype=None):
     """Apply a list of (strength_patch, value, strength_model) to an fp32 ``weight``."""
     for strength, v, strength_model in patches:
         if strength_model != 1.0:
             weight = weight * strength_model
         if isinstance(v, list):
-            v = (calculate_weight(v[1:], v[0].clone(), key),)
+            v = (calculate_weight(v[1:], v[0].clone(), key, base_dtype),)
         if len(v) == 1:
             kind, v = "diff", v
         else:
@@ -79,7 +79,8 @@ def calculate_weight(patches, weight, key):
                 shp = [down.shape[1], down.shape[0], mid.shape[2], mid.shape[3]]
                 down = torch.mm(down.transpose(0, 1).flatten(1), mid.transpose(0, 1).flatten(1)).reshape(shp).transpose(0, 1)
             try:
-                diff = _lora_product(up.flatten(1), down.flatten(1)).reshape(weight.shape)
+                diff = _lora_product(up.flatten(1), down.flatten(1),
+                                     bf16_ok=base_dtype == torch.bfloat16).reshape(weight.shape)
             except RuntimeError as e:
                 logging.error("ERROR %s %s %s", kind, key, e)
                 continue
@@ -131,11 +132,13 @@ def calculate_weight(patches, weight, key):
     return weight
 
 
-def _lora_product(up: torch.Tensor, down: torch.Tensor) -> torch.Tensor:
-    """up [O, r] @ down [r, I] (K20). On the GPU: the HIP MFMA GEMM (bf16 factors, fp32 accumulate,
-    one bf16 rounding of the rank-r product, which is then added to the fp32 weight); everywhere else,
-    and for ranks the GEMM does not tile (r % 8), fp32 ``torch.mm`` like the reference."""
-    if up.is_cuda and up.shape[1] % 8 == 0 and up.shape[1] == down.shape[0] and os.environ.get("CGS_LORA_HIP", "1") != "0":
+def _lora_product(up: torch.Tensor, down: torch.Tensor, bf16_ok: bool = False) -> torch.Tensor:
+    """up [O, r] @ down [r, I] (K20). For a bf16 base weight on the GPU: the HIP MFMA GEMM (bf16
+    factors, fp32 accumulate, one bf16 rounding of the rank-r product -- below the bf16 rounding of the
+    merged weight itself). fp16 / fp32 base weights, CPU tensors and ranks the GEMM does not tile
+    (r % 8): fp32 ``torch.mm`` like the reference (``comfy/model_patcher.py:370``)."""
+    if bf16_ok and up.is_cuda and up.shape[1] % 8 == 0 and up.shape[1] == down.shape[0] \
+            and os.environ.get("CGS_LORA_HIP", "1") != "0":
         from .. import ops
         return ops.linear(up.to(torch.bfloat16), down.t().contiguous().to(torch.bfloat16)).float()
     return torch.mm(up, down)
@@ -332,7 +335,7 @@ class ModelPatcher:
             self.backup[key] = w.data.clone() if device_to is None else w.data.to(device_to, copy=True)
         base = self.backup[key]
         dev = device_to if device_to is not None else base.device
-        out = calculate_weight(self.patches[key], base.to(dev, torch.float32, copy=True), key)
+        out = calculate_weight(self.patches[key], base.to(dev, torch.float32, copy=True), key, base.dtype)
         if _in_arena(w) and out.shape == w.shape:
             w.data.copy_(out.to(base.dtype))         # patched weight stays in its arena block
         else:
@@ -347,7 +350,11 @@ class ModelPatcher:
             from . import arena
             wa = arena.get(device_to)
             if wa is not None:
-                wa.place_module(self.model)          # weights into the HBM slab (C27)
+                try:
+                    wa.place_module(self.model)      # weights into the HBM slab (C27)
+                except arena.ArenaFull as e:         # does not fit: plain caching-allocator residency
+                    logging.warning("weight arena: %s; loading %s with the caching allocator",
+                                    e, type(self.model).__name__)
                 self.model.to(device_to)             # (anything the arena does not hold)
             else:
                 self.model.to(device_to)

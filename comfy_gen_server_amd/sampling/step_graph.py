@@ -120,7 +120,7 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     guider, lists, use_uncond, index0, mo, ctrl = el
     s = [float(v) for v in sigmas.detach().cpu()]
     n = len(s) - 1
-    if n < 1 or n > CAPACITY:
+    if n < 1 or n >= CAPACITY:      # meta[0] counts up to n: keep every read inside the table
         return None
     cond = _conditioning(guider, lists, x, s[0])
     # device tensors, or host scalars that are constant over the run (SVD's num_video_frames): those are
@@ -214,10 +214,11 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
             dst.copy_(src)
     stats["jobs"] += 1
     for i in range(n):
+        x_pre = plan.x.clone() if callback is not None else None   # the eager loops report x before the update
         plan.graphs[patterns[i]].replay()
         stats["replay"] += 1
         if callback is not None:
-            callback({"x": plan.x.clone(), "i": i, "sigma": s[i], "sigma_hat": s[i], "denoised": plan.den.clone()})
+            callback({"x": x_pre, "i": i, "sigma": s[i], "sigma_hat": s[i], "denoised": plan.den.clone()})
     return plan.x.clone()
 
 
@@ -287,6 +288,7 @@ def _capture(p, model, chain, pattern, rep_sigma, use_uncond, cfg, mo):
     g = torch.cuda.CUDAGraph()
     tok = current_sigma.set(float(rep_sigma))
     saved_x, saved_meta = p.x.clone(), p.meta.clone()
+    p.meta[0] = 0                   # a previous job left meta[0] = its step count: warm-up reads row 0
     try:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())

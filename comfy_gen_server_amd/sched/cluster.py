@@ -1,0 +1,420 @@
+"""Rank-0 front end + per-GPU workers: one ``/prompt`` API for the whole node.
+
+The reference serves a prompt on one process and one GPU (``main.py:93-146`` worker thread ->
+``execution.py:526``). Here ``python -m comfy_gen_server_amd.main --gpus N`` starts N ranks (one process
+per GPU, ``torch.distributed`` over RCCL/xGMI for tensors, Gloo for host control). Rank 0 runs the
+HTTP/WS server, the prompt queue and this ``Coordinator``; ranks 1..N-1 run ``worker_main``.
+
+Per queued prompt the coordinator picks a mode (``choose_mode``):
+
+* ``spmd`` -- the prompt's latent batch is at least the number of live ranks: every rank executes the
+  graph, the samplers and decoders split the batch by global image index (``spmd.py``), rank 0 writes
+  the outputs. A batch-64 prompt uses the whole node;
+* ``single`` -- the prompt runs whole on ONE idle rank (rank 0 included). Independent prompts run
+  concurrently on different GPUs, so N small prompts keep N GPUs busy.
+
+Transport: JSON messages over ``multiprocessing.connection`` (authenticated local socket) -- run
+requests and interrupts down, WS events and completions up. Rank 0 forwards a worker's events to the
+submitting client (``sid``); binary preview frames of remote ranks are not forwarded.
+
+Ranks keep two executors each: one sees only SPMD prompts (identical caches on every rank, so every
+rank reaches the same collectives), one serves single prompts (its own cross-prompt cache). A worker
+whose connection drops is marked dead: its running prompt is reported failed, SPMD stops being used.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import queue
+import secrets
+import socket
+import subprocess
+import sys
+import threading
+import time
+from multiprocessing.connection import Client, Listener
+
+SAMPLER_TYPES = ("KSampler", "KSamplerAdvanced")
+
+
+def _default(o):
+    try:
+        import torch
+        if torch.is_tensor(o):
+            return o.tolist() if o.numel() <= 64 else f"tensor{tuple(o.shape)}"
+    except Exception:  # pragma: no cover
+        pass
+    return str(o)
+
+
+def send_msg(conn, obj, lock=None):
+    data = json.dumps(obj, default=_default).encode()
+    if lock is None:
+        conn.send_bytes(data)
+    else:
+        with lock:
+            conn.send_bytes(data)
+
+
+def recv_msg(conn):
+    return json.loads(conn.recv_bytes().decode())
+
+
+def prompt_batch(prompt: dict) -> int:
+    """Largest image batch a prompt creates (latent constructors / repeats feeding its samplers)."""
+    best = 1
+    for node in prompt.values():
+        if not isinstance(node, dict):
+            continue
+        inputs = node.get("inputs", {})
+        for key in ("batch_size", "amount"):
+            v = inputs.get(key)
+            if isinstance(v, int) and node.get("class_type", "").endswith(("LatentImage", "LatentBatch", "Latent")):
+                best = max(best, v)
+    return best
+
+
+def choose_mode(prompt: dict, extra_data: dict | None, world: int) -> str:
+    """``spmd`` when the batch covers every live rank and the prompt samples; else ``single``.
+    ``extra_data["dp"]`` (``"spmd"`` / ``"single"``) overrides."""
+    want = (extra_data or {}).get("dp", "auto")
+    if world <= 1:
+        return "single"
+    if want in ("spmd", "single"):
+        return want
+    has_sampler = any(isinstance(n, dict) and n.get("class_type") in SAMPLER_TYPES for n in prompt.values())
+    return "spmd" if has_sampler and prompt_batch(prompt) >= world else "single"
+
+
+# ------------------------------------------------------------------------------------------------
+# worker side
+# ------------------------------------------------------------------------------------------------
+class RemoteServer:
+    """Worker-side stand-in for ``PromptServer``: WS events go up to rank 0."""
+    output_map = None
+
+    def __init__(self, conn, lock):
+        self.conn, self.lock = conn, lock
+        self.client_id = None
+        self.last_node_id = None
+        self.last_prompt_id = None
+        self.metrics = {}
+
+    def send_sync(self, event, data, sid=None):
+        if not isinstance(event, str):        # binary preview frames stay local
+            return
+        try:
+            send_msg(self.conn, {"op": "event", "event": event, "data": data, "sid": sid}, self.lock)
+        except (OSError, EOFError):
+            pass
+
+    def queue_updated(self):
+        pass
+
+    def broadcast_yjs_updates(self):
+        pass
+
+
+def _forward_progress(server):
+    from ..runtime import device as dm
+    from ..utils import progress
+
+    def hook(value, total, preview_image):
+        dm.throw_exception_if_processing_interrupted()
+        server.send_sync("progress", {"value": value, "max": total, "prompt_id": server.last_prompt_id,
+                                      "node": server.last_node_id}, server.client_id)
+    progress.set_progress_bar_global_hook(hook)
+
+
+def worker_main(comm, address, authkey: bytes):
+    """Rank >= 1: execute what rank 0 sends until it says stop."""
+    from ..graph.executor import PromptExecutor
+    from ..runtime import device as dm
+    from . import spmd
+    conn = None
+    for _ in range(600):
+        try:
+            conn = Client(tuple(address), authkey=authkey)
+            break
+        except (ConnectionRefusedError, OSError):
+            time.sleep(0.1)
+    if conn is None:
+        raise RuntimeError(f"rank {comm.rank}: cannot reach the coordinator at {address}")
+    lock = threading.Lock()
+    send_msg(conn, {"op": "hello", "rank": comm.rank}, lock)
+    server = RemoteServer(conn, lock)
+    _forward_progress(server)
+    ctx = spmd.SPMD(comm)
+    ex_single = PromptExecutor(server)
+    ex_spmd = PromptExecutor(None, node_hook=ctx)
+    inbox: queue.Queue = queue.Queue()
+
+    def reader():
+        while True:
+            try:
+                m = recv_msg(conn)
+            except (EOFError, OSError):
+                inbox.put({"op": "stop"})
+                return
+            if m.get("op") == "interrupt":
+                dm.interrupt_current_processing(True)
+            else:
+                inbox.put(m)
+    threading.Thread(target=reader, daemon=True).start()
+    while True:
+        m = inbox.get()
+        if m.get("op") == "stop":
+            break
+        if m.get("op") != "run":
+            continue
+        pid, extra = m["prompt_id"], m.get("extra_data") or {}
+        server.last_prompt_id = pid
+        t0 = time.perf_counter()
+        n0 = ctx.images_sampled
+        if m["mode"] == "spmd":
+            with spmd.activate(ctx):
+                ex_spmd.execute(m["prompt"], pid, {}, m["outputs"])
+            ex = ex_spmd
+        else:
+            ex_single.execute(m["prompt"], pid, extra, m["outputs"])
+            ex = ex_single
+        send_msg(conn, {"op": "done", "prompt_id": pid, "rank": comm.rank, "success": ex.success,
+                        "messages": ex.status_messages, "outputs_ui": ex.outputs_ui,
+                        "seconds": time.perf_counter() - t0, "images_sampled": ctx.images_sampled - n0}, lock)
+    try:
+        conn.close()
+    except OSError:
+        pass
+
+
+# ------------------------------------------------------------------------------------------------
+# rank 0
+# ------------------------------------------------------------------------------------------------
+class Coordinator:
+    def __init__(self, q, server, comm, listener, accept_timeout_s: float = 600.0):
+        from ..graph.executor import PromptExecutor
+        from . import spmd
+        self.q, self.server, self.comm = q, server, comm
+        self.world = comm.world
+        self.conns: dict = {}
+        self.locks: dict = {}
+        self.dead: set = set()
+        self.busy: dict = {}          # rank -> prompt_id
+        self.cv = threading.Condition()
+        self.spmd_waiting: dict = {}  # prompt_id -> {rank: done message}
+        self.ran_on: dict = {}        # prompt_id -> rank(s), for /history metrics and tests
+        self.ctx = spmd.SPMD(comm)
+        self.ex_single = PromptExecutor(server)
+        self.ex_spmd = PromptExecutor(server, node_hook=self.ctx)
+        self._inflight: dict = {}     # rank -> (queue item id, prompt id) of its single prompt
+        self._sids: dict = {}         # prompt id -> submitting client (WS)
+
+        def accept_all():
+            while len(self.conns) < self.world - 1:
+                conn = listener.accept()
+                hello = recv_msg(conn)
+                r = int(hello["rank"])
+                self.conns[r], self.locks[r] = conn, threading.Lock()
+        t = threading.Thread(target=accept_all, daemon=True)
+        t.start()
+        t.join(accept_timeout_s)
+        if len(self.conns) < self.world - 1:
+            raise RuntimeError(f"only {len(self.conns)} of {self.world - 1} worker ranks connected")
+        for r, conn in self.conns.items():
+            threading.Thread(target=self._reader, args=(r, conn), daemon=True).start()
+        if hasattr(server, "interrupt_hooks"):
+            server.interrupt_hooks.append(self.interrupt_all)
+
+    # -------------------------------------------------------------- plumbing
+    def live(self):
+        return [r for r in range(self.world) if r not in self.dead]
+
+    def _reader(self, r, conn):
+        while True:
+            try:
+                m = recv_msg(conn)
+            except (EOFError, OSError):
+                self._rank_died(r)
+                return
+            op = m.get("op")
+            if op == "event":
+                self.server.send_sync(m["event"], m["data"], m.get("sid"))
+            elif op == "done":
+                with self.cv:
+                    pid = m["prompt_id"]
+                    if pid in self.spmd_waiting:
+                        self.spmd_waiting[pid][r] = m
+                    else:
+                        self._finish_single(r, m)
+                    self.cv.notify_all()
+
+    def _rank_died(self, r):
+        logging.error("rank %d left the cluster", r)
+        with self.cv:
+            self.dead.add(r)
+            pid = self.busy.pop(r, None)
+            rec = self._inflight.pop(r, None)
+            if rec is not None:
+                self._complete(rec[0], rec[1], {}, False,
+                               [("execution_error", {"prompt_id": pid, "exception_message": f"rank {r} died"})])
+            for w in self.spmd_waiting.values():
+                w.setdefault(r, {"success": False, "messages": [], "outputs_ui": {}})
+            self.cv.notify_all()
+
+    def interrupt_all(self):
+        for r in list(self.busy):
+            if r != 0 and r not in self.dead:
+                try:
+                    send_msg(self.conns[r], {"op": "interrupt"}, self.locks[r])
+                except OSError:
+                    pass
+
+    def _complete(self, item_id, prompt_id, outputs_ui, success, messages):
+        self.q.task_done(item_id, outputs_ui,
+                         status=self.q.ExecutionStatus(status_str="success" if success else "error",
+                                                       completed=success, messages=messages))
+        with self.q.mutex:                       # which rank(s) served it: /history metrics
+            h = self.q.history.get(prompt_id)
+            if h is not None:
+                h.setdefault("metrics", {})["ranks"] = self.ran_on.get(prompt_id)
+        sid = self._sids.pop(prompt_id, None)
+        if sid is not None:
+            self.server.send_sync("executing", {"node": None, "prompt_id": prompt_id}, sid)
+        m = getattr(self.server, "metrics", None)
+        if isinstance(m, dict):
+            m["prompts_total"] = m.get("prompts_total", 0) + 1
+            if not success:
+                m["prompts_failed"] = m.get("prompts_failed", 0) + 1
+
+    def _finish_single(self, r, m):
+        rec = self._inflight.pop(r, None)
+        self.busy.pop(r, None)
+        if rec is None:
+            return
+        item_id, pid = rec
+        self._complete(item_id, pid, m.get("outputs_ui") or {}, bool(m.get("success")), m.get("messages") or [])
+
+    # -------------------------------------------------------------- scheduling
+    def run_forever(self, stop_event: threading.Event | None = None):
+        while stop_event is None or not stop_event.is_set():
+            got = self.q.get(timeout=1.0)
+            if got is None:
+                continue
+            item, item_id = got
+            prompt_id, prompt, extra, outputs = item[1], item[2], item[3] or {}, item[4]
+            sid = extra.get("client_id")
+            if sid is not None:
+                self._sids[prompt_id] = sid
+            mode = choose_mode(prompt, extra, len(self.live()))
+            if mode == "spmd" and len(self.live()) == self.world:
+                self._run_spmd(item_id, prompt_id, prompt, extra, outputs)
+            else:
+                self._run_single(item_id, prompt_id, prompt, extra, outputs)
+
+    def _wait(self, pred):
+        with self.cv:
+            while not pred():
+                self.cv.wait(timeout=1.0)
+
+    def _run_single(self, item_id, prompt_id, prompt, extra, outputs):
+        self._wait(lambda: any(r not in self.busy for r in self.live()))
+        with self.cv:
+            idle = [r for r in self.live() if r not in self.busy]
+            r = max(idle)             # workers first: rank 0 also serves HTTP / WS
+            self.busy[r] = prompt_id
+            self._inflight[r] = (item_id, prompt_id)
+            self.ran_on[prompt_id] = r
+        if r == 0:
+            threading.Thread(target=self._local_single, args=(prompt_id, prompt, extra, outputs), daemon=True).start()
+        else:
+            try:
+                send_msg(self.conns[r], {"op": "run", "mode": "single", "prompt_id": prompt_id, "prompt": prompt,
+                                         "extra_data": extra, "outputs": outputs}, self.locks[r])
+            except OSError:
+                self._rank_died(r)
+
+    def _local_single(self, prompt_id, prompt, extra, outputs):
+        self.server.last_prompt_id = prompt_id
+        self.ex_single.execute(prompt, prompt_id, extra, outputs)
+        with self.cv:
+            self._finish_single(0, {"success": self.ex_single.success, "messages": self.ex_single.status_messages,
+                                    "outputs_ui": self.ex_single.outputs_ui})
+            self.cv.notify_all()
+
+    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs):
+        from . import spmd
+        self._wait(lambda: not self.busy)
+        with self.cv:
+            for r in self.live():
+                self.busy[r] = prompt_id
+            self.spmd_waiting[prompt_id] = {}
+            self.ran_on[prompt_id] = "all"
+        msg = {"op": "run", "mode": "spmd", "prompt_id": prompt_id, "prompt": prompt, "outputs": outputs}
+        for r in self.live():
+            if r != 0:
+                send_msg(self.conns[r], msg, self.locks[r])
+        self.server.last_prompt_id = prompt_id
+        n0 = self.ctx.images_sampled
+        with spmd.activate(self.ctx):
+            self.ex_spmd.execute(prompt, prompt_id, extra, outputs)
+        mine = self.ctx.images_sampled - n0
+        self._wait(lambda: all(r in self.spmd_waiting[prompt_id] for r in self.live() if r != 0)
+                   or len(self.live()) < self.world)
+        with self.cv:
+            done = self.spmd_waiting.pop(prompt_id)
+            ok = self.ex_spmd.success and all(bool(m.get("success")) for m in done.values())
+            msgs = list(self.ex_spmd.status_messages)
+            for r, m in sorted(done.items()):
+                if not m.get("success"):
+                    msgs += [(e, d) for e, d in (m.get("messages") or []) if e == "execution_error"]
+            for r in list(self.busy):
+                if self.busy[r] == prompt_id:
+                    del self.busy[r]
+            self._complete(item_id, prompt_id, self.ex_spmd.outputs_ui, ok, msgs)
+            with self.q.mutex:
+                h = self.q.history.get(prompt_id)
+                if h is not None:   # images sampled per rank (the batch split)
+                    h["metrics"]["images_per_rank"] = {0: mine, **{r: m.get("images_sampled", 0)
+                                                                   for r, m in done.items()}}
+            self.cv.notify_all()
+
+    def shutdown(self):
+        for r, conn in self.conns.items():
+            try:
+                send_msg(conn, {"op": "stop"}, self.locks[r])
+            except OSError:
+                pass
+
+
+# ------------------------------------------------------------------------------------------------
+# launcher
+# ------------------------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int, argv):
+    """Rank 0 (this process, before it touches the GPU): start ranks 1..n-1 as children running the
+    same command line, set up the rendezvous env for all of them, and return (listener, procs)."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    key = secrets.token_hex(16)
+    listener = Listener(("127.0.0.1", 0), authkey=key.encode())
+    env_common = {"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "CGS_SCHED_ADDR": json.dumps(listener.address),
+                  "CGS_SCHED_KEY": key, "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")}
+    os.environ.update(env_common)
+    os.environ.update(RANK="0", LOCAL_RANK="0")
+    procs = []
+    pkg_parent = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    pypath = os.pathsep.join(p for p in (pkg_parent, os.environ.get("PYTHONPATH", "")) if p)
+    for r in range(1, n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), CGS_SCHED_ROLE="worker", PYTHONPATH=pypath)
+        procs.append(subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main"] + list(argv), env=env))
+    return listener, procs
+
+
+def worker_address():
+    return json.loads(os.environ["CGS_SCHED_ADDR"]), os.environ["CGS_SCHED_KEY"].encode()

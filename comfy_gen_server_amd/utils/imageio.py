@@ -44,12 +44,25 @@ def encode_png(arr: np.ndarray, metadata: dict | None = None, compress_level=4) 
     return bio.getvalue()
 
 
+def _claim(folder, filename, counter):
+    """Create ``{filename}_{counter:05}_.png`` exclusively, bumping the counter past names another
+    writer (another rank / thread saving with the same prefix) took meanwhile."""
+    while True:
+        name = f"{filename}_{counter:05}_.png"
+        try:
+            os.close(os.open(os.path.join(folder, name), os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o644))
+            return name, counter
+        except FileExistsError:
+            counter += 1
+
+
 def save_png_batch(images, folder, filename, counter, metadata=None, compress_level=4):
     arrs = to_uint8_cpu(images)
     names = []
     jobs = []
     for i, arr in enumerate(arrs):
-        name = f"{filename}_{counter + i:05}_.png"
+        name, counter = _claim(folder, filename, counter)
+        counter += 1
         names.append(name)
         path = os.path.join(folder, name)
 

@@ -339,3 +339,21 @@ def test_latency_mode_matches_single_gpu(tmp_path, world, layout_batch, attn):
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, (o[-2000:], e[-3000:])
     assert all("maxdiff" in o for o, _ in outs)
+
+
+def test_bench_watchdog_stops_survivors():
+    """``bench.py --gpus 3`` (own launcher): rank 2 dies at its first job; the survivors are blocked in a
+    collective, the parent notices the non-zero exit, stops them and exits non-zero within a minute
+    (instead of hanging until the 600 s communicator timeout)."""
+    import time
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "1", "--warmup", "1", "--cpu",
+           "--family", "tiny", "--res", "64", "--sampler-steps", "2", "--batch-per-gpu", "1"]
+    env = _env()
+    env.pop("WORLD_SIZE", None)
+    env["CGS_FAULT"] = "rank_exit:2"
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "stopped the other ranks" in r.stderr, r.stderr[-3000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert time.time() - t0 < 120

@@ -1,0 +1,144 @@
+"""Node-level multi-rank serving through the prompt API (sched/cluster.py, sched/spmd.py) on the CPU:
+``main --gpus 3 --cpu`` starts rank 0 (HTTP server + coordinator) and two worker ranks over Gloo.
+
+* a batch-6 workflow runs SPMD (2 images per rank, noise keyed by global image index) and returns
+  the same images as the same prompt served whole on one rank;
+* six independent batch-1 prompts are spread over all three ranks.
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _get(url):
+    with urllib.request.urlopen(url, timeout=10) as r:
+        return json.loads(r.read())
+
+
+def _post(url, obj):
+    req = urllib.request.Request(url, data=json.dumps(obj).encode(), headers={"Content-Type": "application/json"})
+    with urllib.request.urlopen(req, timeout=30) as r:
+        return json.loads(r.read())
+
+
+def _graph(seed, batch, prefix):
+    return {
+        "4": {"class_type": "CheckpointLoaderSimple", "inputs": {"ckpt_name": "tiny.safetensors"}},
+        "5": {"class_type": "EmptyLatentImage", "inputs": {"width": 64, "height": 64, "batch_size": batch}},
+        "6": {"class_type": "CLIPTextEncode", "inputs": {"text": "a photo of a cat", "clip": ["4", 1]}},
+        "7": {"class_type": "CLIPTextEncode", "inputs": {"text": "blurry", "clip": ["4", 1]}},
+        "3": {"class_type": "KSampler", "inputs": {"seed": seed, "steps": 2, "cfg": 5.0,
+                                                  "sampler_name": "euler_ancestral", "scheduler": "normal",
+                                                  "denoise": 1.0, "model": ["4", 0], "positive": ["6", 0],
+                                                  "negative": ["7", 0], "latent_image": ["5", 0]}},
+        "8": {"class_type": "VAEDecode", "inputs": {"samples": ["3", 0], "vae": ["4", 2]}},
+        "9": {"class_type": "SaveImage", "inputs": {"filename_prefix": prefix, "images": ["8", 0]}},
+    }
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    base = tmp_path_factory.mktemp("cgs_cluster")
+    for d in ("models/checkpoints", "output", "input", "temp"):
+        os.makedirs(base / d, exist_ok=True)
+    env = dict(os.environ, CGS_FORCE_CPU="1", OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "CGS_SCHED_ROLE"):
+        env.pop(k, None)
+    subprocess.run([sys.executable, "-c",
+                    "import sys, torch; sys.path.insert(0, %r);"
+                    "from comfy_gen_server_amd.tools.synth import register_tiny_family, write_checkpoint;"
+                    "register_tiny_family(); write_checkpoint('tiny', %r, dtype=torch.float32)"
+                    % (ROOT, str(base / "models/checkpoints/tiny.safetensors"))],
+                   check=True, env=env, cwd=ROOT, timeout=300)
+    port = _free_port()
+    env["MASTER_PORT"] = str(_free_port())
+    env["CGS_REGISTER_TINY"] = "1"
+    proc = subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main", "--gpus", "3", "--cpu",
+                             "--listen", "127.0.0.1", "--port", str(port), "--base-directory", str(base),
+                             "--disable-custom-nodes", "--dont-print-server", "--preview-method", "none"],
+                            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                            start_new_session=True)
+    url = f"http://127.0.0.1:{port}"
+    deadline = time.time() + 240
+    while time.time() < deadline:
+        if proc.poll() is not None:
+            raise RuntimeError(proc.stdout.read()[-4000:])
+        try:
+            _get(url + "/queue")
+            break
+        except Exception:
+            time.sleep(0.5)
+    else:
+        os.killpg(proc.pid, signal.SIGKILL)
+        raise RuntimeError("server did not come up")
+    yield url, base
+    os.killpg(proc.pid, signal.SIGTERM)
+    try:
+        proc.wait(timeout=30)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+
+
+def _wait(url, pids, timeout=300):
+    deadline = time.time() + timeout
+    out = {}
+    while time.time() < deadline and len(out) < len(pids):
+        for p in pids:
+            if p not in out:
+                h = _get(f"{url}/history/{p}")
+                if p in h:
+                    out[p] = h[p]
+        time.sleep(0.3)
+    assert len(out) == len(pids), f"timed out: {len(out)} of {len(pids)}"
+    return out
+
+
+def _images(base, entry):
+    from PIL import Image
+    imgs = entry["outputs"]["9"]["images"]
+    return [np.asarray(Image.open(os.path.join(base, "output", i["subfolder"], i["filename"]))).astype(np.int32)
+            for i in imgs]
+
+
+def test_batch_prompt_split_over_ranks_matches_one_rank(cluster):
+    url, base = cluster
+    a = _post(url + "/prompt", {"prompt": _graph(11, 6, "spmd")})["prompt_id"]
+    b = _post(url + "/prompt", {"prompt": _graph(11, 6, "one"), "extra_data": {"dp": "single"}})["prompt_id"]
+    h = _wait(url, [a, b])
+    assert h[a]["status"]["status_str"] == "success", h[a]["status"]
+    assert h[b]["status"]["status_str"] == "success", h[b]["status"]
+    assert h[a]["metrics"]["ranks"] == "all" and isinstance(h[b]["metrics"]["ranks"], int)
+    assert h[a]["metrics"]["images_per_rank"] == {"0": 2, "1": 2, "2": 2}, h[a]["metrics"]
+    ia, ib = _images(base, h[a]), _images(base, h[b])
+    assert len(ia) == len(ib) == 6
+    for x, y in zip(ia, ib):
+        d = np.abs(x - y)
+        assert d.max() <= 2 and d.mean() < 0.25, (d.max(), d.mean())   # per-image noise: same images
+    assert np.abs(ia[0] - ia[1]).mean() > 1.0                           # and distinct per index
+
+
+def test_independent_prompts_use_every_rank(cluster):
+    url, base = cluster
+    pids = [_post(url + "/prompt", {"prompt": _graph(100 + i, 1, f"ind{i}")})["prompt_id"] for i in range(6)]
+    h = _wait(url, pids)
+    assert all(e["status"]["status_str"] == "success" for e in h.values())
+    ranks = {e["metrics"]["ranks"] for e in h.values()}
+    assert ranks == {0, 1, 2}, ranks
+    for e in h.values():
+        assert len(_images(base, e)) == 1
