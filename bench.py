@@ -39,6 +39,10 @@ def main():
                          "stream while job n+1 samples: dp.run_many); every job still completes inside the "
                          "timed region")
     ap.add_argument("--profile-ops", action="store_true", help="(kept for compatibility; op backends are always reported)")
+    ap.add_argument("--via-executor", action="store_true",
+                    help="time the product path: a text-to-image workflow JSON through validate_prompt + "
+                         "PromptExecutor (CLIPTextEncode x2 -> KSampler -> VAEDecode -> SaveImage PNGs); at N > 1 "
+                         "every rank runs it SPMD with the batch split by global image index (sched/spmd.py)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -72,6 +76,15 @@ def main():
     t0 = time.time()
     with torch.inference_mode():
         patcher, clip, vae = build_pipeline(args.family, device=dev, dtype=dtype, seed=1234)
+    arena_stats = None
+    if not args.cpu:
+        # resident weights in the per-GPU HBM slab (runtime/arena.py; on by default on MI355X)
+        from comfy_gen_server_amd.runtime import arena
+        wa = arena.get(dev)
+        if wa is not None:
+            for m in (patcher.model, clip.cond_stage_model, vae.first_stage_model):
+                wa.place_module(m)
+            arena_stats = wa.stats()
     gen = DataParallelGenerator(patcher, clip, vae)
     with torch.inference_mode():
         gen.sync_weights()
@@ -88,6 +101,9 @@ def main():
             print(f"[bench {time.time() - t0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
     log(f"built pipeline in {t_build:.1f}s")
+
+    if args.via_executor:
+        return _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log)
 
     def one_step(i):
         j = Job(**{**job.__dict__, "seed": 1000 + i})
@@ -158,13 +174,93 @@ def main():
                        "cfg": args.cfg, "unet_batch_per_gpu": 2 * args.batch_per_gpu,
                        "parallelism": f"dp{N}", "pipelined": bool(args.pipeline)},
             "build_s": round(t_build, 1),
+            "weight_arena": arena_stats,
         }
         from comfy_gen_server_amd.parallel import dp as _dp
         if _dp.STAGE_TIMES:
             res["stage_seconds"] = {k: [round(x, 3) for x in v] for k, v in _dp.STAGE_TIMES.items()}
         res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
-        from comfy_gen_server_amd.sampling import step_graph as _sg
-        res["step_graph"] = dict(_sg.stats)      # capture / replay / capture_failed counts
+        from comfy_gen_server_amd.sampling import run_graph as _rg, step_graph as _sg
+        res["step_graph"] = dict(_sg.stats)      # capture / replay / capture_failed / ineligible reasons
+        res["run_graph"] = dict(_rg.stats)
+        print(json.dumps(res), flush=True)
+    comm.shutdown()
+
+
+def _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log):
+    """--via-executor: every timed step is one workflow JSON executed by PromptExecutor (rank 0 owns the
+    prompt and broadcasts it; SPMD across ranks). The prompt text changes per step, so the CLIP
+    encodes run every step (no cross-prompt cache hit), as does the PNG encode + write of SaveImage."""
+    import tempfile
+    import torch
+    from comfy_gen_server_amd import ops
+    from comfy_gen_server_amd.graph import registry
+    from comfy_gen_server_amd.graph.executor import PromptExecutor
+    from comfy_gen_server_amd.graph.validation import validate_prompt
+    from comfy_gen_server_amd.sched import spmd
+    from comfy_gen_server_amd.tools import synth
+    from comfy_gen_server_amd.utils import folder_paths
+    registry.init_nodes(custom_nodes=False)
+    synth.register_node()
+    synth._PIPELINES[(args.family, 1234)] = (gen.patcher, gen.clip, gen.vae)   # the weights built above
+    out_dir = tempfile.mkdtemp(prefix="cgs_bench_out_")
+    folder_paths.set_output_directory(out_dir)
+    ctx = spmd.SPMD(comm) if comm.world > 1 else None
+    ex = PromptExecutor(None, node_hook=ctx)
+
+    def step(i):
+        wf = synth.text_to_image_workflow(args.family, seed=1000 + i, text=f"{job.prompt}, variation {i}",
+                                          negative=job.negative, width=args.res, height=args.res,
+                                          batch=global_batch, steps=args.sampler_steps, cfg=args.cfg,
+                                          sampler=args.sampler, save_prefix=f"bench{comm.rank}")
+        wf = comm.broadcast_object(wf)
+        ok, err, outputs, node_errors = validate_prompt(wf)
+        assert ok, (err, node_errors)
+        if ctx is not None:
+            with spmd.activate(ctx):
+                ex.execute(wf, f"bench-{i}", {}, outputs)
+        else:
+            ex.execute(wf, f"bench-{i}", {}, outputs)
+        assert ex.success, ex.status_messages[-1:]
+        if not args.cpu:
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        ts = time.perf_counter()
+        step(i)
+        log(f"warmup workflow {i}: {time.perf_counter() - ts:.2f}s")
+    comm.barrier()
+    ops.reset_stats()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    if not args.cpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    dt = comm.all_reduce_max(time.perf_counter() - t1)
+    if comm.rank == 0:
+        try:
+            with open(os.path.join(HERE, "BASELINE.json")) as f:
+                metric = json.load(f)["metric"]
+        except Exception:
+            metric = "images/sec (whole node), SDXL 1024 20-step Euler-a"
+        saved = sum(1 for f in os.listdir(out_dir) if f.endswith(".png"))
+        res = {"metric": metric, "value": round(global_batch * args.steps / dt, 4), "unit": "images/s",
+               "n_gpus": comm.world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt * 1000.0 / max(1, args.steps), 2), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if args.cpu else "bf16",
+               "data": "synthetic prompts, random-init weights (exact SDXL-base architecture)",
+               "path": "workflow JSON -> validate_prompt -> PromptExecutor (SaveImage PNGs included)",
+               "pngs_written": saved,
+               "config": {"model": f"{args.family}-base" if args.family == "sdxl" else args.family,
+                          "global_batch": global_batch, "seq_len": (args.res // 8) ** 2, "resolution": args.res,
+                          "sampler_steps": args.sampler_steps, "sampler": args.sampler, "cfg": args.cfg,
+                          "parallelism": f"dp{comm.world}"},
+               "build_s": round(t_build, 1)}
+        res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
+        from comfy_gen_server_amd.sampling import run_graph as _rg, step_graph as _sg
+        res["step_graph"] = dict(_sg.stats)
+        res["run_graph"] = dict(_rg.stats)
         print(json.dumps(res), flush=True)
     comm.shutdown()
 

@@ -123,10 +123,10 @@ KERNEL_SIGNATURES = {
     "cgs_gemm_bf16_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
     "cgs_conv2d_nhwc_v": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     # counter-based noise keyed by (seed, global image index, stream) (csrc/kernels/rng.hip, K18)
-    "cgs_philox_randn": [_P, _I, _L, ctypes.c_ulonglong, _L, ctypes.c_ulonglong, _P, _F, _I, _P],
-    "cgs_euler_ancestral_philox": [_P, _P, _I, _L, _F, _F, _F, ctypes.c_ulonglong, _L, ctypes.c_ulonglong, _P],
+    "cgs_philox_randn": [_P, _I, _L, ctypes.c_ulonglong, _L, ctypes.c_ulonglong, _P, _F, _I, _P, _P],
+    "cgs_euler_ancestral_philox": [_P, _P, _I, _L, _F, _F, _F, ctypes.c_ulonglong, _L, ctypes.c_ulonglong, _P, _P],
     "cgs_brownian_increment": [_P, _I, _L, ctypes.c_ulonglong, _L, ctypes.c_double, ctypes.c_double,
-                               ctypes.c_double, ctypes.c_double, ctypes.c_double, _I, _F, _P],
+                               ctypes.c_double, ctypes.c_double, ctypes.c_double, _I, _F, _P, _P],
     # device-parameterised sampler step (one captured graph replayed for every step; rng.hip)
     "cgs_sampler_step_dev": [_P, _P, _P, _P, _I, _L, _F, _P, _I, _P, _P],
     "cgs_step_param": [_P, _I, _P, _I, _I, _P, _P],

@@ -489,6 +489,17 @@ class PromptServer:
             lines.append(f"cgs_resident_models {len(dm.current_loaded_models)}")
             from ..utils import telemetry
             lines += telemetry.prometheus_lines()
+            # sampler-loop graph coverage: why a run was not replayed from hipGraphs
+            from ..sampling import run_graph, step_graph
+            for name, st in (("step_graph", step_graph.stats), ("run_graph", run_graph.stats)):
+                for k, v in st.items():
+                    if isinstance(v, (int, float)):
+                        lines.append(f"# TYPE cgs_{name}_{k} counter")
+                        lines.append(f"cgs_{name}_{k} {v}")
+                lines.append(f"# TYPE cgs_{name}_ineligible counter")
+                for reason, n in sorted(st.get("ineligible", {}).items()):
+                    r = reason.replace("\\", "\\\\").replace('"', "'")
+                    lines.append(f'cgs_{name}_ineligible{{reason="{r}"}} {n}')
             return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
         @routes.get("/health")

@@ -58,6 +58,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--cuda-device", type=int, default=None, metavar="DEVICE_ID")
     p.add_argument("--gpus", type=int, default=1, metavar="N",
                    help="serve one API from N GPU ranks (rank 0: server + coordinator; sched/cluster.py)")
+    p.add_argument("--latency-mode", action="store_true",
+                   help="with --gpus N: prompts whose batch is smaller than N run on all ranks with every UNet "
+                        "call split CFG-/token-parallel (one image sooner) instead of on one idle rank")
     cm = p.add_mutually_exclusive_group()
     cm.add_argument("--cuda-malloc", action="store_true")
     cm.add_argument("--disable-cuda-malloc", action="store_true")

@@ -64,9 +64,14 @@ inline int rng_blocks(long long work) {
 // ------------------------------------------------------------------ N(0,1) fill, [B, n] fp32 / bf16
 template <bool BF16>
 __global__ void philox_randn_kernel(void* __restrict__ out, int B, long long n, uint64_t seed, long long index0,
-                                    uint64_t stream, const long long* __restrict__ dev_step, float scale) {
+                                    uint64_t stream, const long long* __restrict__ dev_step, float scale,
+                                    const long long* __restrict__ dev_key) {
   const long long groups = (n + 3) >> 2;
   if (dev_step) stream += (uint64_t)(*dev_step);
+  if (dev_key) {              // (seed, index0) from device memory: a captured sampler run serves any seed
+    seed = (uint64_t)dev_key[0];
+    index0 = dev_key[1];
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)B * groups;
        i += (long long)gridDim.x * blockDim.x) {
     const int b = (int)(i / groups);
@@ -93,8 +98,12 @@ __global__ void philox_randn_kernel(void* __restrict__ out, int B, long long n, 
 // Bit-identical to cgs_euler_step(noise = philox_randn(stream=step)) — the noise tensor never exists.
 __global__ void euler_anc_philox_kernel(float* __restrict__ x, const float* __restrict__ den, int B, long long n,
                                         float inv_sigma, float dt, float s_up, uint64_t seed, long long index0,
-                                        uint64_t stream) {
+                                        uint64_t stream, const long long* __restrict__ dev_key) {
   const long long groups = n >> 2;  // host guarantees n % 4 == 0
+  if (dev_key) {
+    seed = (uint64_t)dev_key[0];
+    index0 = dev_key[1];
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)B * groups;
        i += (long long)gridDim.x * blockDim.x) {
     const int b = (int)(i / groups);
@@ -151,8 +160,12 @@ __device__ float4 tree_value(uint64_t key, uint64_t g, double t, double t0, doub
 
 __global__ void brownian_increment_kernel(float* __restrict__ out, int B, long long n, uint64_t seed, long long index0,
                                           double t0, double t1, double ta, double tb, double tol, int max_depth,
-                                          float scale) {
+                                          float scale, const long long* __restrict__ dev_key) {
   const long long groups = n >> 2;
+  if (dev_key) {
+    seed = (uint64_t)dev_key[0];
+    index0 = dev_key[1];
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)B * groups;
        i += (long long)gridDim.x * blockDim.x) {
     const int b = (int)(i / groups);
@@ -227,15 +240,15 @@ __global__ void step_advance_kernel(long long* meta) {
 
 CGS_EXPORT int cgs_philox_randn(void* out, int B, long long n, unsigned long long seed, long long index0,
                                 unsigned long long stream, const void* dev_step, float scale, int dtype,
-                                hipStream_t s) {
+                                const void* dev_key, hipStream_t s) {
   if (B <= 0 || n <= 0) return 0;
   const int blocks = rng_blocks((long long)B * ((n + 3) / 4));
   if (dtype == CGS_F32)
     philox_randn_kernel<false><<<blocks, 256, 0, s>>>(out, B, n, seed, index0, stream, (const long long*)dev_step,
-                                                      scale);
+                                                      scale, (const long long*)dev_key);
   else if (dtype == CGS_BF16)
     philox_randn_kernel<true><<<blocks, 256, 0, s>>>(out, B, n, seed, index0, stream, (const long long*)dev_step,
-                                                     scale);
+                                                     scale, (const long long*)dev_key);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
@@ -243,19 +256,20 @@ CGS_EXPORT int cgs_philox_randn(void* out, int B, long long n, unsigned long lon
 
 CGS_EXPORT int cgs_euler_ancestral_philox(void* x, const void* den, int B, long long n, float sigma, float sigma_down,
                                           float sigma_up, unsigned long long seed, long long index0,
-                                          unsigned long long stream, hipStream_t s) {
+                                          unsigned long long stream, const void* dev_key, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   euler_anc_philox_kernel<<<rng_blocks((long long)B * (n / 4)), 256, 0, s>>>(
-      (float*)x, (const float*)den, B, n, 1.0f / sigma, sigma_down - sigma, sigma_up, seed, index0, stream);
+      (float*)x, (const float*)den, B, n, 1.0f / sigma, sigma_down - sigma, sigma_up, seed, index0, stream,
+      (const long long*)dev_key);
   return (int)hipGetLastError();
 }
 
 CGS_EXPORT int cgs_brownian_increment(void* out, int B, long long n, unsigned long long seed, long long index0,
                                       double t0, double t1, double ta, double tb, double tol, int max_depth,
-                                      float scale, hipStream_t s) {
+                                      float scale, const void* dev_key, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   brownian_increment_kernel<<<rng_blocks((long long)B * (n / 4)), 256, 0, s>>>(
-      (float*)out, B, n, seed, index0, t0, t1, ta, tb, tol, max_depth, scale);
+      (float*)out, B, n, seed, index0, t0, t1, ta, tb, tol, max_depth, scale, (const long long*)dev_key);
   return (int)hipGetLastError();
 }
 

@@ -37,7 +37,7 @@ def apply_args(args):
         os.environ["CGS_TUNE_FILE"] = args.tune_file
     if args.hbm_budget_gb:
         os.environ["CGS_HBM_BUDGET_GB"] = str(args.hbm_budget_gb)
-    if getattr(args, "weight_arena_gb", None):
+    if getattr(args, "weight_arena_gb", None) is not None:
         os.environ["CGS_WEIGHT_ARENA_GB"] = str(args.weight_arena_gb)
     if args.hip_graphs:
         os.environ["CGS_GRAPHS"] = "1"
@@ -226,7 +226,7 @@ def main(argv=None):
     if cluster_state is not None:
         from .sched.cluster import Coordinator
         _, comm, listener, procs = cluster_state
-        coord = Coordinator(q, server, comm, listener)
+        coord = Coordinator(q, server, comm, listener, latency_default=args.latency_mode)
         server.cluster = coord
         threading.Thread(target=coord.run_forever, daemon=True).start()
         logging.info("serving on %d ranks (single prompts on idle ranks, batches split across all)", comm.world)

@@ -678,6 +678,7 @@ def common_ksampler(model, seed, steps, cfg, sampler_name, scheduler, positive, 
     the one-GPU batch."""
     from ..sched import spmd
     local, batch_inds, shard = spmd.shard_latent(latent)
+    model = spmd.latency_model(model)
     latent_image = local["samples"]
     if disable_noise:
         noise = torch.zeros(latent_image.size(), dtype=torch.float32, layout=latent_image.layout, device="cpu")

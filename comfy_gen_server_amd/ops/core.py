@@ -839,6 +839,31 @@ def _numel1(shape):
     return n
 
 
+# Device-resident RNG key (sampling/run_graph.py): while a sampler run is being captured into hipGraphs,
+# draws keyed by the run's (seed, index0) read both from this int64 device tensor instead of kernel
+# arguments, so replaying the graphs for another job only rewrites the tensor.
+import contextvars as _cv
+_RNG_KEY: _cv.ContextVar = _cv.ContextVar("cgs_rng_key", default=None)
+
+
+def rng_key_scope(key: torch.Tensor, seed: int, index0: int):
+    """Context manager: draws with (seed, index0) take them from ``key`` = [seed, index0] (device)."""
+    class _Scope:
+        def __enter__(self_):
+            self_.tok = _RNG_KEY.set((key, int(seed) & ((1 << 64) - 1), int(index0)))
+
+        def __exit__(self_, *a):
+            _RNG_KEY.reset(self_.tok)
+    return _Scope()
+
+
+def _dev_key(seed, index0):
+    k = _RNG_KEY.get()
+    if k is not None and k[1] == (int(seed) & ((1 << 64) - 1)) and k[2] == index0:
+        return k[0].data_ptr()
+    return None
+
+
 def philox_randn(shape, seed: int, inds, stream: int, device=None, dtype=torch.float32,
                  dev_step: torch.Tensor | None = None) -> torch.Tensor:
     """N(0,1) noise [B, ...] where image b's values depend only on (seed, inds[b], stream).
@@ -854,7 +879,8 @@ def philox_randn(shape, seed: int, inds, stream: int, device=None, dtype=torch.f
         count("rng", "hip")
         out = torch.empty(tuple(shape), device=device, dtype=dtype)
         _check(_lib().cgs_philox_randn(out.data_ptr(), int(shape[0]), _numel1(shape), int(seed) & ((1 << 64) - 1),
-                                       index0, int(stream), _ptr(dev_step), 1.0, _DT[dtype], _stream()),
+                                       index0, int(stream), _ptr(dev_step), 1.0, _DT[dtype], _dev_key(seed, index0),
+                                       _stream()),
                "cgs_philox_randn")
         return out
     if be == "hip" and dtype in (torch.float32, torch.bfloat16):   # scattered indices: one launch per image
@@ -879,7 +905,8 @@ def euler_ancestral_philox(x: torch.Tensor, denoised: torch.Tensor, sigma: float
         x = x.clone()
         _check(_lib().cgs_euler_ancestral_philox(x.data_ptr(), denoised.data_ptr(), int(x.shape[0]), _numel1(x.shape),
                                                  float(sigma), float(sigma_down), float(sigma_up),
-                                                 int(seed) & ((1 << 64) - 1), index0, int(stream), _stream()),
+                                                 int(seed) & ((1 << 64) - 1), index0, int(stream),
+                                                 _dev_key(seed, index0), _stream()),
                "cgs_euler_ancestral_philox")
         return x
     noise = philox_randn(x.shape, seed, inds, stream, device=x.device, dtype=x.dtype) if sigma_up > 0 else None
@@ -901,7 +928,8 @@ def brownian_increment(shape, seed: int, inds, t0: float, t1: float, ta: float, 
         out = torch.empty(tuple(shape), device=device, dtype=torch.float32)
         _check(_lib().cgs_brownian_increment(out.data_ptr(), int(shape[0]), _numel1(shape),
                                              int(seed) & ((1 << 64) - 1), index0, float(t0), float(t1), float(ta),
-                                             float(tb), float(tol), int(max_depth), float(scale), _stream()),
+                                             float(tb), float(tol), int(max_depth), float(scale),
+                                             _dev_key(seed, index0), _stream()),
                "cgs_brownian_increment")
         return out
     count("rng", "torch")

@@ -48,9 +48,26 @@ def native_required() -> bool:
     return os.environ.get("CGS_ALLOW_TORCH_FALLBACK", "0") != "1"
 
 
+_reference_depth = 0
+
+
+class torch_reference:
+    """``with torch_reference():`` every op takes its ``torch`` path (fp32 math, device tensors included):
+    the numerics oracle of the production-scale golden tests (tests/test_golden_sdxl_gpu.py)."""
+
+    def __enter__(self):
+        global _reference_depth
+        _reference_depth += 1
+        return self
+
+    def __exit__(self, *a):
+        global _reference_depth
+        _reference_depth -= 1
+
+
 def backend_for(op: str, t: torch.Tensor, kernel: str | None = None) -> str:
     """Pick the backend for op ``op`` given its primary input ``t``."""
-    if t.device.type != "cuda":
+    if t.device.type != "cuda" or _reference_depth > 0:
         return "torch"
     b = _overrides.get(op) or os.environ.get(f"CGS_OP_{op.upper()}") or _DEFAULT_DEVICE_BACKEND.get(op, "hip")
     if b == "hip":

@@ -8,8 +8,10 @@ seen, and evicting a model leaves holes the activation pools cannot reuse. The s
 contiguous, makes residency accounting exact (``stats()``), and eviction / reload of a model is a
 block free / best-fit placement without touching the activation pools or the hipGraph pools.
 
-Enable with ``--weight-arena-gb N`` (env ``CGS_WEIGHT_ARENA_GB``); ``ModelPatcher.patch_model`` then
-places modules here instead of ``module.to(device)``, and ``unpatch_model`` evicts them.
+On by default on a GPU with at least 128 GB of HBM (a 48 GiB slab, allocated when the first model
+is placed); ``--weight-arena-gb N`` / env ``CGS_WEIGHT_ARENA_GB`` sets the size, 0 disables.
+``ModelPatcher.patch_model`` places modules here instead of ``module.to(device)`` (a model that does
+not fit falls back to the caching allocator), and ``unpatch_model`` evicts them.
 """
 from __future__ import annotations
 
@@ -145,11 +147,28 @@ _ARENAS: dict = {}
 _LOCK = threading.Lock()
 
 
+DEFAULT_GB = 48.0
+
+
+def configured_gb(device) -> float:
+    """Slab size for ``device``: CGS_WEIGHT_ARENA_GB, else DEFAULT_GB on >= 128 GB devices, else 0."""
+    v = os.environ.get("CGS_WEIGHT_ARENA_GB", "auto") or "auto"
+    if v != "auto":
+        return float(v)
+    try:
+        total = torch.cuda.get_device_properties(device).total_memory
+    except Exception:
+        return 0.0
+    return DEFAULT_GB if total >= (128 << 30) else 0.0
+
+
 def get(device) -> WeightArena | None:
-    """The arena of ``device`` when enabled (``CGS_WEIGHT_ARENA_GB``), created on first use."""
-    gb = float(os.environ.get("CGS_WEIGHT_ARENA_GB", "0") or 0)
+    """The arena of ``device`` when enabled, created on first use."""
     device = torch.device(device)
-    if gb <= 0 or device.type != "cuda":
+    if device.type != "cuda":
+        return None
+    gb = configured_gb(device)
+    if gb <= 0:
         return None
     key = device.index if device.index is not None else torch.cuda.current_device()
     with _LOCK:

@@ -472,8 +472,11 @@ class KSAMPLER(Sampler):
         total = len(sigmas) - 1
         timed = telemetry.step_timer(callback)        # per-step wall clock + fault site
         k_cb = lambda x: timed(x["i"], x["denoised"], x["x"], total)  # noqa: E731
-        samples = self.sampler_function(mk, noise, sigmas, extra_args=extra_args, callback=k_cb, disable=disable_pbar,
-                                        **self.extra_options)
+        from . import run_graph
+        samples = run_graph.try_run(self, model_wrap, mk, noise, sigmas, extra_args, k_cb)   # one hipGraph per step
+        if samples is None:
+            samples = self.sampler_function(mk, noise, sigmas, extra_args=extra_args, callback=k_cb,
+                                            disable=disable_pbar, **self.extra_options)
         return ms.inverse_noise_scaling(sigmas[-1], samples)
 
 

@@ -55,43 +55,61 @@ def _ancestral(s0, s1, eta):
     return get_ancestral_step(s0, s1, eta=eta)
 
 
-def _eligible(mk, x, extra_args):
+def _no(reason):
+    """Record why the fused step graph declined a run (bench JSON / ``/metrics``: ``ineligible``); the
+    run then goes to the per-step run capture (run_graph.py) or the eager loop."""
+    d = stats.setdefault("ineligible", {})
+    d[reason] = d.get(reason, 0) + 1
+    return None
+
+
+def _eligible(mk, x, extra_args, record=False):
     from .samplers import CFGGuider, KSamplerX0Inpaint, _simple_conds
-    if not graphs.enabled() or not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous():
+    no = _no if record else (lambda reason: None)
+    if not graphs.enabled():
+        return no("hip graphs disabled")
+    if not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous():
+        return no("latent not a contiguous fp32 device tensor")
+    try:
+        if torch.cuda.is_current_stream_capturing():      # inside a sampler-run capture (run_graph.py)
+            return None
+    except Exception:
         return None
-    if x[0].numel() % 4 or not isinstance(mk, KSamplerX0Inpaint) or extra_args.get("denoise_mask") is not None:
-        return None
+    if x[0].numel() % 4 or not isinstance(mk, KSamplerX0Inpaint):
+        return no("latent shape")
+    if extra_args.get("denoise_mask") is not None:
+        return no("denoise mask (inpaint)")
     if extra_args.get("seed") is None:
-        return None
+        return no("no seed")
     inds = extra_args.get("noise_inds") or list(range(x.shape[0]))
     index0, contiguous = rng.contiguous_inds(inds)
     if not contiguous or len(inds) != x.shape[0]:
-        return None
+        return no("non-contiguous noise indices")
     guider = mk.inner_model
     if type(guider) is not CFGGuider:
-        return None
+        return no("custom guider")
     mo = extra_args.get("model_options") or {}
     if any(k in mo for k in ("sampler_cfg_function", "sampler_post_cfg_function", "model_function_wrapper",
                              "denoise_mask_function")):
-        return None
+        return no("sampler cfg / post-cfg / wrapper hook")
     to = mo.get("transformer_options", {})
     if to.get("patches") or to.get("patches_replace"):
-        return None
+        return no("transformer patches")
     pos, neg = guider.conds.get("positive"), guider.conds.get("negative")
     use_uncond = not (abs(guider.cfg - 1.0) < 1e-9 and not mo.get("disable_cfg1_optimization", False))
     lists = [pos, neg] if use_uncond else [pos]
     if any(cl is None or len(cl) != 1 for cl in lists) or not _simple_conds(lists):
-        return None
+        return no("area / mask / timestep-range / multi-entry conds")
     if any(cl[0].get("gligen") is not None for cl in lists):
-        return None
+        return no("gligen")
     ctrls = [cl[0].get("control") for cl in lists]
     ctrl = ctrls[0]
     if any(c is not ctrl for c in ctrls):       # cond and uncond must share the control (one batch)
-        return None
+        return no("different controlnets on cond / uncond")
     if ctrl is not None:
         from ..runtime.controlnet import ControlNet
         if any(type(cn) is not ControlNet and not issubclass(type(cn), ControlNet) for cn in _chain(ctrl)):
-            return None                          # T2I adapters / others: eager
+            return no("t2i adapter / non-controlnet control")   # T2I adapters / others: eager
     return guider, lists, use_uncond, index0, mo, ctrl
 
 
@@ -114,7 +132,7 @@ def _conditioning(guider, lists, x, sigma0):
 
 def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0, s_noise: float = 1.0):
     """Run the whole sampling loop from graph replays; None when not eligible (caller runs eager)."""
-    el = _eligible(mk, x, extra_args)
+    el = _eligible(mk, x, extra_args, record=True)
     if el is None:
         return None
     guider, lists, use_uncond, index0, mo, ctrl = el

@@ -75,16 +75,21 @@ def prompt_batch(prompt: dict) -> int:
     return best
 
 
-def choose_mode(prompt: dict, extra_data: dict | None, world: int) -> str:
-    """``spmd`` when the batch covers every live rank and the prompt samples; else ``single``.
-    ``extra_data["dp"]`` (``"spmd"`` / ``"single"``) overrides."""
+def choose_mode(prompt: dict, extra_data: dict | None, world: int, latency_default: bool = False) -> str:
+    """``spmd`` when the batch covers every live rank and the prompt samples; ``latency`` for a smaller
+    batch when the server runs with ``--latency-mode`` (one image sooner instead of more images per
+    second); else ``single``. ``extra_data["dp"]`` (``"spmd"`` / ``"latency"`` / ``"single"``) overrides."""
     want = (extra_data or {}).get("dp", "auto")
     if world <= 1:
         return "single"
-    if want in ("spmd", "single"):
+    if want in ("spmd", "single", "latency"):
         return want
     has_sampler = any(isinstance(n, dict) and n.get("class_type") in SAMPLER_TYPES for n in prompt.values())
-    return "spmd" if has_sampler and prompt_batch(prompt) >= world else "single"
+    if not has_sampler:
+        return "single"
+    if prompt_batch(prompt) >= world:
+        return "spmd"
+    return "latency" if latency_default else "single"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -172,8 +177,8 @@ def worker_main(comm, address, authkey: bytes):
         server.last_prompt_id = pid
         t0 = time.perf_counter()
         n0 = ctx.images_sampled
-        if m["mode"] == "spmd":
-            with spmd.activate(ctx):
+        if m["mode"] in ("spmd", "latency"):
+            with spmd.activate(ctx, m["mode"]):
                 ex_spmd.execute(m["prompt"], pid, {}, m["outputs"])
             ex = ex_spmd
         else:
@@ -192,11 +197,12 @@ def worker_main(comm, address, authkey: bytes):
 # rank 0
 # ------------------------------------------------------------------------------------------------
 class Coordinator:
-    def __init__(self, q, server, comm, listener, accept_timeout_s: float = 600.0):
+    def __init__(self, q, server, comm, listener, accept_timeout_s: float = 600.0, latency_default=False):
         from ..graph.executor import PromptExecutor
         from . import spmd
         self.q, self.server, self.comm = q, server, comm
         self.world = comm.world
+        self.latency_default = latency_default
         self.conns: dict = {}
         self.locks: dict = {}
         self.dead: set = set()
@@ -204,9 +210,6 @@ class Coordinator:
         self.cv = threading.Condition()
         self.spmd_waiting: dict = {}  # prompt_id -> {rank: done message}
         self.ran_on: dict = {}        # prompt_id -> rank(s), for /history metrics and tests
-        self.ctx = spmd.SPMD(comm)
-        self.ex_single = PromptExecutor(server)
-        self.ex_spmd = PromptExecutor(server, node_hook=self.ctx)
         self._inflight: dict = {}     # rank -> (queue item id, prompt id) of its single prompt
         self._sids: dict = {}         # prompt id -> submitting client (WS)
 
@@ -221,6 +224,10 @@ class Coordinator:
         t.join(accept_timeout_s)
         if len(self.conns) < self.world - 1:
             raise RuntimeError(f"only {len(self.conns)} of {self.world - 1} worker ranks connected")
+        # after the handshakes: building the SPMD context is collective (latency-mode process groups)
+        self.ctx = spmd.SPMD(comm)
+        self.ex_single = PromptExecutor(server)
+        self.ex_spmd = PromptExecutor(server, node_hook=self.ctx)
         for r, conn in self.conns.items():
             threading.Thread(target=self._reader, args=(r, conn), daemon=True).start()
         if hasattr(server, "interrupt_hooks"):
@@ -306,9 +313,9 @@ class Coordinator:
             sid = extra.get("client_id")
             if sid is not None:
                 self._sids[prompt_id] = sid
-            mode = choose_mode(prompt, extra, len(self.live()))
-            if mode == "spmd" and len(self.live()) == self.world:
-                self._run_spmd(item_id, prompt_id, prompt, extra, outputs)
+            mode = choose_mode(prompt, extra, len(self.live()), self.latency_default)
+            if mode in ("spmd", "latency") and len(self.live()) == self.world:
+                self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode)
             else:
                 self._run_single(item_id, prompt_id, prompt, extra, outputs)
 
@@ -342,21 +349,21 @@ class Coordinator:
                                     "outputs_ui": self.ex_single.outputs_ui})
             self.cv.notify_all()
 
-    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs):
+    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd"):
         from . import spmd
         self._wait(lambda: not self.busy)
         with self.cv:
             for r in self.live():
                 self.busy[r] = prompt_id
             self.spmd_waiting[prompt_id] = {}
-            self.ran_on[prompt_id] = "all"
-        msg = {"op": "run", "mode": "spmd", "prompt_id": prompt_id, "prompt": prompt, "outputs": outputs}
+            self.ran_on[prompt_id] = "all" if mode == "spmd" else "latency"
+        msg = {"op": "run", "mode": mode, "prompt_id": prompt_id, "prompt": prompt, "outputs": outputs}
         for r in self.live():
             if r != 0:
                 send_msg(self.conns[r], msg, self.locks[r])
         self.server.last_prompt_id = prompt_id
         n0 = self.ctx.images_sampled
-        with spmd.activate(self.ctx):
+        with spmd.activate(self.ctx, mode):
             self.ex_spmd.execute(prompt, prompt_id, extra, outputs)
         mine = self.ctx.images_sampled - n0
         self._wait(lambda: all(r in self.spmd_waiting[prompt_id] for r in self.live() if r != 0)

@@ -18,7 +18,10 @@ order), and:
   then run on rank 0 only, which writes the files and sends the WebSocket events;
 * interrupts: a rank only stops at a node boundary, where the ranks agree through a max-reduction of
   their interrupt flags on the Gloo control group (an unagreed stop would strand the others in a
-  collective).
+  collective);
+* ``mode = "latency"`` (a batch smaller than the node): nothing is sharded; every rank runs the whole
+  prompt and each UNet call is split CFG- and token-parallel over the ranks (``parallel/latency.py``),
+  so one image finishes sooner.
 """
 from __future__ import annotations
 
@@ -38,6 +41,13 @@ class SPMD:
         self.comm = comm
         self.rank, self.world = comm.rank, comm.world
         self.images_sampled = 0       # images this rank sampled in SPMD prompts (shard sizes)
+        # "spmd": split the image batch; "latency": every rank runs the whole (small) batch and each
+        # UNet call is split CFG-/token-parallel over the ranks (parallel/latency.py)
+        self.mode = "spmd"
+        self.latency = None
+        if comm.world > 1 and comm.enabled:
+            from ..parallel.latency import LatencyParallel
+            self.latency = LatencyParallel(comm)    # collective: every rank builds its SPMD context once
 
     def shard(self, total: int):
         """(offset, count) of this rank's images of a batch of ``total`` (even split, remainder first)."""
@@ -109,25 +119,35 @@ def active() -> SPMD | None:
     return _CTX.get()
 
 
-class activate:
-    """``with spmd.activate(ctx): executor.execute(...)`` -- the SPMD context of this thread."""
+def latency_model(model):
+    """In a latency-mode prompt: ``model`` (ModelPatcher) with its UNet calls split over the ranks."""
+    ctx = active()
+    if ctx is None or ctx.mode != "latency" or ctx.latency is None:
+        return model
+    return ctx.latency.patch(model)
 
-    def __init__(self, ctx: SPMD):
-        self.ctx = ctx
+
+class activate:
+    """``with spmd.activate(ctx[, mode]): executor.execute(...)`` -- the SPMD context of this thread."""
+
+    def __init__(self, ctx: SPMD, mode: str = "spmd"):
+        self.ctx, self.mode = ctx, mode
 
     def __enter__(self):
+        self.prev_mode, self.ctx.mode = self.ctx.mode, self.mode
         self.tok = _CTX.set(self.ctx)
         return self.ctx
 
     def __exit__(self, *exc):
         _CTX.reset(self.tok)
+        self.ctx.mode = self.prev_mode
 
 
 def shard_latent(latent: dict):
     """In an SPMD prompt: this rank's part of a LATENT (already sharded or not) ->
     (local dict, global batch indices, (off, n, total)); outside: (latent, batch_index, None)."""
     ctx = active()
-    if ctx is None:
+    if ctx is None or ctx.mode == "latency":
         return latent, latent.get("batch_index"), None
     if "dp_shard" in latent:
         off, n, total = latent["dp_shard"]

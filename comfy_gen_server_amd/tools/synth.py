@@ -191,3 +191,56 @@ def random_lora(model_patcher, rank=4, seed=0, prefix_filter=("attn1.to_q", "att
         sd[f"{name}.lora_down.weight"] = torch.randn((rank, in_f), generator=g) * 0.01
         sd[f"{name}.alpha"] = torch.tensor(float(rank))
     return sd
+
+
+_PIPELINES: dict = {}
+
+
+class SyntheticCheckpointLoader:
+    """Workflow node: random-init (MODEL, CLIP, VAE) of a family's exact architecture, built once per
+    (family, seed) on the device -- the product workflow path (bench.py --via-executor, tests) without
+    a checkpoint file. Registered on demand (``register_node``), never by default."""
+
+    @classmethod
+    def INPUT_TYPES(cls):
+        return {"required": {"family": (sorted(FAMILY_UNET),), "seed": ("INT", {"default": 0, "min": 0})}}
+
+    RETURN_TYPES = ("MODEL", "CLIP", "VAE")
+    FUNCTION = "load"
+    CATEGORY = "loaders/testing"
+
+    def load(self, family, seed):
+        key = (family, int(seed))
+        if key not in _PIPELINES:
+            from ..runtime import device as dm
+            dev = dm.get_torch_device()
+            dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+            with torch.inference_mode():
+                _PIPELINES[key] = build_pipeline(family, device=dev, dtype=dtype, seed=int(seed))
+        return _PIPELINES[key]
+
+
+def register_node():
+    from ..graph import registry
+    registry.NODE_CLASS_MAPPINGS["CGSSyntheticCheckpoint"] = SyntheticCheckpointLoader
+    registry.NODE_DISPLAY_NAME_MAPPINGS["CGSSyntheticCheckpoint"] = "Synthetic checkpoint (random init)"
+
+
+def text_to_image_workflow(family="sdxl", seed=0, text="a photo", negative="blurry", width=1024, height=1024,
+                           batch=1, steps=20, cfg=8.0, sampler="euler_ancestral", scheduler="normal",
+                           model_seed=1234, save_prefix="bench"):
+    """The reference's default text-to-image graph (script_examples/basic_api_example.py shape) on the
+    synthetic loader."""
+    enc = "CLIPTextEncode"
+    return {
+        "4": {"class_type": "CGSSyntheticCheckpoint", "inputs": {"family": family, "seed": model_seed}},
+        "5": {"class_type": "EmptyLatentImage", "inputs": {"width": width, "height": height, "batch_size": batch}},
+        "6": {"class_type": enc, "inputs": {"text": text, "clip": ["4", 1]}},
+        "7": {"class_type": enc, "inputs": {"text": negative, "clip": ["4", 1]}},
+        "3": {"class_type": "KSampler", "inputs": {"seed": seed, "steps": steps, "cfg": cfg, "sampler_name": sampler,
+                                                  "scheduler": scheduler, "denoise": 1.0, "model": ["4", 0],
+                                                  "positive": ["6", 0], "negative": ["7", 0],
+                                                  "latent_image": ["5", 0]}},
+        "8": {"class_type": "VAEDecode", "inputs": {"samples": ["3", 0], "vae": ["4", 2]}},
+        "9": {"class_type": "SaveImage", "inputs": {"filename_prefix": save_prefix, "images": ["8", 0]}},
+    }

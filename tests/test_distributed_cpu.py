@@ -357,3 +357,19 @@ def test_bench_watchdog_stops_survivors():
     assert "stopped the other ranks" in r.stderr, r.stderr[-3000:]
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert time.time() - t0 < 120
+
+
+def test_bench_via_executor_two_ranks():
+    """``bench.py --via-executor --gpus 2``: the workflow-JSON path (validate_prompt + PromptExecutor),
+    SPMD over two ranks; rank 0 writes every image of the batch."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1", "--cpu",
+           "--family", "tiny", "--res", "64", "--sampler-steps", "2", "--batch-per-gpu", "2", "--via-executor"]
+    env = _env()
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 4 and "PromptExecutor" in res["path"]
+    assert res["pngs_written"] == 8        # warmup + timed step, 4 images each, all on rank 0

@@ -1,0 +1,70 @@
+"""Pipelined multi-rank DP serving on the device (parallel/dp.py ``run_many(pipeline=True)``): three rank
+processes share the box's GPU (Gloo process group, so the collectives are host-side here; on a node each
+rank has its own GPU and RCCL). Job n's VAE decode + image gather run on a side HIP stream while job
+n+1 samples on the main stream; the gathered batches on rank 0 must equal a one-rank run."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_WORKER = r'''
+import os, sys, torch
+sys.path.insert(0, os.environ["PYTHONPATH"])
+from comfy_gen_server_amd.parallel.comm import init_from_env
+c = init_from_env(backend="gloo")
+from comfy_gen_server_amd.tools.synth import build_pipeline
+from comfy_gen_server_amd.parallel.dp import DataParallelGenerator, Job
+dev = torch.device("cuda", 0)
+with torch.inference_mode():
+    patcher, clip, vae = build_pipeline("tiny", device=dev, dtype=torch.bfloat16, seed=3)
+    gen = DataParallelGenerator(patcher, clip, vae)
+    gen.sync_weights()
+    jobs = [Job(batch=5, steps=3, width=64, height=64, seed=40 + i) for i in range(3)]
+    outs = list(gen.run_many(iter(jobs), pipeline=True))
+torch.cuda.synchronize()
+if c.rank == 0:
+    torch.save([o.cpu() for o in outs], os.path.join(os.environ["CGS_TEST_OUT"], f"ws{c.world}.pt"))
+c.shutdown()
+'''
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_pipelined_run_many_three_ranks_matches_one(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    script = tmp_path / "w.py"
+    script.write_text(_WORKER)
+    env = dict(os.environ, PYTHONPATH=ROOT, CGS_TEST_OUT=str(tmp_path), MASTER_ADDR="127.0.0.1", LOCAL_RANK="0",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, str(script)], env=dict(env, WORLD_SIZE="1", RANK="0"), cwd=ROOT,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    port = str(_free_port())
+    procs = [subprocess.Popen([sys.executable, str(script)], cwd=ROOT,
+                              env=dict(env, WORLD_SIZE="3", RANK=str(k), MASTER_PORT=port),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for k in range(3)]
+    try:
+        rcs = [p.wait(timeout=600) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0, 0], (rcs, procs[0].stderr.read()[-3000:])
+    one = torch.load(tmp_path / "ws1.pt", weights_only=True)
+    three = torch.load(tmp_path / "ws3.pt", weights_only=True)
+    assert len(one) == len(three) == 3
+    for a, b in zip(one, three):
+        assert a.shape == b.shape == (5, 64, 64, 3)
+        d = (a.int() - b.int()).abs()
+        assert d.max() <= 2 and d.float().mean() < 0.25, (d.max(), d.float().mean())

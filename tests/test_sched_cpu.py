@@ -52,8 +52,7 @@ def _graph(seed, batch, prefix):
     }
 
 
-@pytest.fixture(scope="module")
-def cluster(tmp_path_factory):
+def _start(tmp_path_factory, n, extra=()):
     base = tmp_path_factory.mktemp("cgs_cluster")
     for d in ("models/checkpoints", "output", "input", "temp"):
         os.makedirs(base / d, exist_ok=True)
@@ -69,9 +68,10 @@ def cluster(tmp_path_factory):
     port = _free_port()
     env["MASTER_PORT"] = str(_free_port())
     env["CGS_REGISTER_TINY"] = "1"
-    proc = subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main", "--gpus", "3", "--cpu",
+    proc = subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main", "--gpus", str(n), "--cpu",
                              "--listen", "127.0.0.1", "--port", str(port), "--base-directory", str(base),
-                             "--disable-custom-nodes", "--dont-print-server", "--preview-method", "none"],
+                             "--disable-custom-nodes", "--dont-print-server", "--preview-method", "none"]
+                            + list(extra),
                             cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                             start_new_session=True)
     url = f"http://127.0.0.1:{port}"
@@ -87,12 +87,22 @@ def cluster(tmp_path_factory):
     else:
         os.killpg(proc.pid, signal.SIGKILL)
         raise RuntimeError("server did not come up")
-    yield url, base
+    return proc, url, base
+
+
+def _stop(proc):
     os.killpg(proc.pid, signal.SIGTERM)
     try:
         proc.wait(timeout=30)
     except subprocess.TimeoutExpired:
         os.killpg(proc.pid, signal.SIGKILL)
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    proc, url, base = _start(tmp_path_factory, 3)
+    yield url, base
+    _stop(proc)
 
 
 def _wait(url, pids, timeout=300):
@@ -142,3 +152,20 @@ def test_independent_prompts_use_every_rank(cluster):
     assert ranks == {0, 1, 2}, ranks
     for e in h.values():
         assert len(_images(base, e)) == 1
+
+
+def test_latency_mode_batch_one_matches_one_rank(tmp_path_factory):
+    """``--gpus 2 --latency-mode``: a batch-1 prompt runs on both ranks with each UNet call split
+    CFG-parallel (cond on rank 0, uncond on rank 1, outputs all-gathered) -- same image as one rank."""
+    proc, url, base = _start(tmp_path_factory, 2, ["--latency-mode"])
+    try:
+        a = _post(url + "/prompt", {"prompt": _graph(21, 1, "lat")})["prompt_id"]
+        b = _post(url + "/prompt", {"prompt": _graph(21, 1, "lat1"), "extra_data": {"dp": "single"}})["prompt_id"]
+        h = _wait(url, [a, b])
+    finally:
+        _stop(proc)
+    assert h[a]["status"]["status_str"] == "success", h[a]["status"]
+    assert h[a]["metrics"]["ranks"] == "latency"
+    x, y = _images(base, h[a])[0], _images(base, h[b])[0]
+    d = np.abs(x - y)
+    assert d.max() <= 2 and d.mean() < 0.25, (d.max(), d.mean())
