@@ -39,6 +39,9 @@ def main():
                          "stream while job n+1 samples: dp.run_many); every job still completes inside the "
                          "timed region")
     ap.add_argument("--profile-ops", action="store_true", help="(kept for compatibility; op backends are always reported)")
+    ap.add_argument("--latency", action="store_true",
+                    help="latency mode: ONE image per step for the whole node; every UNet call split CFG-/token-"
+                         "parallel over the N ranks (parallel/latency.py); reports sec/image (strong scaling)")
     ap.add_argument("--via-executor", action="store_true",
                     help="time the product path: a text-to-image workflow JSON through validate_prompt + "
                          "PromptExecutor (CLIPTextEncode x2 -> KSampler -> VAEDecode -> SaveImage PNGs); at N > 1 "
@@ -104,6 +107,8 @@ def main():
 
     if args.via_executor:
         return _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log)
+    if args.latency:
+        return _bench_latency(args, comm, gen, job, t0, t_build, log)
 
     def one_step(i):
         j = Job(**{**job.__dict__, "seed": 1000 + i})
@@ -261,6 +266,49 @@ def _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log):
         from comfy_gen_server_amd.sampling import run_graph as _rg, step_graph as _sg
         res["step_graph"] = dict(_sg.stats)
         res["run_graph"] = dict(_rg.stats)
+        print(json.dumps(res), flush=True)
+    comm.shutdown()
+
+
+def _bench_latency(args, comm, gen, job, t0, t_build, log):
+    """--latency: batch 1 per node; rank r evaluates its CFG half / token shard of every UNet call."""
+    import torch
+    from comfy_gen_server_amd import ops
+    from comfy_gen_server_amd.parallel.dp import Job, encode_prompt, generate_local
+    from comfy_gen_server_amd.parallel.latency import LatencyParallel
+    lat = LatencyParallel(comm)
+    patcher = lat.patch(gen.patcher)
+
+    def step(i):
+        j = Job(**{**job.__dict__, "seed": 1000 + i, "batch": 1})
+        with torch.inference_mode():
+            img = generate_local(patcher, gen.clip, gen.vae, j, 0, 1, decode="uint8")
+        if not args.cpu:
+            torch.cuda.synchronize()
+        return img
+
+    for i in range(args.warmup):
+        ts = time.perf_counter()
+        step(i)
+        log(f"warmup image {i}: {time.perf_counter() - ts:.2f}s")
+    comm.barrier()
+    ops.reset_stats()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    comm.barrier()
+    dt = comm.all_reduce_max(time.perf_counter() - t1)
+    if comm.rank == 0:
+        res = {"metric": "sec/image, one image per node (latency mode)", "value": round(dt / max(1, args.steps), 4),
+               "unit": "s/image", "n_gpus": comm.world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt * 1000.0 / max(1, args.steps), 2), "higher_is_better": False,
+               "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if args.cpu else "bf16",
+               "data": "synthetic prompts, random-init weights (exact SDXL-base architecture)",
+               "config": {"model": f"{args.family}-base" if args.family == "sdxl" else args.family, "global_batch": 1,
+                          "resolution": args.res, "sampler_steps": args.sampler_steps, "sampler": args.sampler,
+                          "cfg": args.cfg, "parallelism": f"cfg{lat.G}xtoken{lat.Q}"},
+               "unet_calls_on_rank0": lat.calls, "build_s": round(t_build, 1)}
+        res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
         print(json.dumps(res), flush=True)
     comm.shutdown()
 

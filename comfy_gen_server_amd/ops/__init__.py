@@ -12,7 +12,7 @@ xformers / SDPA) — on MI355X all of them collapse to one LDS-tiled MFMA flash-
 """
 from . import dispatch  # noqa: F401
 from .dispatch import (  # noqa: F401
-    backend_for, set_backend_override, native_required, NativeMissingError, stats, reset_stats,
+    backend_for, set_backend_override, native_required, NativeMissingError, stats, reset_stats, torch_reference,
 )
 from .core import (  # noqa: F401
     linear, linear_geglu, attention, attention_lse, group_norm, layer_norm, conv2d, conv_transpose2d,
@@ -22,4 +22,5 @@ from .core import (  # noqa: F401
     attention_with_probs, philox_randn, euler_ancestral_philox, brownian_increment, step_param, sampler_step_dev,
     step_advance, vae_out_u8, region_accumulate, region_normalize, clip_embed, pooled_gather,
     layernorm_stats, lnfold_weights, linear_lnfold, lnfold_available, fourier_filter, tome_match,
+    rng_key_scope,
 )

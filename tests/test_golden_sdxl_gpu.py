@@ -6,7 +6,6 @@ path (``ops.dispatch.torch_reference``), graphs off.
 
 Bounds (relative L2): one UNet forward < 3e-2, VAE decode < 3e-2, CLIP-G < 3e-2, a 20-step Euler-a run
 < 5e-2. No vendor-library (``lib``) call may appear on the HIP path."""
-import copy
 import os
 
 import pytest
@@ -31,17 +30,31 @@ def sdxl():
     yield dev, patcher, clip, vae
 
 
-def _fp32_copy_unet(patcher):
-    from comfy_gen_server_amd.models.layers import invalidate_all
-    p32 = copy.deepcopy(patcher)
-    dm = p32.model.diffusion_model
-    dm.float()
-    dm.dtype = torch.float32
-    invalidate_all(p32.model)
-    p32.model.__dict__.pop("_graph_runner", None)
-    p32.model.__dict__.pop("_step_graph_plans", None)
-    p32.model.__dict__.pop("_run_graph_plans", None)
-    return p32
+class _as_fp32:
+    """Convert a module (and the wrapper's dtype attributes) to fp32 IN PLACE for the oracle run, then
+    back to bf16 -- bf16 -> fp32 -> bf16 is exact, so the HIP runs before and after see the same
+    weights. (A deep copy is not possible: models carry captured hipGraphs and native tokenizers.)"""
+
+    def __init__(self, module, owner=None, attr=None):
+        self.module, self.owner, self.attr = module, owner, attr
+
+    def __enter__(self):
+        from comfy_gen_server_amd.models import layers
+        self.module.float()
+        if self.owner is not None:
+            self.prev = getattr(self.owner, self.attr)
+            setattr(self.owner, self.attr, torch.float32)
+        layers.stamp_epoch(self.module)       # retire graphs / derived layouts over the bf16 buffers
+        layers.invalidate_all(self.module)
+        return self.module
+
+    def __exit__(self, *a):
+        from comfy_gen_server_amd.models import layers
+        self.module.to(torch.bfloat16)
+        if self.owner is not None:
+            setattr(self.owner, self.attr, self.prev)
+        layers.stamp_epoch(self.module)
+        layers.invalidate_all(self.module)
 
 
 def _no_lib():
@@ -67,10 +80,8 @@ def test_sdxl_unet_forward_1024(sdxl, monkeypatch):
         _no_lib()
         assert ops.stats().get(("gemm", "hip"), 0) > 0
         monkeypatch.setenv("CGS_GRAPHS", "0")
-        p32 = _fp32_copy_unet(patcher)
-        with torch_reference():
-            want = p32.model.diffusion_model(x, t, context=ctx, y=y).float()
-        del p32
+        with _as_fp32(unet, unet, "dtype"), torch_reference():
+            want = unet(x, t, context=ctx, y=y).float()
     err = _rel(got, want)
     assert err < 3e-2, err
 
@@ -86,14 +97,8 @@ def test_sdxl_vae_decode_1024(sdxl):
         got = vae.decode(lat).float()
         torch.cuda.synchronize()
         _no_lib()
-        v32 = copy.deepcopy(vae)
-        v32.first_stage_model.float()
-        v32.vae_dtype = torch.float32
-        from comfy_gen_server_amd.models.layers import invalidate_all
-        invalidate_all(v32.first_stage_model)
-        with torch_reference():
-            want = v32.decode(lat).float()
-        del v32
+        with _as_fp32(vae.first_stage_model, vae, "vae_dtype"), torch_reference():
+            want = vae.decode(lat).float()
     assert got.shape == want.shape == (1, 1024, 1024, 3)
     err = _rel(got, want)
     assert err < 3e-2, err
@@ -101,17 +106,12 @@ def test_sdxl_vae_decode_1024(sdxl):
 
 def test_sdxl_clip_g_77_tokens(sdxl):
     from comfy_gen_server_amd.ops.dispatch import torch_reference
-    from comfy_gen_server_amd.models.layers import invalidate_all
     dev, patcher, clip, vae = sdxl
     tokens = clip.tokenize("a photo of an astronaut riding a horse on mars, (highly detailed:1.2), 8k")
     with torch.inference_mode():
         cond, pooled = clip.encode_from_tokens(tokens, return_pooled=True)
-        c32 = copy.deepcopy(clip)
-        c32.cond_stage_model.float()
-        invalidate_all(c32.cond_stage_model)
-        with torch_reference():
-            want, want_pooled = c32.encode_from_tokens(tokens, return_pooled=True)
-        del c32
+        with _as_fp32(clip.cond_stage_model), torch_reference():
+            want, want_pooled = clip.encode_from_tokens(tokens, return_pooled=True)
     assert cond.shape == want.shape == (1, 77, 2048)
     assert _rel(cond, want) < 3e-2, _rel(cond, want)
     assert _rel(pooled, want_pooled) < 3e-2, _rel(pooled, want_pooled)
@@ -138,11 +138,10 @@ def test_sdxl_20_step_euler_a_captured_vs_fp32_eager(sdxl, monkeypatch):
         assert step_graph.stats.get("kv_refresh", 0) > before.get("kv_refresh", 0)   # static K/V active
         _no_lib()
         monkeypatch.setenv("CGS_GRAPHS", "0")
-        p32 = _fp32_copy_unet(patcher)
         conds32 = tuple([[c[0].float(), {k: (v.float() if torch.is_tensor(v) else v) for k, v in c[1].items()}]
                          for c in cl] for cl in conds)
-        with torch_reference():
-            want = generate_local(p32, clip, vae, job, 0, 2, conds=conds32, decode=False).float()
-        del p32
+        unet = patcher.model.diffusion_model
+        with _as_fp32(unet, unet, "dtype"), torch_reference():
+            want = generate_local(patcher, clip, vae, job, 0, 2, conds=conds32, decode=False).float()
     err = _rel(got, want)
     assert err < 5e-2, err
