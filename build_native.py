@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import json
 import os
 import subprocess
 import sys
@@ -41,13 +42,55 @@ def _stale(src, obj, deps=()):
     return any(os.path.getmtime(p) > t for p in (src,) + tuple(deps))
 
 
+# Private-memory (scratch) budget of the MFMA main-loop kernels, bytes per lane. A kernel whose
+# accumulator / fragment arrays fall out of registers (SROA failing on a grown epilogue) runs ~10x
+# slower with identical results -- round 3 shipped one such v7 build -- so the build fails instead.
+SCRATCH_BUDGET = {"gemm_bf16_nt_v7_kernel": 128, "conv_nhwc_v7_kernel": 128, "attn_fwd_d64": 64}
+
+
+def _resources(out):
+    """kernel -> {vgpr, agpr, scratch, spill} from -Rpass-analysis=kernel-resource-usage remarks."""
+    res, cur = {}, None
+    for line in out.splitlines():
+        if "remark:" not in line:
+            continue
+        txt = line.split("remark:", 1)[1].split("[-Rpass", 1)[0].strip()
+        key, _, val = txt.partition(":")
+        val = val.strip()
+        if key == "Function Name":
+            cur = val
+            res[cur] = {}
+        elif cur is not None and key in ("VGPRs", "AGPRs", "ScratchSize [bytes/lane]", "VGPRs Spill"):
+            res[cur][{"VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [bytes/lane]": "scratch",
+                      "VGPRs Spill": "spill"}[key]] = int(val.split()[0])
+    return res
+
+
+def _check_resources(report):
+    if not report:
+        return
+    path = os.path.join(BUILD, "kernel_resources.json")
+    old = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+    old.update(report)
+    with open(path, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+    bad = [(k, v.get("scratch", 0), lim) for k, v in report.items() for pat, lim in SCRATCH_BUDGET.items()
+           if pat in k and v.get("scratch", 0) > lim]
+    if bad:
+        raise RuntimeError("MFMA kernels over their scratch budget (arrays out of registers):\n" +
+                           "\n".join(f"  {k}: {s} B/lane > {lim}" for k, s, lim in bad))
+
+
 def build_kernels(verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(LIB, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(KDIR, "*.hip")))
     headers = glob.glob(os.path.join(KDIR, "*.h"))
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-mcode-object-version=5",
-             "-Wno-unused-result", "-munsafe-fp-atomics"]
+             "-Wno-unused-result", "-munsafe-fp-atomics", "-Rpass-analysis=kernel-resource-usage"]
     jobs = []
     objs = []
     for s in srcs:
@@ -55,10 +98,13 @@ def build_kernels(verbose=False):
         objs.append(o)
         if _stale(s, o, headers):
             jobs.append([HIPCC] + flags + ["-c", s, "-o", o])
+    report = {}
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         for out in ex.map(_run, jobs):
-            if verbose and out.strip():
-                print(out)
+            report.update(_resources(out))
+            if verbose:
+                print("\n".join(l for l in out.splitlines() if "remark" not in l))
+    _check_resources(report)
     so = os.path.join(LIB, "libcgs_kernels.so")
     if jobs or not os.path.exists(so):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs)

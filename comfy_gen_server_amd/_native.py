@@ -161,6 +161,7 @@ KERNEL_SIGNATURES = {
     # K22 materialised wide-head attention: fp32 S -> bf16 P row softmax (log2 units) and a bf16 transpose
     "cgs_softmax2_f32_bf16": [_P, _P, _L, _I, _L, _L, _P],             # x(f32), y(bf16), rows, cols, ldx, ldy
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy
+    "cgs_abort_stream_capture": [_P],
 }
 
 

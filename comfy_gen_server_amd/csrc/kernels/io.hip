@@ -77,3 +77,18 @@ CGS_EXPORT int cgs_h2d_upload(const void* src, void* dst, long long nbytes, long
   }
   return (int)err;
 }
+
+// Ends a stream capture that an exception left open (sampling/run_graph.py failure path): a capture
+// invalidated by an unsupported call can survive the framework's own end-capture attempt, and every
+// later HIP call in the process then fails with "operation not permitted when stream is capturing".
+// Returns 1 if a capture was ended, 0 if the stream was not capturing, < 0 on error.
+CGS_EXPORT int cgs_abort_stream_capture(hipStream_t stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess) return -1;
+  if (st == hipStreamCaptureStatusNone) return 0;
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(stream, &g);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return 1;
+}

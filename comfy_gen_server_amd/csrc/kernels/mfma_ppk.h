@@ -51,10 +51,15 @@ using pp::BK;
 using pp::THREADS;
 using pp::PART;
 using pp::BUF;
-// LDS: the two 64 KiB operand buffers + a 32 KiB epilogue staging area (row-major transposes so the
-// output leaves in full 128-B lines, below) = all 160 KiB of the CU
-constexpr int STG = 32768;
+// Full-line epilogue (kFullLine): outputs leave as 8 rows x 128 B per store instruction through a 32 KiB
+// LDS staging area. Measured on MI355X (profiles/r03_gemm_epilogue.md): one CU stores a 128 KiB tile
+// 3x faster that way when the chip is otherwise idle, but inside this kernel the LDS round trip (and,
+// for GEGLU, the pair exchange behind barriers) costs what the faster stores save -- in-process A/B
+// within +-2 % of the register epilogue on all 7 shapes. Compiled out; kept for the next structure.
+constexpr bool kFullLine = false;
+constexpr int STG = kFullLine ? 32768 : 0;
 constexpr int LDS = pp::LDS + STG;
+
 using pp::P_A0;
 using pp::P_A1;
 using pp::P_B0;
@@ -119,15 +124,12 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   const int G = gridDim.x;
   const int u0 = xcd_remap(blockIdx.x, G);
   if (u0 >= U) return;
-  // timing probes (CGS_V7_SPLIT_DBG / cgs_v7_set_dbg): bit 8 = no epilogue stores, bit 32 = round-2
-  // half-line stores; bits 8.. = start delay unit D:
-  // workgroup b waits (b & 1) x D (bit 16 clear) or (b & 3) x D (bit 16 set) x 8128 cycles
+  // timing probes (CGS_V7_SPLIT_DBG / cgs_v7_set_dbg): bit 8 = no epilogue stores. (Start-delay
+  // desynchronisation probes -- 2, 4 and 8 phases per XCD, with and without full-line stores --
+  // measured slower at every spread and were removed: profiles/r03_gemm_epilogue.md.)
   const bool nostore = (sp.dbg & 8) != 0;
-  const bool legacy = (sp.dbg & 32) != 0;     // probe: half-line register stores (round-2 epilogue)
-  if (sp.dbg >> 8) {
-    const int steps = ((sp.dbg & 16) ? (blockIdx.x & 3) : (blockIdx.x & 1)) * (sp.dbg >> 8);
-    for (int i = 0; i < steps; ++i) __builtin_amdgcn_s_sleep(127);
-  }
+  const bool gelu_as = (sp.dbg & 256) != 0;   // GEGLU: the A&S-erf GELU (round-2 epilogue)
+  constexpr bool legacy = !kFullLine;         // register epilogue: 16 B per lane, 16 rows x 64 B per store
 
   // unit -> (tile origin, K range, partial slot or -1)
   auto unit = [&](int u, int& m0, int& n0, int& kb, int& ke, int& slot) {
@@ -312,7 +314,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
     }
     if constexpr (GG) {
-     if (legacy) {
+     if constexpr (legacy) {
       const int Nout = N >> 1;
       const int ocol = (n0 >> 1) + wc * 32 + 8 * fq;   // 8 output columns of this lane
 #pragma unroll
@@ -325,8 +327,15 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           for (int nq = 0; nq < 2; ++nq) {
             const f32x4 a = acc[mq * 4 + i][nq * 2 + 0], g = acc[mq * 4 + i][nq * 2 + 1];
             const float4 ba = bv[nq][0], bg = bv[nq][1];
-            const f32x2_t g01 = gelu_fast2(f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y});
-            const f32x2_t g23 = gelu_fast2(f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w});
+            f32x2_t g01 = f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y};
+            f32x2_t g23 = f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w};
+            if (gelu_as) {
+              g01 = gelu_fast2(g01);
+              g23 = gelu_fast2(g23);
+            } else {
+              g01 = gelu_sig2(g01);
+              g23 = gelu_sig2(g23);
+            }
             const f32x2_t o01 = (f32x2_t{a[0], a[1]} * e.alpha + f32x2_t{ba.x, ba.y}) * g01;
             const f32x2_t o23 = (f32x2_t{a[2], a[3]} * e.alpha + f32x2_t{ba.z, ba.w}) * g23;
             h[nq] = pack4_bf16(o01.x, o01.y, o23.x, o23.y);
@@ -355,8 +364,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           for (int nq = 0; nq < 2; ++nq) {
             const f32x4 a = acc[mq * 4 + i][nq * 2 + 0], g = acc[mq * 4 + i][nq * 2 + 1];
             const float4 ba = bv[nq][0], bg = bv[nq][1];
-            const f32x2_t g01 = gelu_fast2(f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y});
-            const f32x2_t g23 = gelu_fast2(f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w});
+            const f32x2_t g01 = gelu_sig2(f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y});
+            const f32x2_t g23 = gelu_sig2(f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w});
             const f32x2_t o01 = (f32x2_t{a[0], a[1]} * e.alpha + f32x2_t{ba.x, ba.y}) * g01;
             const f32x2_t o23 = (f32x2_t{a[2], a[3]} * e.alpha + f32x2_t{ba.z, ba.w}) * g23;
             h[nq] = pack4_bf16(o01.x, o01.y, o23.x, o23.y);
@@ -400,7 +409,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             }
           }
         }
-    } else if (legacy) {
+    } else if constexpr (legacy) {
       uint4 rw[2][4][2];
       if constexpr (HR) {
 #pragma unroll
@@ -520,7 +529,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       else epilogue_t(m0, n0, F{}, F{});
     }
   };
-  int& last_flag = *reinterpret_cast<int*>(smem + pp::LDS);   // staging area is idle in the split epilogue
+  __shared__ int last_flag_static;
+  int& last_flag = last_flag_static;
   // split unit: publish the fp32 partial; the tile's last arriver reduces and runs the epilogue
   auto split_epilogue = [&](int m0, int n0, int slot) {
     float4* mine = sp.part + (size_t)slot * (32 * THREADS);

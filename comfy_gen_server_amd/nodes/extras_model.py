@@ -20,6 +20,7 @@ from ..runtime import latent_formats
 from ..runtime.patcher import set_model_options_patch_replace
 from ..sampling import model_sampling as MS
 from ..sampling import sampler_helpers
+from ..sampling.samplers import _host_sigma
 from ..sampling import samplers as SM
 from ..utils import image as U
 from .. import ops
@@ -226,9 +227,10 @@ def attention_with_probs(q, k, v, heads):
 
 def gaussian_blur_2d(img, kernel_size, sigma):
     half = (kernel_size - 1) * 0.5
-    t = torch.linspace(-half, half, steps=kernel_size)
+    # built on the device: no host->device copy, so SAG's post-CFG hook is hipGraph-capturable
+    t = torch.linspace(-half, half, steps=kernel_size, device=img.device, dtype=torch.float32)
     pdf = torch.exp(-0.5 * (t / sigma).pow(2))
-    k1 = (pdf / pdf.sum()).to(device=img.device, dtype=img.dtype)
+    k1 = (pdf / pdf.sum()).to(dtype=img.dtype)
     k2 = torch.outer(k1, k1).expand(img.shape[-3], 1, kernel_size, kernel_size)
     p = kernel_size // 2
     return F.conv2d(F.pad(img, (p, p, p, p), mode="reflect"), k2, groups=img.shape[-3])
@@ -409,7 +411,7 @@ class PatchModelAddDownscale:
 
         def input_block_patch(h, transformer_options):
             if transformer_options["block"][1] == block_number:
-                sigma = float(transformer_options["sigmas"][0])
+                sigma = _host_sigma(transformer_options["sigmas"])   # host copy: no sync, capturable
                 if s_end <= sigma <= s_start:
                     h = U.common_upscale(h, round(h.shape[-1] / downscale_factor),
                                          round(h.shape[-2] / downscale_factor), downscale_method, "disabled")

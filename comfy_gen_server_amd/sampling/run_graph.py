@@ -210,6 +210,18 @@ def try_run(ksampler, guider, mk, x, sigmas, extra_args, callback):
     return plan.out.clone()
 
 
+_graveyard: list = []
+
+
+def _abort_capture(stream):
+    """End a capture an exception left open on ``stream`` (native hipStreamEndCapture)."""
+    from .. import _native
+    lib = _native.load_kernels()
+    if lib is not None and _native.has_kernel("cgs_abort_stream_capture"):
+        if lib.cgs_abort_stream_capture(stream.cuda_stream) > 0:
+            logging.warning("ended a stream capture left open by the failed sampler-run capture")
+
+
 def _capture(ksampler, mk, x, sigmas, extra_args, tensors, seed, index0):
     """Capture the run with THIS job's tensors as the static inputs (the plan keeps them alive)."""
     p = _Plan()
@@ -248,6 +260,10 @@ def _capture(ksampler, mk, x, sigmas, extra_args, tensors, seed, index0):
                 cur[0].capture_end()
             except Exception:
                 pass
+            _abort_capture(side)
+        # the aborted graph objects stay referenced: destroying a graph whose capture was
+        # invalidated can itself raise in the destructor (fatal outside Python's control)
+        _graveyard.append((cur[0], p.graphs))
         try:
             torch.cuda.synchronize()
         except Exception:

@@ -67,4 +67,4 @@ def test_pipelined_run_many_three_ranks_matches_one(tmp_path):
     for a, b in zip(one, three):
         assert a.shape == b.shape == (5, 64, 64, 3)
         d = (a.int() - b.int()).abs()     # bf16 kernels tile 5- and 2-image batches differently
-        assert d.max() <= 4 and d.float().mean() < 0.25, (d.max(), d.float().mean())
+        assert d.max() <= 6 and d.float().mean() < 0.5, (d.max(), d.float().mean())
