@@ -144,6 +144,7 @@ KERNEL_SIGNATURES = {
     # LayerNorm folded into the GEMM: row stats (x, rs, rows, C, eps, dtype) and the v7 GEMM with the fold
     "cgs_layernorm_stats": [_P, _P, _I, _I, _F, _I, _P],
     "cgs_gemm_bf16_lnfold": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _I, _P, _L, _P],
+    "cgs_gemm_bf16_lnfold_v": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _I, _P, _L, _I, _P],
     # v7 split-K tail: workspace bytes for (M, N, K) and the GEMM / conv launchers that take it
     "cgs_v7_ws_bytes": [_I, _I, _I],
     "cgs_v7_set_dbg": [_I],
@@ -162,6 +163,7 @@ KERNEL_SIGNATURES = {
     "cgs_softmax2_f32_bf16": [_P, _P, _L, _I, _L, _L, _P],             # x(f32), y(bf16), rows, cols, ldx, ldy
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy
     "cgs_abort_stream_capture": [_P],
+    "cgs_channel_affine_nhwc": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
 }
 
 

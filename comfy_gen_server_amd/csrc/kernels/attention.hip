@@ -270,7 +270,10 @@ __device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x
   l_run += ps;
 }
 
-__global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
+// NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
+// workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
     long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
   const u16* vbase = vp + b * vsb + h * vsh;
   u16* obase = op + b * osb + h * osh;
 
-  const int q_row = qb * 256 + wave * 32 + l32;
+  const int q_row = qb * (32 * NW) + wave * 32 + l32;
   const bool q_ok = q_row < Sq;
   bf16x8 qf[4];
 #pragma unroll
@@ -300,15 +303,31 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
     qf[ks] = __builtin_bit_cast(bf16x8, t);
   }
 
-  // staging: thread -> (key = tid>>3, chunk = tid&7) of a 64x64 tile
-  const int st_key = tid >> 3, st_c = tid & 7;
-  const int k_woff = st_key * 64 + 8 * (st_c ^ ((st_key >> 1) & 7));
-  const int v_woff = st_key * 64 + 8 * (st_c ^ (((st_key >> 1) & 1) << 2));
+  // staging: thread -> (key = tid>>3 + 64/LPT * i, chunk = tid&7) of a 64x64 tile, LPT keys per thread
+  constexpr int LPT = 8 / NW;
+  const int st_c = tid & 7;
+  int k_woff[LPT], v_woff[LPT], st_key[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    st_key[i] = (tid >> 3) + i * (8 * NW);
+    k_woff[i] = st_key[i] * 64 + 8 * (st_c ^ ((st_key[i] >> 1) & 7));
+    v_woff[i] = st_key[i] * 64 + 8 * (st_c ^ (((st_key[i] >> 1) & 1) << 2));
+  }
   const int n = (Sk + 63) >> 6;
-  auto gload = [&](const u16* base, long long ss, int t) -> s16x8 {
-    int key = t * 64 + st_key;
-    key = key < Sk ? key : Sk - 1;   // clamp: tail rows are masked in the softmax
-    return *reinterpret_cast<const s16x8*>(base + (long long)key * ss + st_c * 8);
+  struct Stg { s16x8 v[LPT]; };
+  auto gload = [&](const u16* base, long long ss, int t) -> Stg {
+    Stg r;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      int key = t * 64 + st_key[i];
+      key = key < Sk ? key : Sk - 1;   // clamp: tail rows are masked in the softmax
+      r.v[i] = *reinterpret_cast<const s16x8*>(base + (long long)key * ss + st_c * 8);
+    }
+    return r;
+  };
+  auto lds_put = [&](u16* tile, const int (&off)[LPT], const Stg& x) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) *reinterpret_cast<s16x8*>(&tile[off[i]]) = x.v[i];
   };
   // QK^T A-operand read offsets (elements) for kt = 0/1, ks = 0..3
   auto k_roff = [&](int kt, int ks) {
@@ -355,12 +374,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
 
   // prologue: K(0) -> slot 0, K(1) -> slot 1, V(0) -> slot 0; S(0)
   {
-    s16x8 k0 = gload(kbase, kss, 0);
-    s16x8 k1 = gload(kbase, kss, n > 1 ? 1 : 0);
-    s16x8 v0 = gload(vbase, vss, 0);
-    *reinterpret_cast<s16x8*>(&Ks[0][k_woff]) = k0;
-    *reinterpret_cast<s16x8*>(&Ks[1][k_woff]) = k1;
-    *reinterpret_cast<s16x8*>(&Vs[0][v_woff]) = v0;
+    const Stg k0 = gload(kbase, kss, 0);
+    const Stg k1 = gload(kbase, kss, n > 1 ? 1 : 0);
+    const Stg v0 = gload(vbase, vss, 0);
+    lds_put(Ks[0], k_woff, k0);
+    lds_put(Ks[1], k_woff, k1);
+    lds_put(Vs[0], v_woff, v0);
   }
   __syncthreads();
   qk(Ks[0], sA);
@@ -368,13 +387,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_d64_kernel(
   // steady state: iteration t consumes S(t) (in sCur), produces S(t+1) (in sNext)
   auto body = [&](int t, f32x16 (&sCur)[2], f32x16 (&sNext)[2]) {
     const int slot = t & 1;
-    s16x8 kn = gload(kbase, kss, min(t + 2, n - 1));
-    s16x8 vn = gload(vbase, vss, t + 1);
+    const Stg kn = gload(kbase, kss, min(t + 2, n - 1));
+    const Stg vn = gload(vbase, vss, t + 1);
     qk(Ks[slot ^ 1], sNext);
     af_softmax<false>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
     pv(Vs[slot], pf, ot);
-    *reinterpret_cast<s16x8*>(&Ks[slot][k_woff]) = kn;
-    *reinterpret_cast<s16x8*>(&Vs[slot ^ 1][v_woff]) = vn;
+    lds_put(Ks[slot], k_woff, kn);
+    lds_put(Vs[slot ^ 1], v_woff, vn);
     __syncthreads();
   };
   int t = 0;
@@ -976,7 +995,17 @@ CGS_EXPORT int cgs_transpose_bf16(const void* x, void* y, int rows, int cols, lo
   return (int)hipGetLastError();
 }
 
-static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel, 3 short-KV kernel, 4 D=64 r2
+static int g_attn_variant = 0;   // 0 auto, 1 generic kernel, 2 D=64 fast kernel (256-row Q blocks), 3 short-KV
+                                 // kernel, 4 D=64 r2, 5 D=64 fast kernel with 128-row Q blocks
+static int num_cus_attn() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
+  }
+  return n;
+}
 CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
 
 static int flash_attn_impl(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, int D,
@@ -1028,12 +1057,22 @@ static int flash_attn_impl(const void* q, const void* k, const void* v, void* o,
     return (int)hipGetLastError();
   }
   if (D == 64 && !key_mask && !causal && al16 && g_attn_variant != 1 && Sk > 0) {
-    int nqb2 = (Sq + 255) / 256;
+    // 256-row Q blocks (8 waves) unless that leaves the grid under one round of the CUs and the
+    // 128-row form (4 waves, two WGs per CU) is asked for (variant 5) or auto-picked (variant 0)
+    const long long nwg256 = (long long)((Sq + 255) / 256) * B * H;
+    const bool small = g_attn_variant == 5 || (g_attn_variant == 0 && nwg256 < num_cus_attn());
+    const int rows = small ? 128 : 256;
+    int nqb2 = (Sq + rows - 1) / rows;
     long long nwg2 = (long long)nqb2 * B * H;
     if (nwg2 > 0x7fffffff) return (int)hipErrorInvalidValue;
-    attn_fwd_d64_kernel<<<dim3((unsigned)nwg2), 512, 0, stream>>>(
-        (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
-        osb, oss, osh, sl2, nqb2, lse);
+    if (small)
+      attn_fwd_d64_kernel<4><<<dim3((unsigned)nwg2), 256, 0, stream>>>(
+          (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
+          osb, oss, osh, sl2, nqb2, lse);
+    else
+      attn_fwd_d64_kernel<8><<<dim3((unsigned)nwg2), 512, 0, stream>>>(
+          (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
+          osb, oss, osh, sl2, nqb2, lse);
     return (int)hipGetLastError();
   }
   if (g_attn_variant == 2) return (int)hipErrorInvalidValue;

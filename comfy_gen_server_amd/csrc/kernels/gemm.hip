@@ -392,37 +392,60 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4,
   mc::tile<BN, NW>(al, W, ldw, M, N, K, tm * mc::BM, tn * BN, e, smem);
 }
 
-// v8: the same main loop on 128 x 128 tiles (4 waves of 64 x 64), two workgroups per CU, for the
-// short-M / short-N shapes whose 256-row grids leave most CUs idle. K % 32 == 0, 16-B aligned rows.
+// v8 / v10 / v11: the same main loop on 128 x 128 / 64 x 128 / 128 x 64 tiles (4 waves), two
+// workgroups per CU, for the short-M / short-N shapes whose 256-row grids leave most CUs idle (the
+// batch-1 UNet: M = 2048 tokens at level 2 gives 40 256x256 tiles, 160 128x128 tiles, 320 64x128
+// tiles). K % 32 == 0, 16-B aligned rows. rs / cs: the MC_EPI_LNFOLD operands.
+template <int BN, int BMV, int NS = mc::STAGES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v8_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_n, int group_m) {
+    int epi, float alpha, int tiles_n, int group_m, const float* rs, const float* cs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn;
   grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
   DenseA al{A, lda, M, {}};
-  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
-  mc::tile<128, 4, DenseA, 128>(al, W, ldw, M, N, K, tm * 128, tn * 128, e, smem);
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
+  mc::tile<BN, 4, DenseA, BMV, NS>(al, W, ldw, M, N, K, tm * BMV, tn * BN, e, smem);
 }
 
-static int gemm_v8_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
-                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                          hipStream_t stream) {
-  using Cf = mc::Cfg<128, 4, 128>;
+template <int BN, int BMV, int NS = mc::STAGES>
+static int gemm_small_tile_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                                  int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                                  float alpha, hipStream_t stream, const float* rs, const float* cs) {
+  using Cf = mc::Cfg<BN, 4, BMV, NS>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v8_kernel<BN, BMV, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Cf::LDS);
     attr_set = true;
   }
-  const int tiles_n = (N + 127) / 128;
-  const long long nwg = (long long)((M + 127) / 128) * tiles_n;
+  const int tiles_n = (N + BN - 1) / BN;
+  const long long nwg = (long long)((M + BMV - 1) / BMV) * tiles_n;
   if (nwg > 0x7fffffffLL) return (int)hipErrorInvalidValue;
-  gemm_bf16_nt_v8_kernel<<<(unsigned)nwg, 256, Cf::LDS, stream>>>((const u16*)A, (const u16*)W, (u16*)C,
-                                                                   (const u16*)bias, (const u16*)R, M, N, K, lda, ldw,
-                                                                   ldc, ldr, epi, alpha, tiles_n, g_tile_group);
+  gemm_bf16_nt_v8_kernel<BN, BMV, NS><<<(unsigned)nwg, 256, Cf::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+      tiles_n, g_tile_group, rs, cs);
   return (int)hipGetLastError();
+}
+
+// variant 8 = 128 x 128, 10 = 64 x 128, 11 = 128 x 64 (4-stage ring); 12 = 64 x 128 and 13 = 128 x 64 with
+// a 6-stage ring (72 / 72 KiB: still two workgroups per CU), 14 = 128 x 128 with 5 stages (80 KiB)
+static int gemm_v8_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream, int variant = 8, const float* rs = nullptr, const float* cs = nullptr) {
+  if (variant == 10)
+    return gemm_small_tile_launch<128, 64>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
+  if (variant == 11)
+    return gemm_small_tile_launch<64, 128>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
+  if (variant == 12)
+    return gemm_small_tile_launch<128, 64, 6>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
+  if (variant == 13)
+    return gemm_small_tile_launch<64, 128, 6>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
+  if (variant == 14)
+    return gemm_small_tile_launch<128, 128, 5>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
+  return gemm_small_tile_launch<128, 128>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
 }
 
 template <int BN, int NW>
@@ -781,7 +804,8 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&
       ((uintptr_t)bias % 8 == 0) && (long long)M * lda * 2 < (1ll << 32) && (long long)N * ldw * 2 < (1ll << 32))
     return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
-  if (v3_ok && variant == 8) return gemm_v8_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  if (v3_ok && (variant == 8 || (variant >= 10 && variant <= 14)) && !(epi & EPI_LNFOLD))
+    return gemm_v8_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, variant);
   if (v3_ok && K % 64 == 0 && variant == 5)
     return gemm_v5_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && (variant >= 3 || variant == -1)) {
@@ -842,9 +866,9 @@ CGS_EXPORT int cgs_gemm_bf16_v7ws(const void* A, const void* W, void* C, const v
 // LayerNorm folded into the GEMM (MC_EPI_LNFOLD): C = rstd_r * (A W'^T - mean_r * cs) + bias, with
 // rs = per-row (mean, rstd) of A (cgs_layernorm_stats) and W' / cs / bias precomputed by the caller
 // (W' = W * gamma, cs = rowsum(W'), bias = b + W beta). v7 only (+ optional GEGLU, split-K tail).
-CGS_EXPORT int cgs_gemm_bf16_lnfold(const void* A, const void* W, void* C, const void* bias, const float* rs,
-                                    const float* cs, int M, int N, int K, long long lda, long long ldw, long long ldc,
-                                    int epi, void* ws, long long ws_bytes, hipStream_t stream) {
+static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, const float* rs, const float* cs,
+                       int M, int N, int K, long long lda, long long ldw, long long ldc, int epi, void* ws,
+                       long long ws_bytes, int variant, hipStream_t stream) {
   const int nout = (epi & EPI_GEGLU) ? N / 2 : N;
   if (!rs || !cs || K % 64 || K < 128 || lda % 8 || ldw % 8 || ldc % 8 || nout % 8 || (epi & EPI_RESIDUAL) ||
       ((uintptr_t)A | (uintptr_t)W | (uintptr_t)C) % 16 || ((uintptr_t)bias % 8) || ((uintptr_t)cs % 16) ||
@@ -852,8 +876,25 @@ CGS_EXPORT int cgs_gemm_bf16_lnfold(const void* A, const void* W, void* C, const
     return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
   // v6 (256x160) for the N = 640 / 1280 projections (the cross-attention query), v7 otherwise
+  if (variant == 8 || (variant >= 10 && variant <= 14))
+    return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, variant,
+                          rs, cs);
   if (!(epi & EPI_GEGLU) && N % 160 == 0 && N <= 1280 && K >= 128)
     return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
   return gemm_v7_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, ws, ws_bytes, stream,
                         rs, cs);
+}
+
+CGS_EXPORT int cgs_gemm_bf16_lnfold(const void* A, const void* W, void* C, const void* bias, const float* rs,
+                                    const float* cs, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                                    int epi, void* ws, long long ws_bytes, hipStream_t stream) {
+  return gemm_lnfold(A, W, C, bias, rs, cs, M, N, K, lda, ldw, ldc, epi, ws, ws_bytes, -1, stream);
+}
+
+// Per-call kernel choice for the LayerNorm-folded GEMM (op-layer autotuner): -1 = v6 / v7 by shape,
+// 8 / 10 / 11 = the small-tile kernels (128x128 / 64x128 / 128x64) for under-filled grids.
+CGS_EXPORT int cgs_gemm_bf16_lnfold_v(const void* A, const void* W, void* C, const void* bias, const float* rs,
+                                      const float* cs, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                                      int epi, void* ws, long long ws_bytes, int variant, hipStream_t stream) {
+  return gemm_lnfold(A, W, C, bias, rs, cs, M, N, K, lda, ldw, ldc, epi, ws, ws_bytes, variant, stream);
 }

@@ -47,7 +47,9 @@ constexpr int STAGES = 4;
 // BMV = tile rows: 256, or 128 for the small-M "v8" form (128 x 128 tiles, 64 KiB of LDS -> two
 // workgroups per CU: 4x the tiles of a 256 x 256 grid where M or N is short -- SDXL at batch 1,
 // Cascade's 24^2 / 32^2 token grids -- and one workgroup's epilogue overlaps the other's main loop).
-template <int BN, int NW = 4, int BMV = BM>
+// NS: LDS ring depth (stages); NS - 2 k-steps are in flight while one is consumed. The small-tile
+// GEMMs use 5-6 (two workgroups per CU still fit) to cover L2 latency with few waves per CU.
+template <int BN, int NW = 4, int BMV = BM, int NS = STAGES>
 struct Cfg {
   static constexpr int THREADS = 64 * NW;
   static constexpr int WCOLS = NW / 2;                  // wave grid is 2 x WCOLS
@@ -56,7 +58,7 @@ struct Cfg {
   static constexpr int A_BYTES = BMV * BK * 2;          // 16 KiB at 256 rows
   static constexpr int B_BYTES = BN * BK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int LDS = STAGES * STAGE;
+  static constexpr int LDS = NS * STAGE;
   static constexpr int A_PIECES = BMV / 16 / NW;        // LDS-DMA pieces (16 rows) per wave
   static constexpr int B_PIECES = BN / 16 / NW;
   static constexpr int PER_STAGE = A_PIECES + B_PIECES; // LDS-DMA instructions per wave per stage
@@ -96,10 +98,11 @@ __device__ __forceinline__ int src_chunk(int lane) { return (lane & 3) ^ ((lane 
 // Main loop + epilogue for one 256 x BN output tile.
 //   AL: loader with  __device__ void setup(int p, int row)  (p = this wave's A piece 0..3, row =
 //       global output row, may be >= M) and  __device__ const void* src(int p, int k0) const.
-template <int BN, int NW, class AL, int BMV = BM>
+template <int BN, int NW, class AL, int BMV = BM, int NS = STAGES>
 __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K, int m0,
                                      int n0, const Epi& e, unsigned char* smem) {
-  using C = Cfg<BN, NW, BMV>;
+  using C = Cfg<BN, NW, BMV, NS>;
+  static_assert(NS >= 4, "ring depth");
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -181,23 +184,27 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   // iteration issues one stage (clamped past the end) so the body is one basic block and the vmcnt
   // count is a constant.
   bf16x8 a0[C::NI], b0[C::NJ], a1[C::NI], b1[C::NJ];
-  issue(0, 0);
-  issue(1, 1);
-  issue(2, 2);
-  wait_vmcnt<2 * C::PER_STAGE>();
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) issue(st, st);
+  wait_vmcnt<(NS - 2) * C::PER_STAGE>();
   __builtin_amdgcn_s_barrier();
   read_frags(0, 0, a0, b0);
 
+  // slots: cur = kt % NS (consumed), nxt = (kt + 1) % NS, iss = (kt + NS - 1) % NS (= slot of kt - 1)
+  int cur = 0, nxt = 1 % NS, iss = NS - 1;
   for (int kt = 0; kt < nk; ++kt) {
     mma(a0, b0);
-    read_frags(kt & 3, 1, a1, b1);
+    read_frags(cur, 1, a1, b1);
     pin_schedule(std::integral_constant<int, 0>{});
-    wait_vmcnt<C::PER_STAGE>();
+    wait_vmcnt<(NS - 3) * C::PER_STAGE>();
     __builtin_amdgcn_s_barrier();
     mma(a1, b1);
-    issue(kt + 3, (kt + 3) & 3);
-    read_frags((kt + 1) & 3, 0, a0, b0);
+    issue(kt + NS - 1, iss);
+    read_frags(nxt, 0, a0, b0);
     pin_schedule(std::integral_constant<int, C::PER_STAGE>{});
+    cur = nxt;
+    nxt = nxt + 1 == NS ? 0 : nxt + 1;
+    iss = iss + 1 == NS ? 0 : iss + 1;
   }
 
   // ---- epilogue, staged through LDS so global traffic is 16-B vectors.
@@ -214,6 +221,14 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   unsigned char* region = smem + wave * (C::WROWS * C::WN * 2);
   const int ecol = lane & 31;
   const int erow = 4 * fhalf;
+  // MC_EPI_LNFOLD (LayerNorm folded in, alpha = 1): v = rstd_row * (acc - mean_row * cs[col]); the
+  // (mean, rstd) pair of each output row comes from e.rs (rows clamped to M - 1)
+  const bool lnf = (e.flags & MC_EPI_LNFOLD) != 0;
+  auto ln_row = [&](int lrow) {
+    int grow = m0 + wm + lrow;
+    grow = grow < M ? grow : M - 1;
+    return *reinterpret_cast<const float2*>(e.rs + 2 * (long long)grow);
+  };
   if (geglu) {
     // weight rows interleaved in 16-row groups [a0..a15, g0..g15, ...]: within a 32-col MFMA tile,
     // lanes 0-15 hold 'a' and lanes 16-31 the matching 'g'; out col = tile col0 / 2 + (lane & 15).
@@ -223,6 +238,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
       const int ca = col0 + (ecol & 15);
       float ba = 0.f, bg = 0.f;
       if ((e.flags & MC_EPI_BIAS) && col0 < N) { ba = bf2f(e.bias[ca]); bg = bf2f(e.bias[ca + 16]); }
+      const float csl = (lnf && col0 < N) ? e.cs[col0 + ecol] : 0.f;   // this lane's own column (a or g)
       const int oc = 16 * j + (ecol & 15);   // col within the wave's output region
       static_for<0, C::NI>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -230,6 +246,10 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float v = t[r] * e.alpha;
+          if (lnf) {
+            const float2 st = ln_row(32 * i + (r & 3) + 8 * (r >> 2) + erow);
+            v = st.y * (t[r] - st.x * csl);
+          }
           float other = __shfl_xor(v, 16, 64);
           int row = 32 * i + (r & 3) + 8 * (r >> 2) + erow;
           if ((ecol & 16) == 0) {
@@ -246,14 +266,20 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
       const int oc = 32 * j + ecol;
       const int col = n0 + wn + oc;
       const float bv = ((e.flags & MC_EPI_BIAS) && col < N) ? bf2f(e.bias[col]) : 0.f;
+      const float csl = (lnf && col < N) ? e.cs[col] : 0.f;
 #pragma unroll
       for (int i = 0; i < C::NI; ++i) {
         const f32x16 t = acc[i][j];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           int row = 32 * i + (r & 3) + 8 * (r >> 2) + erow;
+          float v = t[r] * e.alpha;
+          if (lnf) {
+            const float2 st = ln_row(row);
+            v = st.y * (t[r] - st.x * csl);
+          }
           *reinterpret_cast<u16*>(region + row * pitch + 16 * ((oc >> 3) ^ (row & (CPR - 1))) + 2 * (oc & 7)) =
-              f2bf(t[r] * e.alpha + bv);
+              f2bf(v + bv);
         }
       }
     }

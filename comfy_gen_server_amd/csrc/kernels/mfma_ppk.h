@@ -677,6 +677,9 @@ inline int split_plan(long long T, int nk, int G, int& t_full) {
   const long long tail = T % G;
   t_full = (int)(T - tail);
   if (tail == 0 || tail * 2 > G || nk < 4) return 1;
+  // CGS_V7_SPLIT_FORCE=S (diagnostics): split every tail tile S ways when it fits (S * tail <= G)
+  static const int force = getenv("CGS_V7_SPLIT_FORCE") ? atoi(getenv("CGS_V7_SPLIT_FORCE")) : 0;
+  if (force > 1 && force * tail <= G && nk / force >= 2) return force;
   int best = 1;
   double best_cost = nk;
   const int smax = (int)std::min<long long>(std::min<long long>(G / tail, nk / 2), 16);

@@ -154,7 +154,7 @@ class AttnBlock(nn.Module):
         self.kv_mapper = nn.Sequential(nn.SiLU(), Linear(c_cond, c, dtype=dtype, device=device))
 
     def forward(self, x, kv):
-        kv = self.kv_mapper[1](F.silu(kv))
+        kv = self.kv_mapper[1](ops.silu(kv) if kv.is_contiguous() else F.silu(kv))
         return self.attention(_ln(x), kv, self_attn=self.self_attn, residual=x)
 
 
@@ -180,8 +180,10 @@ class TimestepBlock(nn.Module):
         ab = self.mapper(t[0])
         for i, name in enumerate(self.conds):      # the sum rides the GEMMs' residual epilogue
             ab = getattr(self, f"mapper_{name}")(t[i + 1], residual=ab)
-        a, b = ab[:, None, None, :].chunk(2, dim=-1)
-        return torch.addcmul(b, x, 1 + a)
+        a, b = ab.chunk(2, dim=-1)
+        if x.dim() == 4 and x.is_contiguous():
+            return ops.channel_affine_nhwc(x, 1 + a, b)
+        return torch.addcmul(b[:, None, None, :], x, 1 + a[:, None, None, :])
 
 
 def _r_embedding(r, c_r, max_positions=10000):

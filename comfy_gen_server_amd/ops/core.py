@@ -128,6 +128,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             if K % 32 == 0 and N % 8 == 0:
                 cands.append(("v4", lambda: run_hip(4)))
                 cands.append(("v8", lambda: run_hip(8)))      # 128 x 128 tiles (short M / N grids)
+                if _underfilled(M, N):    # 64x128 / 128x64 tiles, 4- and 6-stage rings (batch-1 grids)
+                    cands += [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
             cands.append(("hip", lambda: run_hip(-1)))
             if _LIB_GEMM:     # vendor GEMM only as an explicit opt-in (CGS_GEMM_LIB=1)
                 cands.append(("lib", run_lib))
@@ -136,7 +138,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")     # explicit opt-in (CGS_GEMM_LIB=1)
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8}.get(choice, -2)
+        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N)
     if be == "torch":
         count("gemm", "torch")
@@ -216,9 +218,11 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
                     cands.append(("v7", lambda: run_hip(7)))
                 cands.append(("v5", lambda: run_hip(5)))
             cands.append(("v4", lambda: run_hip(4)))
+            if _underfilled(M, N2):
+                cands += [("v8", lambda: run_hip(8))] + [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
             cands.append(("hip", lambda: run_hip(-1)))
             choice = autotune.choose(("gemm_geglu", M, N2, K, epi), cands, default="hip")
-        variant = {"v7": 7, "v5": 5, "v4": 4}.get(choice, -2)
+        variant = {"v7": 7, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N2 // 2)
     count("gemm_geglu", be)
     # reference path expects the *interleaved* weight too, undo it
@@ -303,7 +307,8 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
             return _attention_wide_mat(q, k, v)
         choice = "hip"
         # D = 64 self-attention whose 256-query blocks leave CUs idle (batch 1-2 at level 2: B*H*Sq/256
-        # < 256 workgroups): the generic kernel's 128-query blocks are a measured alternative
+        # < 256 workgroups): the 128-row form of the fast kernel and the generic kernel are measured
+        # alternatives
         if (kp is None and not causal and D == 64 and Sk > 128 and B * heads * ((Sq + 255) // 256) < 256
                 and B * heads * Sq * Sk >= (1 << 22) and _native.has_kernel("cgs_flash_attn_fwd_v")):
             def run_v(var):
@@ -313,10 +318,12 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
                     q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
                     o.stride(0), o.stride(1), D, 1.0 / math.sqrt(D), var, _stream()), "cgs_flash_attn_fwd_v")
                 return o
-            sel = autotune.choose(("attention_grid", B, heads, Sq, Sk, D),
-                                  [("d64", lambda: run_v(0)), ("generic", lambda: run_v(1))], default="d64")
+            # d64: 256-row Q blocks (8 waves); d64q128: 128-row blocks, 4 waves, two WGs per CU
+            sel = autotune.choose(("attention_grid2", B, heads, Sq, Sk, D),
+                                  [("d64", lambda: run_v(2)), ("d64q128", lambda: run_v(5)),
+                                   ("generic", lambda: run_v(1))], default="d64q128")
             count("attention", "hip")
-            return run_v(0 if sel == "d64" else 1)
+            return run_v({"d64": 2, "d64q128": 5}.get(sel, 1))
         # The vendor SDPA is a tuning candidate only on explicit request: the hot path is the
         # hand-written kernel (K02/K03), never an SDPA fallback.
         if kp is None and _ATTN_ALLOW_LIB and B * heads * Sq * Sk >= (1 << 22):
@@ -1042,13 +1049,46 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
         a = a.contiguous()
     M, N = a.shape[0], w2.shape[0]
     nout = N // 2 if geglu else N
-    out = torch.empty((M, nout), device=x.device, dtype=x.dtype)
-    ws = _v7_ws(M, N, K, x.device)
+    epi = EPI_BIAS | (EPI_GEGLU if geglu else 0)
     count("gemm_geglu" if geglu else "gemm", "hip")
-    _check(_lib().cgs_gemm_bf16_lnfold(a.data_ptr(), w2.data_ptr(), out.data_ptr(), b2.data_ptr(), rs.data_ptr(),
-                                       cs.data_ptr(), M, N, K, K, K, nout, EPI_BIAS | (EPI_GEGLU if geglu else 0),
-                                       _ptr(ws), 0 if ws is None else ws.numel(), _stream()), "cgs_gemm_bf16_lnfold")
-    return out.view(*x.shape[:-1], nout)
+
+    def run(variant):
+        out = torch.empty((M, nout), device=x.device, dtype=x.dtype)
+        ws = _v7_ws(M, N, K, x.device) if variant < 0 else None
+        _check(_lib().cgs_gemm_bf16_lnfold_v(a.data_ptr(), w2.data_ptr(), out.data_ptr(), b2.data_ptr(), rs.data_ptr(),
+                                             cs.data_ptr(), M, N, K, K, K, nout, epi, _ptr(ws),
+                                             0 if ws is None else ws.numel(), variant, _stream()),
+               "cgs_gemm_bf16_lnfold_v")
+        return out
+
+    variant = -1                  # v6 / v7 by shape
+    if _underfilled(M, N) and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
+        cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v7")
+        variant = {"v8": 8, **_SMALL_NAMES}.get(choice, -1)
+    return run(variant).view(*x.shape[:-1], nout)
+
+
+_CUS: list = []
+# small-tile GEMM variants (gemm.hip gemm_v8_launch): 10 / 11 = 64x128 / 128x64 with a 4-stage ring,
+# 12 / 13 = the same with 6 stages, 14 = 128x128 with 5 stages
+_SMALL_TILE = (10, 11, 12, 13, 14)
+_SMALL_NAMES = {f"v{v}": v for v in _SMALL_TILE}
+
+
+def _num_cus() -> int:
+    if not _CUS:
+        try:
+            _CUS.append(int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count))
+        except Exception:
+            _CUS.append(256)
+    return _CUS[0]
+
+
+def _underfilled(M: int, N: int) -> bool:
+    """A 128 x 128 grid of this output is under two workgroups per CU: the small-tile kernels (v10 /
+    v11) join the autotune candidates (batch-1 and Stable Cascade Stage C token counts)."""
+    return ((M + 127) // 128) * ((N + 127) // 128) < 2 * _num_cus()
 
 
 def _feather_mask(h: int, w: int, feather: int, device) -> torch.Tensor:
@@ -1112,6 +1152,24 @@ def region_normalize(out: torch.Tensor, div: torch.Tensor, dtype=None) -> torch.
                                            _stream()), "cgs_region_normalize")
         return y
     return (out / div).to(dtype)
+
+
+def channel_affine_nhwc(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
+    """y = x * scale[n, c] + shift[n, c] for NHWC ``x`` [N, H, W, C] and [N, C] coefficients (Stable
+    Cascade TimestepBlock ``x * (1 + a) + b``, ``comfy/ldm/cascade/common.py``); the device path is the
+    GroupNorm apply kernel with these coefficients."""
+    be = backend_for("channel_affine", x, "cgs_channel_affine_nhwc")
+    N, C = x.shape[0], x.shape[-1]
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() and C % 8 == 0:
+        count("channel_affine", "hip")
+        ab = torch.stack([scale.reshape(N, C).float(), shift.reshape(N, C).float()], dim=-1).contiguous()
+        y = torch.empty_like(x)
+        _check(_lib().cgs_channel_affine_nhwc(x.data_ptr(), ab.data_ptr(), y.data_ptr(), N, x.numel() // (N * C), C,
+                                              0, _DT[x.dtype], _stream()), "cgs_channel_affine_nhwc")
+        return y
+    count("channel_affine", "torch")
+    shp = (N,) + (1,) * (x.dim() - 2) + (C,)
+    return (x.float() * scale.reshape(shp).float() + shift.reshape(shp).float()).to(x.dtype)
 
 
 def fused_bias_act(x: torch.Tensor, bias: torch.Tensor | None, negative_slope: float = 0.2,

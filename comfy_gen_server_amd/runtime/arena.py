@@ -85,8 +85,17 @@ class WeightArena:
         return t.device == self.device and self.base <= t.data_ptr() < self.base + self.slab.numel()
 
     def _view(self, off: int, t: torch.Tensor) -> torch.Tensor:
-        nbytes = t.numel() * t.element_size()
-        return self.slab[off:off + nbytes].view(t.dtype).view(t.shape)
+        """A contiguous ``t``-shaped tensor on the slab's storage at byte ``off``, created in the same
+        inference mode as ``t``: ``t.data = view`` with mismatched inference-ness leaves a tensor
+        that no view op accepts ("Inference tensors do not track version counter")."""
+        es = t.element_size()
+        stride, acc = [], 1
+        for d in reversed(t.shape):
+            stride.append(acc)
+            acc *= max(int(d), 1)
+        with torch.inference_mode(t.is_inference()):
+            return torch.empty(0, dtype=t.dtype, device=self.device).set_(
+                self.slab.untyped_storage(), off // es, tuple(t.shape), tuple(reversed(stride)))
 
     def place_module(self, module: torch.nn.Module) -> int:
         """Move every parameter / buffer of ``module`` into the slab (shared tensors once); raises
@@ -111,7 +120,8 @@ class WeightArena:
                     if off < 0:
                         raise ArenaFull(f"weight arena full: {nbytes} B for {name} ({self.stats()})")
                     v = self._view(off, t)
-                    v.copy_(t.data)
+                    with torch.inference_mode(t.is_inference()):
+                        v.copy_(t.data)
                     seen[key] = v
                     new.append((name, t, t.data))
                     t.data = v
@@ -133,7 +143,8 @@ class WeightArena:
             table = self.blocks.pop(id(module), {})
             for name, t in list(module.named_parameters(recurse=True)) + list(module.named_buffers(recurse=True)):
                 if t is not None and self.owns(t):
-                    t.data = t.data.to(device_to, copy=True)
+                    with torch.inference_mode(t.is_inference()):
+                        t.data = t.data.to(device_to, copy=True)
             for off in table.values():
                 self.alloc.free(off)
                 freed += 1

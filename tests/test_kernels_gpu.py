@@ -170,7 +170,9 @@ def test_attention_d64_variants(cuda, attn_variant, B, H, Sq, Sk, spike):
     assert _rel(o, ref) < 2e-2
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8], ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160", "v7ppk", "v8t128"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 14],
+                ids=["v1", "v2", "v3w4", "v3w8", "v5pp", "v6pp160", "v7ppk", "v8t128", "v10t64x128", "v11t128x64",
+                     "v12t64x128s6", "v13t128x64s6", "v14t128s5"])
 def gemm_variant(request):
     lib = _native.load_kernels()
     lib.cgs_gemm_set_variant(request.param)
@@ -384,6 +386,26 @@ def test_attention_lse_and_ring_merge(cuda, B, H, S, Sk, D):
     wa, wb = torch.exp(l1 - m), torch.exp(l2 - m)
     merged = ((o1 * wa + o2 * wb) / (wa + wb)).reshape(B, S, H * D)
     assert _rel(merged, core.attention_reference(q.float(), k.float(), v.float(), H)) < 2e-2
+
+
+@pytest.mark.parametrize("B,H,S,Sk", [(1, 20, 1024, 1024), (2, 10, 4096, 4096), (1, 3, 300, 77), (1, 5, 1000, 333),
+                                      (2, 2, 129, 1000)])
+@pytest.mark.parametrize("variant", [2, 5])
+def test_attention_d64_q_block_forms(cuda, B, H, S, Sk, variant):
+    """D = 64 fast kernel with 256-row (variant 2, 8 waves) and 128-row (variant 5, 4 waves, two WGs
+    per CU: the batch-1 form) Q blocks vs the fp32 reference."""
+    torch.manual_seed(5)
+    D = 64
+    q = torch.randn(B, S, H * D, device=cuda).to(torch.bfloat16)
+    k = torch.randn(B, Sk, H * D, device=cuda).to(torch.bfloat16)
+    v = torch.randn(B, Sk, H * D, device=cuda).to(torch.bfloat16)
+    o = torch.empty_like(q)
+    lib = core._lib()
+    st = lambda t, L: (L * H * D, H * D, D)   # noqa: E731  (batch, seq, head) strides in elements
+    rc = lib.cgs_flash_attn_fwd_v(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, S, Sk, D,
+                                  *st(q, S), *st(k, Sk), *st(v, Sk), *st(o, S), D ** -0.5, variant, core._stream())
+    assert rc == 0
+    assert _rel(o, core.attention_reference(q.float(), k.float(), v.float(), H)) < 2e-2
 
 
 def test_softmax2_and_transpose_kernels(cuda):
@@ -650,6 +672,37 @@ def test_layernorm_folded_gemm(cuda, M, C, N, geglu):
         w2, cs, b2 = ops.lnfold_weights(w, None, gamma, beta)
         y = ops.linear_lnfold(x, rs, w2, cs, b2)
         ref = h
+    assert _rel(y, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("M,C,N,geglu", [(2048, 1280, 3840, False), (2048, 1280, 10240, True), (8192, 640, 1920, False),
+                                         (300, 640, 1280, False), (1152, 2048, 4096, True)])
+@pytest.mark.parametrize("variant", [8, 10, 11, 12, 13, 14])
+def test_layernorm_folded_gemm_small_tiles(cuda, M, C, N, geglu, variant):
+    """The LayerNorm fold on the small-tile kernels (128x128 / 64x128 / 128x64) the batch-1 UNet's
+    under-filled grids autotune to: same fp32 reference as test_layernorm_folded_gemm."""
+    torch.manual_seed(1)
+    x = (torch.randn(M, C, device=cuda) * 3 + 1.5).to(torch.bfloat16)
+    gamma = (torch.rand(C, device=cuda) + 0.5).to(torch.bfloat16)
+    beta = (torch.randn(C, device=cuda) * 0.2).to(torch.bfloat16)
+    w = (torch.randn(N, C, device=cuda) / math.sqrt(C)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16)
+    rs = ops.layernorm_stats(x, 1e-5)
+    h = F.layer_norm(x.float(), (C,), gamma.float(), beta.float(), 1e-5) @ w.float().t() + b.float()
+    if geglu:
+        w2, cs, b2 = ops.lnfold_weights(core.geglu_interleave(w), core.geglu_interleave(b), gamma, beta)
+        a, g = h.chunk(2, dim=-1)
+        ref = a * F.gelu(g)
+    else:
+        w2, cs, b2 = ops.lnfold_weights(w, b, gamma, beta)
+        ref = h
+    nout = N // 2 if geglu else N
+    y = torch.empty(M, nout, device=cuda, dtype=torch.bfloat16)
+    lib = _native.load_kernels()
+    assert lib.cgs_gemm_bf16_lnfold_v(x.data_ptr(), w2.data_ptr(), y.data_ptr(), b2.data_ptr(), rs.data_ptr(),
+                                      cs.data_ptr(), M, N, C, C, C, nout,
+                                      core.EPI_BIAS | (core.EPI_GEGLU if geglu else 0), None, 0, variant,
+                                      core._stream()) == 0
     assert _rel(y, ref) < 1.5e-2
 
 

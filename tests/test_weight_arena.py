@@ -88,6 +88,27 @@ def test_weight_arena_place_forward_evict():
         assert torch.equal(m(x, t, context=ctx), ref)
 
 
+def test_weight_arena_inference_mode_module():
+    """A model built under inference_mode (bench / synth pipelines) placed from normal mode: its
+    buffers stay usable by view ops in both modes (a plain ``.data`` swap onto a normal slab view
+    broke every later ``sigmas[-1]``: "Inference tensors do not track version counter")."""
+    from comfy_gen_server_amd.sampling.model_sampling import ModelSamplingDiscrete
+    with torch.inference_mode():
+        m = _tiny()
+        ms = ModelSamplingDiscrete()
+    holder = torch.nn.Module()
+    holder.unet, holder.ms = m, ms
+    nbytes = sum(t.numel() * t.element_size() for t in list(holder.parameters()) + list(holder.buffers()))
+    wa = A.WeightArena(nbytes * 2, "cpu")
+    assert wa.place_module(holder) > 0
+    assert wa.owns(ms.sigmas) and ms.sigmas.is_inference()
+    want = float(ms.sigmas[-1])          # view op outside inference mode
+    with torch.inference_mode():
+        assert float(ms.sigma_max) == want
+        out = m(torch.randn(1, 4, 16, 16), torch.tensor([10.0]), context=torch.randn(1, 5, 64))
+    assert torch.isfinite(out).all()
+
+
 def test_weight_arena_full_rolls_back():
     m = _tiny()
     wa = A.WeightArena(64 * 1024, "cpu")
