@@ -231,9 +231,12 @@ __device__ __forceinline__ float af_xmax(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-template <bool TAIL>
+// MSUM: the row sums come from the P.V MFMAs (an all-ones A operand into ``lsum``, see
+// attn_fwd_d64_kernel) instead of 32 v_add_f32 per lane per tile; only the rescale touches lsum.
+template <bool TAIL, bool MSUM = false>
 __device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x16 (&ot)[2], float& m_run,
-                                           float& l_run, float c, int key0, int Sk, int hf) {
+                                           float& l_run, float c, int key0, int Sk, int hf,
+                                           f32x16* lsum = nullptr) {
   if (TAIL) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -256,6 +259,10 @@ __device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) ot[dt][r] *= alpha;
+    if constexpr (MSUM) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) (*lsum)[r] *= alpha;
+    }
   }
   const float nm = -m_run;
   float ps = 0.f;
@@ -264,10 +271,10 @@ __device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][r], c, nm));
-      ps += p;
+      if constexpr (!MSUM) ps += p;
       pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p;
     }
-  l_run += ps;
+  if constexpr (!MSUM) l_run += ps;
 }
 
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
@@ -315,13 +322,22 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
   }
   const int n = (Sk + 63) >> 6;
   struct Stg { s16x8 v[LPT]; };
-  auto gload = [&](const u16* base, long long ss, int t) -> Stg {
+  // per-lane row offsets computed once; per tile only the uniform t * 64 * stride (scalar) is added
+  // (keys past Sk read the last row: they are masked in the softmax)
+  long long koff[LPT], voff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    koff[i] = (long long)st_key[i] * kss + st_c * 8;
+    voff[i] = (long long)st_key[i] * vss + st_c * 8;
+  }
+  const long long kclamp = (long long)(Sk - 1) * kss + st_c * 8, vclamp = (long long)(Sk - 1) * vss + st_c * 8;
+  auto gload = [&](const u16* base, long long ss, const long long (&off)[LPT], long long clampo, int t) -> Stg {
     Stg r;
+    const long long tb = (long long)(t * 64) * ss;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      int key = t * 64 + st_key[i];
-      key = key < Sk ? key : Sk - 1;   // clamp: tail rows are masked in the softmax
-      r.v[i] = *reinterpret_cast<const s16x8*>(base + (long long)key * ss + st_c * 8);
+      const long long o = (t * 64 + st_key[i] < Sk) ? tb + off[i] : clampo;
+      r.v[i] = *reinterpret_cast<const s16x8*>(base + o);
     }
     return r;
   };
@@ -346,11 +362,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     }
   };
   const int i16 = lane & 15;
+  // row sums on the matrix core: an all-ones A operand turns P into sum_k P[k][q] in every row of
+  // lsum (bf16-rounded P, the same weights the numerator uses)
+  const bf16x8 ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                       (__bf16)1.f};
+  f32x16 lsum = f32x16{};
   auto pv = [&](const u16* Vt, const bf16x8 (&pf)[4], f32x16 (&ot)[2]) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
+        lsum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kt * 2 + st], lsum, 0, 0, 0);
         const int row0 = kt * 32 + 16 * st + 4 * hf + (i16 >> 2);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
@@ -374,9 +396,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
 
   // prologue: K(0) -> slot 0, K(1) -> slot 1, V(0) -> slot 0; S(0)
   {
-    const Stg k0 = gload(kbase, kss, 0);
-    const Stg k1 = gload(kbase, kss, n > 1 ? 1 : 0);
-    const Stg v0 = gload(vbase, vss, 0);
+    const Stg k0 = gload(kbase, kss, koff, kclamp, 0);
+    const Stg k1 = gload(kbase, kss, koff, kclamp, n > 1 ? 1 : 0);
+    const Stg v0 = gload(vbase, vss, voff, vclamp, 0);
     lds_put(Ks[0], k_woff, k0);
     lds_put(Ks[1], k_woff, k1);
     lds_put(Vs[0], v_woff, v0);
@@ -387,10 +409,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
   // steady state: iteration t consumes S(t) (in sCur), produces S(t+1) (in sNext)
   auto body = [&](int t, f32x16 (&sCur)[2], f32x16 (&sNext)[2]) {
     const int slot = t & 1;
-    const Stg kn = gload(kbase, kss, min(t + 2, n - 1));
-    const Stg vn = gload(vbase, vss, t + 1);
+    const Stg kn = gload(kbase, kss, koff, kclamp, min(t + 2, n - 1));
+    const Stg vn = gload(vbase, vss, voff, vclamp, t + 1);
     qk(Ks[slot ^ 1], sNext);
-    af_softmax<false>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
+    af_softmax<false, true>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
     pv(Vs[slot], pf, ot);
     lds_put(Ks[slot], k_woff, kn);
     lds_put(Vs[slot ^ 1], v_woff, vn);
@@ -404,14 +426,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
   if (t + 1 < n) {   // one full iteration left before the last tile
     body(t, sA, sB);
     ++t;
-    af_softmax<true>(sB, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
+    af_softmax<true, true>(sB, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
   } else {
-    af_softmax<true>(sA, pf, ot, m_run, l_run, c, t * 64, Sk, hf);
+    af_softmax<true, true>(sA, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
   }
   pv(Vs[t & 1], pf, ot);
 
-  // epilogue: O[q][d] = O^T[d][q] / l
-  float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  // epilogue: O[q][d] = O^T[d][q] / l (every row of lsum holds the full key sum of this lane's q)
+  float l_tot = lsum[0];
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (lse && q_ok && hf == 0)
     lse[((long long)b * H + h) * Sq + q_row] = l_tot > 0.f ? (m_run + __log2f(l_tot)) * 0.69314718055994531f : -INFINITY;

@@ -92,7 +92,15 @@ def test_lora_merge_product_on_hip(cuda):
     w = torch.randn(640, 1280, generator=g)
     up, down = torch.randn(640, 32, generator=g) * 0.1, torch.randn(32, 1280, generator=g) * 0.1
     ref = calculate_weight([(0.8, ("lora", (up, down, 16.0, None, None)), 1.0)], w.clone(), "k")
+    # bf16 base weight: the rank-r product runs on the HIP GEMM (its one bf16 rounding is below the
+    # merged bf16 weight's own)
     ops.reset_stats()
-    out = calculate_weight([(0.8, ("lora", (up.to(cuda), down.to(cuda), 16.0, None, None)), 1.0)], w.to(cuda), "k")
+    out = calculate_weight([(0.8, ("lora", (up.to(cuda), down.to(cuda), 16.0, None, None)), 1.0)], w.to(cuda), "k",
+                           base_dtype=torch.bfloat16)
     assert ops.stats().get(("gemm", "hip"), 0) == 1
     assert torch.allclose(out.cpu(), ref, atol=2e-3, rtol=1e-3)
+    # fp32 base weight: fp32 torch.mm like the reference, no bf16 GEMM
+    ops.reset_stats()
+    out32 = calculate_weight([(0.8, ("lora", (up.to(cuda), down.to(cuda), 16.0, None, None)), 1.0)], w.to(cuda), "k")
+    assert ops.stats().get(("gemm", "hip"), 0) == 0
+    assert torch.allclose(out32.cpu(), ref, atol=2e-5, rtol=1e-5)
