@@ -163,7 +163,7 @@ KERNEL_SIGNATURES = {
     "cgs_softmax2_f32_bf16": [_P, _P, _L, _I, _L, _L, _P],             # x(f32), y(bf16), rows, cols, ldx, ldy
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy
     "cgs_abort_stream_capture": [_P],
-    "cgs_channel_affine_nhwc": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "cgs_channel_affine2": [_P, _P, _P, _L, _P, _I, _I, _I, _F, _I, _P],
 }
 
 

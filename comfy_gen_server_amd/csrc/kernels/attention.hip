@@ -403,28 +403,37 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     lds_put(Ks[1], k_woff, k1);
     lds_put(Vs[0], v_woff, v0);
   }
+  // two register stages: the K / V rows written to LDS at the end of tile t were loaded during tile
+  // t - 1, so a global load has a whole tile of compute (not just the rest of its own tile) to land
+  Stg kq[2], vq[2];
+  kq[0] = gload(kbase, kss, koff, kclamp, min(2, n - 1));
+  vq[0] = gload(vbase, vss, voff, vclamp, min(1, n - 1));
   __syncthreads();
   qk(Ks[0], sA);
 
-  // steady state: iteration t consumes S(t) (in sCur), produces S(t+1) (in sNext)
-  auto body = [&](int t, f32x16 (&sCur)[2], f32x16 (&sNext)[2]) {
+  // steady state: iteration t consumes S(t) (in sCur), produces S(t+1) (in sNext); it loads
+  // K(t+3) / V(t+2) into register set LD and writes K(t+2) / V(t+1) from set WR (= t & 1)
+  auto body = [&](int t, f32x16 (&sCur)[2], f32x16 (&sNext)[2], auto ldc) {
+    constexpr int LD = decltype(ldc)::value, WR = LD ^ 1;
     const int slot = t & 1;
-    const Stg kn = gload(kbase, kss, koff, kclamp, min(t + 2, n - 1));
-    const Stg vn = gload(vbase, vss, voff, vclamp, t + 1);
+    kq[LD] = gload(kbase, kss, koff, kclamp, min(t + 3, n - 1));
+    vq[LD] = gload(vbase, vss, voff, vclamp, min(t + 2, n - 1));
     qk(Ks[slot ^ 1], sNext);
     af_softmax<false, true>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
     pv(Vs[slot], pf, ot);
-    lds_put(Ks[slot], k_woff, kn);
-    lds_put(Vs[slot ^ 1], v_woff, vn);
+    lds_put(Ks[slot], k_woff, kq[WR]);
+    lds_put(Vs[slot ^ 1], v_woff, vq[WR]);
     __syncthreads();
   };
+  using L1 = std::integral_constant<int, 1>;
+  using L0 = std::integral_constant<int, 0>;
   int t = 0;
   for (; t + 2 < n; t += 2) {
-    body(t, sA, sB);
-    body(t + 1, sB, sA);
+    body(t, sA, sB, L1{});
+    body(t + 1, sB, sA, L0{});
   }
   if (t + 1 < n) {   // one full iteration left before the last tile
-    body(t, sA, sB);
+    body(t, sA, sB, L1{});
     ++t;
     af_softmax<true, true>(sB, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
   } else {

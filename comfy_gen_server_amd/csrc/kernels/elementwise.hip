@@ -124,7 +124,7 @@ __global__ void geglu_kernel(const u16* __restrict__ x, u16* __restrict__ out, i
     s16x8 g = *reinterpret_cast<const s16x8*>(x + r * 2 * N + N + c);
     s16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(bf2f((u16)a[j]) * gelu_f(bf2f((u16)g[j])));
+    for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(bf2f((u16)a[j]) * gelu_sig(bf2f((u16)g[j])));
     *reinterpret_cast<s16x8*>(out + r * N + c) = o;
   }
 }

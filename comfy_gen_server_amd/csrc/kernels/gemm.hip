@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(
           if (row < M) {
             float a = acc[i][2 * jp][r] * alpha + ba;
             float g = acc[i][2 * jp + 1][r] * alpha + bg;
-            C[row * ldc + oc] = f2bf(a * gelu_f(g));
+            C[row * ldc + oc] = f2bf(a * gelu_sig(g));
           }
         }
       }
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_nt_v2_kernel(
           if (row < M) {
             float a = acc[i][2 * jp][r] * alpha + ba;
             float g = acc[i][2 * jp + 1][r] * alpha + bg;
-            C[row * ldc + oc] = f2bf(a * gelu_f(g));
+            C[row * ldc + oc] = f2bf(a * gelu_sig(g));
           }
         }
     }

@@ -251,12 +251,13 @@ __global__ void __launch_bounds__(256) grn2_sumsq_kernel(const u16* __restrict__
   if (ch < nchunk) {
     const int r0 = sl * rows_per, r1 = min(HW, r0 + rows_per);
     const u16* xb = x + (size_t)n * HW * C + ch * 8;
-    for (int r = r0 + rg; r < r1; r += 4) {
+#pragma unroll 4
+    for (int r = r0 + rg; r < r1; r += 4) {   // unrolled: several row loads in flight per thread
       const s16x8 v = *reinterpret_cast<const s16x8*>(xb + (size_t)r * C);
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         f32x2_t f = {cvt_in<DT>((u16)v[j]), cvt_in<DT>((u16)v[j + 1])};
-        if (GELU) f = gelu_fast2(f);     // A&S 7.1.26 erf (|err| <= 1.5e-7): erff made GRN ALU-bound
+        if (GELU) f = gelu_sig2(f);      // sigmoid-quintic GELU (|err| <= 2.6e-5): erff made GRN ALU-bound
         acc[j] += f.x * f.x;
         acc[j + 1] += f.y * f.y;
       }
@@ -278,7 +279,8 @@ __global__ void __launch_bounds__(1024) grn2_finalize_kernel(const float* __rest
   __shared__ float red[16];
   const int n = blockIdx.x;
   float sum = 0.f;
-  for (int c = threadIdx.x; c < C; c += 1024) {
+#pragma unroll 4
+  for (int c = threadIdx.x; c < C; c += 1024) {   // unrolled: loads of several channels in flight
     const float4* p = reinterpret_cast<const float4*>(part + ((size_t)n * C + c) * S);
     float ss = 0.f;
     for (int q = 0; q < S / 4; ++q) {
@@ -320,7 +322,7 @@ __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       f32x2_t f = {cvt_in<DT>((u16)v[j]), cvt_in<DT>((u16)v[j + 1])};
-      if (GELU) f = gelu_fast2(f);
+      if (GELU) f = gelu_sig2(f);
       o[j] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j]) + f.x * (1.f + cvt_in<DT>((u16)gm[j]) * nv[j]));
       o[j + 1] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j + 1]) + f.y * (1.f + cvt_in<DT>((u16)gm[j + 1]) * nv[j + 1]));
     }
@@ -858,6 +860,51 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
     if (pre_gelu) { CGS_GRN2(CGS_F16, true); } else { CGS_GRN2(CGS_F16, false); }
   }
 #undef CGS_GRN2
+  return (int)hipGetLastError();
+}
+
+// Per-(image, channel) affine on NHWC straight from a [N, ld] activation-dtype coefficient tensor:
+// y = x * (add + s[n][c]) + t[n][c] (Stable Cascade TimestepBlock x * (1 + a) + b with a, b the two
+// halves of the mapper GEMM output, comfy/ldm/cascade/common.py TimestepBlock) -- no fp32 cast /
+// stack of the coefficients on the host side of the op.
+template <int DT>
+__global__ void __launch_bounds__(256) chan_affine_kernel(const u16* __restrict__ x, const u16* __restrict__ sc,
+                                                          const u16* __restrict__ sh, long long ld,
+                                                          u16* __restrict__ y, long long chunks, int HW, int C,
+                                                          float add) {
+  const unsigned cpr = (unsigned)C >> 3;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < chunks; i += (long long)gridDim.x * 256) {
+    const unsigned iu = (unsigned)i;
+    const unsigned row = iu / cpr;
+    const int c0 = (int)(iu - row * cpr) * 8;
+    const long long n = row / (unsigned)HW;
+    const s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
+    const s16x8 a = *reinterpret_cast<const s16x8*>(sc + n * ld + c0);
+    const s16x8 b = *reinterpret_cast<const s16x8*>(sh + n * ld + c0);
+    s16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o[j] = (short)cvt_out<DT>(__builtin_fmaf(cvt_in<DT>((u16)v[j]), add + cvt_in<DT>((u16)a[j]), cvt_in<DT>((u16)b[j])));
+    reinterpret_cast<s16x8*>(y)[i] = o;
+  }
+}
+
+CGS_EXPORT int cgs_channel_affine2(const void* x, const void* scale, const void* shift, long long ld, void* y, int N,
+                                   int HW, int C, float add, int dtype, hipStream_t stream) {
+  if (N <= 0 || HW <= 0) return 0;
+  if (C % 8 || ld % 8 || dtype == CGS_F32 ||
+      (((uintptr_t)x | (uintptr_t)y | (uintptr_t)scale | (uintptr_t)shift) & 15))
+    return (int)hipErrorInvalidValue;
+  const long long chunks = (long long)N * HW * (C / 8);
+  if (chunks >= (1LL << 32)) return (int)hipErrorInvalidValue;
+  long long nb = (chunks + 255) / 256;
+  const int blocks = (int)(nb > 16384 ? 16384 : nb);
+  if (dtype == CGS_BF16)
+    chan_affine_kernel<CGS_BF16><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)scale, (const u16*)shift, ld,
+                                                             (u16*)y, chunks, HW, C, add);
+  else
+    chan_affine_kernel<CGS_F16><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)scale, (const u16*)shift, ld,
+                                                            (u16*)y, chunks, HW, C, add);
   return (int)hipGetLastError();
 }
 

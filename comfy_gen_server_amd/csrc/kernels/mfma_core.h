@@ -255,7 +255,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
           if ((ecol & 16) == 0) {
             float gl = other + bg;
             *reinterpret_cast<u16*>(region + row * pitch + 16 * ((oc >> 3) ^ (row & (CPR - 1))) + 2 * (oc & 7)) =
-                f2bf((v + ba) * gelu_f(gl));
+                f2bf((v + ba) * gelu_sig(gl));
           }
         }
       });

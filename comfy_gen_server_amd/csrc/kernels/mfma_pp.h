@@ -208,7 +208,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
           const float a = acc[i][2 * p][r] * e.alpha + ba;
           const float g = acc[i][2 * p + 1][r] * e.alpha + bg;
           *reinterpret_cast<u16*>(region + row * pitch + 16 * ((oc >> 3) ^ (row & (CPR - 1))) + 2 * (oc & 7)) =
-              f2bf(a * gelu_f(g));
+              f2bf(a * gelu_sig(g));
         }
     });
   } else {

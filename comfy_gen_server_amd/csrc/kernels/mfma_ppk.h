@@ -128,7 +128,6 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   // desynchronisation probes -- 2, 4 and 8 phases per XCD, with and without full-line stores --
   // measured slower at every spread and were removed: profiles/r03_gemm_epilogue.md.)
   const bool nostore = (sp.dbg & 8) != 0;
-  const bool gelu_as = (sp.dbg & 256) != 0;   // GEGLU: the A&S-erf GELU (round-2 epilogue)
   constexpr bool legacy = !kFullLine;         // register epilogue: 16 B per lane, 16 rows x 64 B per store
 
   // unit -> (tile origin, K range, partial slot or -1)
@@ -329,13 +328,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             const float4 ba = bv[nq][0], bg = bv[nq][1];
             f32x2_t g01 = f32x2_t{g[0], g[1]} * e.alpha + f32x2_t{bg.x, bg.y};
             f32x2_t g23 = f32x2_t{g[2], g[3]} * e.alpha + f32x2_t{bg.z, bg.w};
-            if (gelu_as) {
-              g01 = gelu_fast2(g01);
-              g23 = gelu_fast2(g23);
-            } else {
-              g01 = gelu_sig2(g01);
-              g23 = gelu_sig2(g23);
-            }
+            g01 = gelu_sig2(g01);
+            g23 = gelu_sig2(g23);
             const f32x2_t o01 = (f32x2_t{a[0], a[1]} * e.alpha + f32x2_t{ba.x, ba.y}) * g01;
             const f32x2_t o23 = (f32x2_t{a[2], a[3]} * e.alpha + f32x2_t{ba.z, ba.w}) * g23;
             h[nq] = pack4_bf16(o01.x, o01.y, o23.x, o23.y);

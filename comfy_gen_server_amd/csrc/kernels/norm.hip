@@ -293,31 +293,6 @@ CGS_EXPORT int cgs_groupnorm_nhwc_dual(const void* x, const void* x2, int C1, vo
   return groupnorm_impl(x, x2, C1, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream);
 }
 
-// Per-(image, channel) affine on NHWC: y = x * ab[n][c].a + ab[n][c].b (optionally SiLU) -- the
-// GroupNorm apply pass with caller-provided coefficients (Stable Cascade TimestepBlock:
-// x * (1 + a) + b, reference comfy/ldm/cascade/common.py TimestepBlock.forward).
-CGS_EXPORT int cgs_channel_affine_nhwc(const void* x, const float* ab, void* y, int N, int HW, int C, int silu,
-                                       int dtype, hipStream_t stream) {
-  if (C % 8 || (dtype != CGS_BF16 && dtype != CGS_F16)) return (int)hipErrorInvalidValue;
-  const int cpr = C / 8;
-  const long long rows_total = (long long)N * HW;
-  if (rows_total == 0) return 0;
-  if (rows_total * cpr >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  long long chunks = rows_total * cpr;
-  long long nbk = (chunks + 255) / 256;
-  int blocks = (int)(nbk < 8192 ? nbk : 8192);
-  int rows_per_iter = (blocks * 256) / cpr;
-  if (rows_per_iter < 1) rows_per_iter = 1, blocks = (cpr + 255) / 256;
-  if (dtype == CGS_BF16) {
-    if (silu) gn_apply_kernel<CGS_BF16, true><<<blocks, 256, 0, stream>>>((const u16*)x, nullptr, C, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
-    else gn_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)x, nullptr, C, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
-  } else {
-    if (silu) gn_apply_kernel<CGS_F16, true><<<blocks, 256, 0, stream>>>((const u16*)x, nullptr, C, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
-    else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, nullptr, C, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
-  }
-  return (int)hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------------------------
 // LayerNorm over the last dim; one wave per row.
 // ------------------------------------------------------------------------------------------------

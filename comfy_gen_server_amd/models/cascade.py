@@ -182,7 +182,7 @@ class TimestepBlock(nn.Module):
             ab = getattr(self, f"mapper_{name}")(t[i + 1], residual=ab)
         a, b = ab.chunk(2, dim=-1)
         if x.dim() == 4 and x.is_contiguous():
-            return ops.channel_affine_nhwc(x, 1 + a, b)
+            return ops.channel_affine_nhwc(x, a, b, add=1.0)
         return torch.addcmul(b[:, None, None, :], x, 1 + a[:, None, None, :])
 
 

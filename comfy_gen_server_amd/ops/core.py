@@ -1154,22 +1154,25 @@ def region_normalize(out: torch.Tensor, div: torch.Tensor, dtype=None) -> torch.
     return (out / div).to(dtype)
 
 
-def channel_affine_nhwc(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
-    """y = x * scale[n, c] + shift[n, c] for NHWC ``x`` [N, H, W, C] and [N, C] coefficients (Stable
-    Cascade TimestepBlock ``x * (1 + a) + b``, ``comfy/ldm/cascade/common.py``); the device path is the
-    GroupNorm apply kernel with these coefficients."""
-    be = backend_for("channel_affine", x, "cgs_channel_affine_nhwc")
+def channel_affine_nhwc(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, add: float = 0.0) -> torch.Tensor:
+    """y = x * (add + scale[n, c]) + shift[n, c] for NHWC ``x`` [N, H, W, C] and [N, C] coefficient
+    views in x's dtype (row stride free: e.g. the two halves of one [N, 2C] GEMM output). Stable
+    Cascade TimestepBlock ``x * (1 + a) + b`` (``comfy/ldm/cascade/common.py``) with ``add = 1``."""
+    be = backend_for("channel_affine", x, "cgs_channel_affine2")
     N, C = x.shape[0], x.shape[-1]
-    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() and C % 8 == 0:
+    if (be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() and C % 8 == 0
+            and scale.dtype == shift.dtype == x.dtype and scale.dim() == 2 and shift.dim() == 2
+            and scale.stride(1) == 1 and shift.stride(1) == 1 and scale.stride(0) == shift.stride(0)
+            and scale.stride(0) % 8 == 0 and scale.data_ptr() % 16 == 0 and shift.data_ptr() % 16 == 0):
         count("channel_affine", "hip")
-        ab = torch.stack([scale.reshape(N, C).float(), shift.reshape(N, C).float()], dim=-1).contiguous()
         y = torch.empty_like(x)
-        _check(_lib().cgs_channel_affine_nhwc(x.data_ptr(), ab.data_ptr(), y.data_ptr(), N, x.numel() // (N * C), C,
-                                              0, _DT[x.dtype], _stream()), "cgs_channel_affine_nhwc")
+        _check(_lib().cgs_channel_affine2(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), scale.stride(0),
+                                          y.data_ptr(), N, x.numel() // (N * C), C, float(add), _DT[x.dtype],
+                                          _stream()), "cgs_channel_affine2")
         return y
     count("channel_affine", "torch")
     shp = (N,) + (1,) * (x.dim() - 2) + (C,)
-    return (x.float() * scale.reshape(shp).float() + shift.reshape(shp).float()).to(x.dtype)
+    return (x.float() * (add + scale.reshape(shp).float()) + shift.reshape(shp).float()).to(x.dtype)
 
 
 def fused_bias_act(x: torch.Tensor, bias: torch.Tensor | None, negative_slope: float = 0.2,

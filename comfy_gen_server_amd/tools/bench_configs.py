@@ -14,6 +14,7 @@ Prints one JSON line per measurement: {"config", "batch", "sec_per_job", "sec_pe
 from __future__ import annotations
 
 import argparse
+import os
 import copy
 import json
 import sys
@@ -56,6 +57,21 @@ def bench_sdxl_b1(reps):
     best, mean = _timed(run, reps)
     _emit("sdxl_b1", 1, best, mean, steps=20, resolution=1024)
     return patcher, clip, vae
+
+
+def _aten_table(run, top=25):
+    """Which ATen (non-native) device ops a run launches, with the Python line that issued them
+    (CGS_TORCH_PROFILE=1): the glue the op layer has not absorbed yet."""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        run()
+        torch.cuda.synchronize()
+    rows = prof.key_averages(group_by_stack_n=4)
+    rows = [r for r in rows if r.key.startswith("aten::") and r.device_time_total > 0]
+    rows.sort(key=lambda r: -r.device_time_total)
+    for r in rows[:top]:
+        stack = " <- ".join(f for f in (r.stack or []) if "comfy_gen_server_amd" in f)[:400]
+        print(f"ATEN {r.key:34s} calls={r.count:6d} dev_ms={r.device_time_total / 1e3:8.2f}  {stack}", flush=True)
 
 
 def bench_sdxl_cn_lora(reps, pipe=None):
@@ -157,6 +173,8 @@ def bench_cascade(reps):
                                                 1.0)[0]
                 NM["VAEDecode"]().decode(vae, out_b)
         best, mean = _timed(run, reps)
+        if os.environ.get("CGS_TORCH_PROFILE") == "1" and batch == 1:
+            _aten_table(run)
         _emit("cascade_c_b_a", batch, best, mean, steps_c=20, steps_b=10, resolution=1024,
               params_c_b=round(n_c, 3), params_b_b=round(n_b, 3))
 

@@ -858,3 +858,17 @@ def test_cascade_stage_a_decode_on_hip(cuda):
     assert st.get(("conv", "lib"), 0) == 0 and st.get(("conv", "hip"), 0) >= 4 and st.get(("gemm", "lib"), 0) == 0, st
     assert y.shape == ref.shape
     assert _rel(y.float().cpu(), ref) < 3e-2
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 24, 24, 2048), (1, 16, 16, 1280), (4, 7, 9, 64)])
+def test_channel_affine_nhwc(cuda, N, H, W, C):
+    """Cascade TimestepBlock: x * (1 + a) + b with a, b the halves of one [N, 2C] mapper output."""
+    torch.manual_seed(2)
+    x = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16)
+    ab = torch.randn(N, 2 * C, device=cuda).to(torch.bfloat16)
+    a, b = ab.chunk(2, dim=-1)
+    ops.reset_stats()
+    y = ops.channel_affine_nhwc(x, a, b, add=1.0)
+    assert ops.stats().get(("channel_affine", "hip"), 0) == 1
+    ref = x.float() * (1 + a.float()[:, None, None, :]) + b.float()[:, None, None, :]
+    assert _rel(y, ref) < 1e-2
