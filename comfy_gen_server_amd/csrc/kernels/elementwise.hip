@@ -91,17 +91,20 @@ CGS_EXPORT int cgs_timestep_embedding(const void* t, void* out, int n, int dim, 
 }
 
 // ---------------------------------------------------------------- nearest upsample x2, NHWC
+// IDX = unsigned (32-bit index math, the common case) or unsigned long long (outputs >= 2^32 chunks):
+// 64-bit integer division is emulated and dominated this memory-bound kernel.
+template <class IDX>
 __global__ void upsample2x_nhwc_kernel(const s16x8* __restrict__ x, s16x8* __restrict__ y, int N, int H, int W,
                                        int C8) {
-  long long total = (long long)N * 2 * H * 2 * W * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C8);
-    long long p = i / C8;
-    int ox = (int)(p % (2 * W));
-    long long q = p / (2 * W);
-    int oy = (int)(q % (2 * H));
-    int n = (int)(q / (2 * H));
-    y[i] = x[(((long long)n * H + (oy >> 1)) * W + (ox >> 1)) * C8 + c];
+  const IDX total = (IDX)N * 2 * H * 2 * W * C8;
+  for (IDX i = (IDX)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (IDX)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (IDX)C8);
+    const IDX p = i / (IDX)C8;
+    const int ox = (int)(p % (IDX)(2 * W));
+    const IDX q = p / (IDX)(2 * W);
+    const int oy = (int)(q % (IDX)(2 * H));
+    const int n = (int)(q / (IDX)(2 * H));
+    y[i] = x[(((IDX)n * H + (oy >> 1)) * W + (ox >> 1)) * C8 + c];
   }
 }
 
@@ -109,7 +112,11 @@ CGS_EXPORT int cgs_upsample_nearest2x_nhwc(const void* x, void* y, int N, int H,
                                            hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   long long total = (long long)N * 4 * H * W * (C / 8);
-  upsample2x_nhwc_kernel<<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (s16x8*)y, N, H, W, C / 8);
+  if (total < (1LL << 32) - (1LL << 24))
+    upsample2x_nhwc_kernel<unsigned><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (s16x8*)y, N, H, W, C / 8);
+  else
+    upsample2x_nhwc_kernel<unsigned long long><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (s16x8*)y, N, H,
+                                                                                     W, C / 8);
   return (int)hipGetLastError();
 }
 
@@ -140,18 +147,22 @@ CGS_EXPORT int cgs_geglu(const void* x, void* out, int M, int N, int dtype, hipS
 // Out-of-range taps are zero ("zeros" padding) or clamped to the border (replicate=1, Stage A).
 // One thread per 8 channels of one output pixel; neighbouring pixels of a wave share the same rows,
 // so the k*k tap re-reads hit L1/L2 — the kernel streams x and y once from HBM.
-template <int DT>
+template <int DT, int KF>   // KF: compile-time kernel size (3 / 7: unrolled taps), 0 = runtime k
 __global__ __launch_bounds__(256) void dwconv_nhwc_kernel(const s16x8* __restrict__ x, const u16* __restrict__ wt,
                                                           const u16* __restrict__ b, s16x8* __restrict__ y, int N,
-                                                          int H, int W, int C8, int k, int replicate) {
-  const long long total = (long long)N * H * W * C8;
+                                                          int H, int W, int C8, int kr, int replicate) {
+  // 32-bit index math (the launcher checks N*H*W*C8 < 2^31): the 64-bit divisions / modulos of the
+  // first version made this memory-bound kernel ALU-bound (~10x its streaming time at Cascade sizes)
+  const unsigned total = (unsigned)N * H * W * C8;
+  const int k = KF ? KF : kr;
   const int p = k >> 1;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8);
-    long long pix = i / C8;
-    const int wo = (int)(pix % W);
-    const int ho = (int)((pix / W) % H);
-    const int n = (int)(pix / ((long long)W * H));
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % (unsigned)C8);
+    const unsigned pix = i / (unsigned)C8;
+    const int wo = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int ho = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
     float acc[8];
     if (b) {
       s16x8 bv = reinterpret_cast<const s16x8*>(b)[c8];
@@ -161,15 +172,19 @@ __global__ __launch_bounds__(256) void dwconv_nhwc_kernel(const s16x8* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
     }
-    for (int di = 0; di < k; ++di) {
+#pragma unroll
+    for (int di = 0; di < (KF ? KF : 15); ++di) {
+      if (!KF && di >= k) break;
       int hi = ho + di - p;
       if (replicate) hi = min(max(hi, 0), H - 1);
       else if (hi < 0 || hi >= H) continue;
-      for (int dj = 0; dj < k; ++dj) {
+#pragma unroll
+      for (int dj = 0; dj < (KF ? KF : 15); ++dj) {
+        if (!KF && dj >= k) break;
         int wi = wo + dj - p;
         if (replicate) wi = min(max(wi, 0), W - 1);
         else if (wi < 0 || wi >= W) continue;
-        s16x8 xv = x[(((long long)n * H + hi) * W + wi) * C8 + c8];
+        s16x8 xv = x[(((unsigned)n * H + hi) * W + wi) * (unsigned)C8 + c8];
         s16x8 wv = reinterpret_cast<const s16x8*>(wt + (size_t)(di * k + dj) * C8 * 8)[c8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += cvt_in<DT>((u16)xv[j]) * cvt_in<DT>((u16)wv[j]);
@@ -184,13 +199,17 @@ __global__ __launch_bounds__(256) void dwconv_nhwc_kernel(const s16x8* __restric
 
 CGS_EXPORT int cgs_dwconv_nhwc(const void* x, const void* wt, const void* b, void* y, int N, int H, int W, int C,
                                int k, int replicate, int dtype, hipStream_t stream) {
-  if (C % 8 || (k & 1) == 0) return (int)hipErrorInvalidValue;
+  if (C % 8 || (k & 1) == 0 || k > 15) return (int)hipErrorInvalidValue;
   long long total = (long long)N * H * W * (C / 8);
-  if (dtype == CGS_BF16)
-    dwconv_nhwc_kernel<CGS_BF16><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b,
-                                                                      (s16x8*)y, N, H, W, C / 8, k, replicate);
-  else
-    dwconv_nhwc_kernel<CGS_F16><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b,
-                                                                     (s16x8*)y, N, H, W, C / 8, k, replicate);
+  if (total >= (1LL << 31)) return (int)hipErrorInvalidValue;
+#define CGS_DW(DTV, KV)                                                                                           \
+  dwconv_nhwc_kernel<DTV, KV><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b, \
+                                                                    (s16x8*)y, N, H, W, C / 8, k, replicate)
+  if (dtype == CGS_BF16) {
+    if (k == 3) CGS_DW(CGS_BF16, 3); else if (k == 7) CGS_DW(CGS_BF16, 7); else CGS_DW(CGS_BF16, 0);
+  } else {
+    if (k == 3) CGS_DW(CGS_F16, 3); else if (k == 7) CGS_DW(CGS_F16, 7); else CGS_DW(CGS_F16, 0);
+  }
+#undef CGS_DW
   return (int)hipGetLastError();
 }

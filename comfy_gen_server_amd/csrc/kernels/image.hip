@@ -274,37 +274,46 @@ __global__ void __launch_bounds__(256) grn2_sumsq_kernel(const u16* __restrict__
   }
 }
 
-__global__ void __launch_bounds__(1024) grn2_finalize_kernel(const float* __restrict__ part, float* __restrict__ nx,
-                                                             int C, int S) {
-  __shared__ float red[16];
-  const int n = blockIdx.x;
-  float sum = 0.f;
-#pragma unroll 4
-  for (int c = threadIdx.x; c < C; c += 1024) {   // unrolled: loads of several channels in flight
+// gx[n][c] = ||x[n, :, c]||_2 from the slice partials, one thread per channel over a (C / 256, N) grid
+// (a one-block-per-image form was latency-bound at batch 1-4: 2-8 workgroups); each block also
+// leaves the sum of its 256 gx values in bsum[n][block] -- the apply pass forms mean_C(gx) from those.
+__global__ void __launch_bounds__(256) grn2_finalize_kernel(const float* __restrict__ part, float* __restrict__ gx,
+                                                            float* __restrict__ bsum, int C, int S) {
+  __shared__ float red[4];
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  float g = 0.f;
+  if (c < C) {
     const float4* p = reinterpret_cast<const float4*>(part + ((size_t)n * C + c) * S);
     float ss = 0.f;
     for (int q = 0; q < S / 4; ++q) {
       const float4 v = p[q];
       ss += (v.x + v.y) + (v.z + v.w);
     }
-    const float g = sqrtf(ss);
-    nx[(size_t)n * C + c] = g;
-    sum += g;
+    g = sqrtf(ss);
+    gx[(size_t)n * C + c] = g;
   }
-  sum = wave_sum(sum);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  g = wave_sum(g);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
   __syncthreads();
-  float tot = 0.f;
-#pragma unroll
-  for (int w = 0; w < 16; ++w) tot += red[w];
-  const float inv = 1.f / (tot / (float)C + 1e-6f);
-  for (int c = threadIdx.x; c < C; c += 1024) nx[(size_t)n * C + c] *= inv;
+  if (threadIdx.x == 0) bsum[(size_t)n * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// N <= GRN_MAXN images: each block first forms 1 / (mean_C gx + 1e-6) of every image from the
+// finalize block sums (N x C/256 loads), then nx = gx * that inside the element loop.
+#define GRN_MAXN 64
 template <int DT, bool GELU>
-__global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__ x, const float* __restrict__ nx,
+__global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__ x, const float* __restrict__ gxp,
+                                                         const float* __restrict__ bsum, int nblk, int N,
                                                          const u16* __restrict__ gamma, const u16* __restrict__ beta,
                                                          u16* __restrict__ y, long long chunks, int HW, int C) {
+  __shared__ float inv_s[GRN_MAXN];
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float t = 0.f;
+    for (int b = 0; b < nblk; ++b) t += bsum[(size_t)n * nblk + b];
+    inv_s[n] = 1.f / (t / (float)C + 1e-6f);
+  }
+  __syncthreads();
   const unsigned cpr = (unsigned)C >> 3;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < chunks; i += (long long)gridDim.x * 256) {
     // 32-bit index math (chunks < 2^32, checked by the launcher): 64-bit divisions cost ~10x
@@ -315,9 +324,10 @@ __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__
     const s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
     const s16x8 gm = *reinterpret_cast<const s16x8*>(gamma + c0);
     const s16x8 bt = *reinterpret_cast<const s16x8*>(beta + c0);
-    const float4* np = reinterpret_cast<const float4*>(nx + (size_t)n * C + c0);
+    const float4* np = reinterpret_cast<const float4*>(gxp + (size_t)n * C + c0);
     const float4 n0 = np[0], n1 = np[1];
-    const float nv[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+    const float iv = inv_s[n];
+    const float nv[8] = {n0.x * iv, n0.y * iv, n0.z * iv, n0.w * iv, n1.x * iv, n1.y * iv, n1.z * iv, n1.w * iv};
     s16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
@@ -824,7 +834,7 @@ CGS_EXPORT int cgs_tome_match(const void* a, const void* b, float* ws, float* vm
   return (int)hipGetLastError();
 }
 
-// K28 v2 launcher: ws >= N * (S + 1) * C floats with S = cgs_grn_slices(N, HW, C).
+// K28 v2 launcher: ws >= N * ((S + 1) * C + ceil(C / 256)) floats with S = cgs_grn_slices(N, HW, C), N <= 64.
 CGS_EXPORT int cgs_grn_slices(int N, int HW, int C) {
   // ~512 pass-1 blocks, a multiple of 4 slices (pass 2 reads each channel's partials as float4s)
   const int cb = (C / 8 + 63) / 64;
@@ -842,8 +852,11 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
     return (int)hipErrorInvalidValue;
   const int S = cgs_grn_slices(N, HW, C);
   const int rows_per = (HW + S - 1) / S;
+  if (N > GRN_MAXN) return (int)hipErrorInvalidValue;
   float* part = ws;
   float* nx = ws + (size_t)N * S * C;
+  const int nblk = (C + 255) / 256;
+  float* bsum = nx + (size_t)N * C;                 // ws >= N * ((S + 1) * C + nblk) floats
   dim3 g1((unsigned)((C / 8 + 63) / 64), (unsigned)S, (unsigned)N);
   const long long chunks = (long long)N * HW * (C / 8);
   if (chunks >= (1LL << 32)) return (int)hipErrorInvalidValue;
@@ -851,9 +864,9 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
   const int blocks = (int)(nb > 16384 ? 16384 : nb);
 #define CGS_GRN2(DTV, GV)                                                                                        \
   grn2_sumsq_kernel<DTV, GV><<<g1, 256, 0, stream>>>((const u16*)x, part, HW, C, rows_per, S);                  \
-  grn2_finalize_kernel<<<N, 1024, 0, stream>>>(part, nx, C, S);                                                  \
-  grn2_apply_kernel<DTV, GV><<<blocks, 256, 0, stream>>>((const u16*)x, nx, (const u16*)gamma, (const u16*)beta, \
-                                                         (u16*)y, chunks, HW, C)
+  grn2_finalize_kernel<<<dim3((unsigned)nblk, (unsigned)N), 256, 0, stream>>>(part, nx, bsum, C, S);            \
+  grn2_apply_kernel<DTV, GV><<<blocks, 256, 0, stream>>>((const u16*)x, nx, bsum, nblk, N, (const u16*)gamma,    \
+                                                         (const u16*)beta, (u16*)y, chunks, HW, C)
   if (dtype == CGS_BF16) {
     if (pre_gelu) { CGS_GRN2(CGS_BF16, true); } else { CGS_GRN2(CGS_BF16, false); }
   } else {

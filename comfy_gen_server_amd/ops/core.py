@@ -1261,13 +1261,13 @@ def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, pre_gelu:
     Linear -> GELU -> GRN of Cascade's ChannelMLP: the GELU is fused into both reads of x)."""
     N, H, W, C = x.shape
     be = backend_for("grn", x, "cgs_grn_nhwc")
-    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0 and \
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0 and N <= 64 and \
             _native.has_kernel("cgs_grn_nhwc_v2"):
         count("grn", "hip")
         xc = x.contiguous()
         y = torch.empty_like(xc)
         S = int(_lib().cgs_grn_slices(N, H * W, C))
-        ws = torch.empty(N * (S + 1) * C, device=x.device, dtype=torch.float32)
+        ws = torch.empty(N * ((S + 1) * C + (C + 255) // 256), device=x.device, dtype=torch.float32)
         g = gamma.to(x.dtype).reshape(-1).contiguous()
         b = beta.to(x.dtype).reshape(-1).contiguous()
         _check(_lib().cgs_grn_nhwc_v2(xc.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(), ws.data_ptr(), N,
