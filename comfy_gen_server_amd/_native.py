@@ -148,6 +148,7 @@ KERNEL_SIGNATURES = {
     # v7 split-K tail: workspace bytes for (M, N, K) and the GEMM / conv launchers that take it
     "cgs_v7_ws_bytes": [_I, _I, _I],
     "cgs_v7_set_dbg": [_I],
+    "cgs_v6_set_mode": [_I],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
     "cgs_conv2d_nhwc_v7ws": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P],
     # K29 FreeU low-frequency filter: x, y, coef ws, B, C, H, W, x strides x4, y strides x4, t, scale, dtype
@@ -167,7 +168,7 @@ KERNEL_SIGNATURES = {
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
             "cgs_attn_set_variant": None}
 

@@ -477,7 +477,7 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   }
 }
 
-template <bool FAST>
+template <bool FAST, int DS = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
@@ -485,7 +485,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   typename std::conditional<FAST, ConvGatherK<true>, ConvGatherA8>::type al;
   al.a = &a;
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
-  pq::run(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n, a.group_m);
+  pq::run<decltype(al), false, DS>(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n,
+                                      a.group_m);
 }
 
 static int conv_num_cus() {
@@ -498,24 +499,38 @@ static int conv_num_cus() {
   return n;
 }
 
-static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
+int v6_ds();   // gemm.hip: v6 DMA placement (CGS_V6_DS / cgs_v6_set_mode)
+
+template <bool FAST, int DS>
+static void conv_v6_launch(ConvArgs& a, int grid, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              pq::LDS);
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<FAST, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               pq::LDS);
     attr = true;
   }
+  conv_nhwc_v6_kernel<FAST, DS><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+}
+
+static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   const int M = a.N * a.Ho * a.Wo;
   a.tiles_n = (a.Cout + pq::BN - 1) / pq::BN;
   const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
   const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
+  const int ds = v6_ds();
+  auto go = [&](auto fc) {
+    constexpr bool F = decltype(fc)::value;
+    switch (ds) {
+      case 0: conv_v6_launch<F, 0>(a, grid, stream); break;
+      case 3: conv_v6_launch<F, 3>(a, grid, stream); break;
+      default: conv_v6_launch<F, 1>(a, grid, stream);
+    }
+  };
   if (conv_fast_ok(a)) {
     conv_magic(a);
-    conv_nhwc_v6_kernel<true><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+    go(std::true_type{});
   } else {
-    conv_nhwc_v6_kernel<false><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+    go(std::false_type{});
   }
 }
 

@@ -525,7 +525,7 @@ static int gemm_v5_launch(const void* A, const void* W, void* C, const void* bia
 
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
-template <bool LN = false>
+template <bool LN = false, int DS = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   DenseA8 al{A, lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
-  pq::run<DenseA8, LN>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  pq::run<DenseA8, LN, DS>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
 }
 static int num_cus() {
   static int n = 0;
@@ -545,29 +545,49 @@ static int num_cus() {
   return n;
 }
 
-static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
-                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                          hipStream_t stream, const float* rs = nullptr, const float* cs = nullptr) {
+// v6 DMA placement (pq::run DS): CGS_V6_DS at first use, cgs_v6_set_mode() after (in-process A/B).
+// Default 1 (A parts in phase 0, B parts in phase 1): +4..11 % over all-in-phase-0 on the SDXL
+// N = 640 / 1280 GEMMs and +2..4 % on the Cout = 320 convs (profiles/r03/v6_dma_split.log).
+static int g_v6_ds = -1;
+int v6_ds() {
+  if (g_v6_ds < 0) g_v6_ds = getenv("CGS_V6_DS") ? atoi(getenv("CGS_V6_DS")) : 1;
+  return g_v6_ds;
+}
+CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; }
+
+template <bool LN, int DS>
+static void gemm_v6_go(int grid, const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                       int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                       int tiles_m, int tiles_n, hipStream_t stream, const float* rs, const float* cs) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              pq::LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               pq::LDS);
     attr_set = true;
   }
+  gemm_bf16_nt_v6_kernel<LN, DS><<<grid, pq::THREADS, pq::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+      tiles_m, tiles_n, g_tile_group, rs, cs);
+}
+
+static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                          hipStream_t stream, const float* rs = nullptr, const float* cs = nullptr) {
   const int tiles_n = (N + pq::BN - 1) / pq::BN;
   const int tiles_m = (M + pq::BM - 1) / pq::BM;
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
-  if (epi & EPI_LNFOLD)
-    gemm_bf16_nt_v6_kernel<true><<<grid, pq::THREADS, pq::LDS, stream>>>(
-        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_m, tiles_n, g_tile_group, rs, cs);
-  else
-    gemm_bf16_nt_v6_kernel<false><<<grid, pq::THREADS, pq::LDS, stream>>>(
-        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi,
-        alpha, tiles_m, tiles_n, g_tile_group);
+  const int ds = v6_ds();
+  auto go = [&](auto lnc) {
+    constexpr bool L = decltype(lnc)::value;
+    switch (ds) {
+      case 0: gemm_v6_go<L, 0>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      case 3: gemm_v6_go<L, 3>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      default: gemm_v6_go<L, 1>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs);
+    }
+  };
+  if (epi & EPI_LNFOLD) go(std::true_type{});
+  else go(std::false_type{});
   return (int)hipGetLastError();
 }
 
@@ -758,7 +778,7 @@ static int gemm_skinny_launch(const void* A, const void* W, void* C, const void*
   gemm_skinny_kernel<MRV><<<g, 64 * SK_WAVES, 0, stream>>>((const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias,         \
                                                  (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha)
   switch (mr) {
-    case 1: CGS_SKINNY(1); break;
+    case 0: CGS_SKINNY(1); break;
     case 2: CGS_SKINNY(2); break;
     case 3: CGS_SKINNY(3); break;
     case 4: CGS_SKINNY(4); break;

@@ -52,7 +52,10 @@ __device__ __forceinline__ int b_col160(int r) {
 // the current tile's last two, and the epilogue (direct 8-B stores from registers, no LDS) runs
 // while they are in flight -- no per-tile prologue bubble, no LDS-staged epilogue (16-B stores for
 // 4 of the 5 column tiles, see b_col160). Needs K >= 128, N % 8 == 0.
-template <class AL, bool LN = false>
+// DS: where a K-tile's DMAs are issued (the per-phase interleave): bits 0-1 the split over the two
+// phases (see stage_part), bit 2 DMAs before / after the phase's fragment reads. Phase-1 DMAs are
+// issued before that phase's counted wait, so the vmcnt counts are the same in every mode.
+template <class AL, bool LN = false, int DS = 0>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -87,15 +90,49 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
     }
   };
-  auto stage = [&](int kt, int slot) {
-    const int k0 = kt * BK;
-    unsigned char* base = smem + slot * STAGE + wave * 1024;
+  // A slot g / B row group g of K-tile kt into ring slot `slot`
+  auto dma_a = [&](int g, int kt, int slot) {
+    mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * 8192);
+  };
+  auto dma_b = [&](int g, int kt, int slot) {
+    if (g < 2 || grp == 0)   // B rows 128..159: group 0 only
+      mc::lds_dma16((const void*)(bsrc[g] + kt * BK), smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192);
+  };
+  // the phase-0 (part 0) / phase-1 (part 1) DMAs of K-tile kt: DS & 3 = 0 all in phase 0, 1 A | B,
+  // 2 B | A, 3 balanced (A0 A1 B0 | A2 A3 B1 B2)
+  auto stage_part = [&](int part, int kt, int slot) {
+    constexpr int D = DS & 3;
+    if constexpr (D == 0) {
+      if (part == 0) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) mc::lds_dma16(al.src(g, k0), base + g * 8192);
-    unsigned char* bb = base + A_BYTES;
-    mc::lds_dma16((const void*)(bsrc[0] + k0), bb);
-    mc::lds_dma16((const void*)(bsrc[1] + k0), bb + 8192);
-    if (grp == 0) mc::lds_dma16((const void*)(bsrc[2] + k0), bb + 16384);   // B rows 128..159
+        for (int g = 0; g < 4; ++g) dma_a(g, kt, slot);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) dma_b(g, kt, slot);
+      }
+    } else if constexpr (D == 1 || D == 2) {
+      if ((part == 0) == (D == 1)) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dma_a(g, kt, slot);
+      } else {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) dma_b(g, kt, slot);
+      }
+    } else {
+      if (part == 0) {
+        dma_a(0, kt, slot);
+        dma_a(1, kt, slot);
+        dma_b(0, kt, slot);
+      } else {
+        dma_a(2, kt, slot);
+        dma_a(3, kt, slot);
+        dma_b(1, kt, slot);
+        dma_b(2, kt, slot);
+      }
+    }
+  };
+  auto stage = [&](int kt, int slot) {
+    stage_part(0, kt, slot);
+    if constexpr ((DS & 3) != 0) stage_part(1, kt, slot);
   };
   auto wait_tile = [&]() {   // all but the 7 (group 0) / 6 (group 1) youngest DMAs retired
     if (grp == 0) mc::wait_vmcnt<7>();
@@ -251,21 +288,21 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       const unsigned char* S = smem + slot * STAGE;
       const int slot2 = slot >= 1 ? slot - 1 : 2;      // (slot + 2) % 3
       // phase 0: fragments k 0..31; DMA the K-tile two ahead in the stream into the slot vacated
+      const int kst = kt + 2 < nk ? kt + 2 : (has_next ? kt + 2 - nk : nk - 1);
+      if (kt + 2 == nk && has_next) setup(nm0, nn0);   // switch the loaders to the next tile
+      // past the last tile: reload the last K-tile into a dead slot (keeps the vmcnt pattern);
+      // DS & 4: the DMAs go out ahead of the phase's fragment reads
+      if constexpr ((DS & 4) != 0) stage_part(0, kst, slot2);
       read_frags(S, 0);
-      if (kt + 2 < nk) {
-        stage(kt + 2, slot2);
-      } else if (has_next) {
-        if (kt + 2 == nk) setup(nm0, nn0);             // switch the loaders to the next tile
-        stage(kt + 2 - nk, slot2);
-      } else {
-        stage(nk - 1, slot2);                          // keep the vmcnt pattern: reload into a dead slot
-      }
+      if constexpr ((DS & 4) == 0) stage_part(0, kst, slot2);
       pp::wait_lgkm0();
       pp::barrier();
       mma();
       pp::barrier();
       // phase 1: fragments k 32..63; retire this wave's DMAs of the next K-tile in the stream
+      if constexpr ((DS & 4) != 0) stage_part(1, kst, slot2);
       read_frags(S, 1);
+      if constexpr ((DS & 4) == 0) stage_part(1, kst, slot2);
       wait_tile();
       pp::wait_lgkm0();
       pp::barrier();
