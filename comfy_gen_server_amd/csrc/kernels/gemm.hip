@@ -899,7 +899,9 @@ static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, 
   if (variant == 8 || (variant >= 10 && variant <= 14))
     return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, variant,
                           rs, cs);
-  if (!(epi & EPI_GEGLU) && N % 160 == 0 && N <= 1280 && K >= 128)
+  const bool v6_ok = !(epi & EPI_GEGLU) && N % 160 == 0;
+  if (variant == 6 && !v6_ok) return (int)hipErrorInvalidValue;
+  if (variant == 6 || (variant < 0 && v6_ok && N <= 1280))
     return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
   return gemm_v7_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, ws, ws_bytes, stream,
                         rs, cs);
@@ -912,7 +914,7 @@ CGS_EXPORT int cgs_gemm_bf16_lnfold(const void* A, const void* W, void* C, const
 }
 
 // Per-call kernel choice for the LayerNorm-folded GEMM (op-layer autotuner): -1 = v6 / v7 by shape,
-// 8 / 10 / 11 = the small-tile kernels (128x128 / 64x128 / 128x64) for under-filled grids.
+// 6 / 7 = v6 / v7 explicitly, 8 / 10..14 = the small-tile kernels for under-filled grids.
 CGS_EXPORT int cgs_gemm_bf16_lnfold_v(const void* A, const void* W, void* C, const void* bias, const float* rs,
                                       const float* cs, int M, int N, int K, long long lda, long long ldw, long long ldc,
                                       int epi, void* ws, long long ws_bytes, int variant, hipStream_t stream) {

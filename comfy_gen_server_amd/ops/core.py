@@ -1054,7 +1054,7 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
 
     def run(variant):
         out = torch.empty((M, nout), device=x.device, dtype=x.dtype)
-        ws = _v7_ws(M, N, K, x.device) if variant < 0 else None
+        ws = _v7_ws(M, N, K, x.device) if variant in (-1, 7) else None
         _check(_lib().cgs_gemm_bf16_lnfold_v(a.data_ptr(), w2.data_ptr(), out.data_ptr(), b2.data_ptr(), rs.data_ptr(),
                                              cs.data_ptr(), M, N, K, K, K, nout, epi, _ptr(ws),
                                              0 if ws is None else ws.numel(), variant, _stream()),
@@ -1066,6 +1066,12 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
         cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v7")
         variant = {"v8": 8, **_SMALL_NAMES}.get(choice, -1)
+    elif not geglu and N % 160 == 0 and N > 1280 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
+        # wide non-GEGLU projections (fused QKV): 256x160 tiles give whole rounds where 256x256 leave
+        # a partial last round (N = 1920 / 3840 at M = 65536 / 16384) -- measured per shape
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), [("v7", lambda: run(7)), ("v6", lambda: run(6))],
+                                 default="v7")
+        variant = 6 if choice == "v6" else 7
     return run(variant).view(*x.shape[:-1], nout)
 
 

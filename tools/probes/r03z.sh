@@ -3,6 +3,6 @@
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 500 python -u tools/probes/v6_ab.py > gpurun_out/r03za_v6ab.log 2>&1
-rc=$?; echo "v6_ab rc=$rc"; cat gpurun_out/r03za_v6ab.log | grep -v amdgpu.ids
+timeout -k 10 500 python -u tools/probes/qkv_ab.py > gpurun_out/r03zb_qkv.log 2>&1
+rc=$?; echo "qkv_ab rc=$rc"; cat gpurun_out/r03zb_qkv.log | grep -v amdgpu.ids
 exit $rc
