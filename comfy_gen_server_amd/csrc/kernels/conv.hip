@@ -43,6 +43,7 @@ struct ConvArgs {
   unsigned cq_magic;   // ceil(2^32 / (Cin / 64)), 0 when Cin == 64 (ConvGatherK tap decode)
   int kw_m16;          // ceil(65536 / kw)
   ppk::Split sp;       // v7 split-K tail (S <= 1: none)
+  float* gnp;          // v6 only: GroupNorm partial statistics out (pq::run GNS), or null
 };
 
 // Host: the multiply-shift constants of ConvGatherK (exact for k0 < kh*kw*Cin, kh*kw <= 32).
@@ -477,7 +478,7 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   }
 }
 
-template <bool FAST, int DS = 0>
+template <bool FAST, int DS = 0, bool GNS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
@@ -485,8 +486,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   typename std::conditional<FAST, ConvGatherK<true>, ConvGatherA8>::type al;
   al.a = &a;
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
-  pq::run<decltype(al), false, DS>(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n,
-                                      a.group_m);
+  e.gnp = a.gnp;
+  e.hw = a.Ho * a.Wo;
+  pq::run<decltype(al), false, DS, GNS>(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n,
+                                           a.group_m);
 }
 
 static int conv_num_cus() {
@@ -501,15 +504,15 @@ static int conv_num_cus() {
 
 int v6_ds();   // gemm.hip: v6 DMA placement (CGS_V6_DS / cgs_v6_set_mode)
 
-template <bool FAST, int DS>
+template <bool FAST, int DS, bool GNS = false>
 static void conv_v6_launch(ConvArgs& a, int grid, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<FAST, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              pq::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<FAST, DS, GNS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
     attr = true;
   }
-  conv_nhwc_v6_kernel<FAST, DS><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+  conv_nhwc_v6_kernel<FAST, DS, GNS><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
 }
 
 static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
@@ -526,6 +529,15 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
       default: conv_v6_launch<F, 1>(a, grid, stream);
     }
   };
+  if (a.gnp) {   // GroupNorm statistics epilogue (split-DMA main loop only)
+    if (conv_fast_ok(a)) {
+      conv_magic(a);
+      conv_v6_launch<true, 1, true>(a, grid, stream);
+    } else {
+      conv_v6_launch<false, 1, true>(a, grid, stream);
+    }
+    return;
+  }
   if (conv_fast_ok(a)) {
     conv_magic(a);
     go(std::true_type{});
@@ -785,6 +797,24 @@ CGS_EXPORT int cgs_conv2d_nhwc_v(const void* x, const void* x2, int C1, const vo
              Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
              (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0, 1};
   return conv_launch(a, stream, variant);
+}
+
+// v6 conv whose epilogue also writes the GroupNorm partial statistics of its output (gnp: [N, Ho*Wo/64,
+// Cout] (mean, M2) float pairs, the cgs_groupnorm_nhwc_part layout with 64 pixels per block), so the
+// following GroupNorm skips its statistics pass. Needs (Ho * Wo) % 256 == 0 and the v6 conditions.
+CGS_EXPORT int cgs_conv2d_nhwc_gns(const void* x, const void* x2, int C1, const void* w, const void* bias,
+                                   const void* res, void* out, int N, int H, int W, int Cin, int Cout, int kh, int kw,
+                                   int stride, int pad, int Ho, int Wo, int flags, float* gnp, hipStream_t stream) {
+  if (!gnp || Cin % 64 || (x2 && C1 % 64) || Cout % 8 || kh * kw * Cin < 128 || (Ho * Wo) % 256 ||
+      ((uintptr_t)bias % 8) || ((uintptr_t)gnp % 16))
+    return (int)hipErrorInvalidValue;
+  ConvArgs a{(const u16*)x, (const u16*)x2, (const u16*)w, (const u16*)bias, (const u16*)res, (u16*)out, N, H, W,
+             Cin, x2 ? C1 : Cin, Cout, kh, kw, stride, pad, Ho, Wo,
+             (bias ? EPI_BIAS : 0) | (res ? EPI_RESIDUAL : 0) | (flags & CONV_UP2X), 0, 1};
+  a.gnp = gnp;
+  a.group_m = g_conv_group;
+  conv_v6_go(a, stream);
+  return (int)hipGetLastError();
 }
 
 // v7 with the split-K tail workspace (>= cgs_v7_ws_bytes(N*Ho*Wo, Cout, kh*kw*Cin) bytes).

@@ -523,6 +523,21 @@ static int gemm_v5_launch(const void* A, const void* W, void* C, const void* bia
   return (int)hipGetLastError();
 }
 
+// Dense A loader with 32-bit byte offsets from one uniform base (global_load_lds saddr + voffset form:
+// one VGPR per slot instead of a 64-bit pointer pair -- the v7 kernel runs at the 256-VGPR cap).
+struct DenseA32 {
+  const unsigned char* A;
+  long long lda;
+  int M;
+  uint32_t off[4];
+  __device__ __forceinline__ void setup(int slot, int row) {
+    row = row < M ? row : M - 1;
+    off[slot] = (uint32_t)(((long long)row * lda + 8 * pp::src_chunk8(slot & 1)) * 2);
+  }
+  __device__ __forceinline__ const void* src(int slot, int k0) const { return A + (off[slot] + (uint32_t)(k0 * 2)); }
+  __device__ __forceinline__ void dma(int slot, int k0, unsigned char* dst) const { mc::lds_dma16(src(slot, k0), dst); }
+};
+
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
 template <bool LN = false, int DS = 0>
@@ -531,6 +546,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
     int epi, float alpha, int tiles_m, int tiles_n, int group_m, const float* rs = nullptr, const float* cs = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // 64-bit operand pointers: the 32-bit-offset (saddr) DMA form measured 3-10 % slower on v6
+  // (profiles/r03/v6_offsets32.log)
   DenseA8 al{A, lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
   pq::run<DenseA8, LN, DS>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
@@ -591,20 +608,6 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   return (int)hipGetLastError();
 }
 
-// Dense A loader with 32-bit byte offsets from one uniform base (global_load_lds saddr + voffset form:
-// one VGPR per slot instead of a 64-bit pointer pair -- the v7 kernel runs at the 256-VGPR cap).
-struct DenseA32 {
-  const unsigned char* A;
-  long long lda;
-  int M;
-  uint32_t off[4];
-  __device__ __forceinline__ void setup(int slot, int row) {
-    row = row < M ? row : M - 1;
-    off[slot] = (uint32_t)(((long long)row * lda + 8 * pp::src_chunk8(slot & 1)) * 2);
-  }
-  __device__ __forceinline__ const void* src(int slot, int k0) const { return A + (off[slot] + (uint32_t)(k0 * 2)); }
-  __device__ __forceinline__ void dma(int slot, int k0, unsigned char* dst) const { mc::lds_dma16(src(slot, k0), dst); }
-};
 
 // ------------------------------------------------------------------------------------------------
 // v7: persistent 256 x 256 x 64 ping-pong with cross-tile prefetch and a register epilogue (mfma_ppk.h)

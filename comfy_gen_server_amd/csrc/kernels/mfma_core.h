@@ -78,6 +78,8 @@ struct Epi {
   float alpha;
   const float* rs = nullptr;   // MC_EPI_LNFOLD: per-row (mean, rstd) pairs of the GEMM's A rows
   const float* cs = nullptr;   // MC_EPI_LNFOLD: per-column sums of the gamma-scaled weight rows
+  float* gnp = nullptr;        // GroupNorm statistics out (pq::run GNS): per-(image, 64-row block, column)
+  int hw = 0;                  //   (mean, M2) partials in the gn_partial layout; hw = rows per image
 };
 
 // s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])

@@ -55,7 +55,11 @@ __device__ __forceinline__ int b_col160(int r) {
 // DS: where a K-tile's DMAs are issued (the per-phase interleave): bits 0-1 the split over the two
 // phases (see stage_part), bit 2 DMAs before / after the phase's fragment reads. Phase-1 DMAs are
 // issued before that phase's counted wait, so the vmcnt counts are the same in every mode.
-template <class AL, bool LN = false, int DS = 0>
+// GNS: the epilogue also writes GroupNorm partial statistics of the stored (bf16) outputs -- per image,
+// 64-row block (one wave's rows) and column, (mean, M2) by an exact two-pass over the wave's registers
+// (DPP row sums) -- into e.gnp in the gn_partial layout with 64 pixels per block, so the next GroupNorm
+// skips its statistics pass over the tensor (host: rows per image % 256 == 0).
+template <class AL, bool LN = false, int DS = 0, bool GNS = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -231,6 +235,54 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
       return pack4_bf16(v0, v1, v2, v3);
     };
+    if constexpr (GNS) {
+      uint2 pk[4][5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pk[i][j] = val(i, j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m_w + 16 * i + fr;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int col = n_w + 32 * p + 8 * fq;
+          if (row < M && col < N)
+            *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) =
+                uint4{pk[i][2 * p].x, pk[i][2 * p].y, pk[i][2 * p + 1].x, pk[i][2 * p + 1].y};
+        }
+        const int col = n_w + 64 + 4 * fq;
+        if (row < M && col < N) *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pk[i][4];
+      }
+      const int img = m_w / e.hw;
+      const int nbk = e.hw >> 6;
+      float* dst = e.gnp + (size_t)(img * nbk + ((m_w - img * e.hw) >> 6)) * N * 2;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        float4 u[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[i] = unpack4_bf16(pk[i][j]);
+        float4 mu = u[0];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) { mu.x += u[i].x; mu.y += u[i].y; mu.z += u[i].z; mu.w += u[i].w; }
+        constexpr float inv = 1.f / 64.f;
+        mu = float4{row16_sum(mu.x) * inv, row16_sum(mu.y) * inv, row16_sum(mu.z) * inv, row16_sum(mu.w) * inv};
+        float4 q = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float dx = u[i].x - mu.x, dy = u[i].y - mu.y, dz = u[i].z - mu.z, dw = u[i].w - mu.w;
+          q.x += dx * dx; q.y += dy * dy; q.z += dz * dz; q.w += dw * dw;
+        }
+        q = float4{row16_sum(q.x), row16_sum(q.y), row16_sum(q.z), row16_sum(q.w)};
+        const int col = n_w + colj(j);
+        if (fr == 0 && col < N) {
+          float4* d4 = reinterpret_cast<float4*>(dst + (size_t)col * 2);
+          d4[0] = float4{mu.x, q.x, mu.y, q.y};
+          d4[1] = float4{mu.z, q.z, mu.w, q.w};
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m_w + 16 * i + fr;

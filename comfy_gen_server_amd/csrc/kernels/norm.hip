@@ -6,7 +6,7 @@
 //   1. gn_partial : block = (pixel chunk, n); each lane owns fixed 8-channel chunks of the row and
 //      accumulates shifted sums (shift = the block's first pixel; 4 rows of loads in flight per wave) -> per-wave (mean, M2) -> Chan combine over
 //      the 4 waves in LDS -> per-(n, block, c) partial.
-//   2. gn_finalize: one block per (n, g), exact two-pass combine of the blocks x channels partials ->
+//   2. gn_finalize: one block per (n, g), one-pass Chan combine of the blocks x channels partials ->
 //      mean/rstd -> per-(n,c) affine a, b (the pre-add shifts the channel mean only, so it folds into b).
 //   3. gn_apply   : y = x*a + b (+SiLU), 16-byte vectors, per-thread channel chunk fixed (a, b in registers).
 // LayerNorm: 8-64 lanes per row (sized to the row), two-pass mean/var from registers, 16-byte vectors.
@@ -128,61 +128,69 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   }
 }
 
+// Chan's parallel combine of (count, mean, M2) triples (exact up to fp32 rounding, no cancellation)
+__device__ __forceinline__ void chan_merge(float& na, float& ma, float& qa, float nb, float mb, float qb) {
+  const float nn = na + nb;
+  if (nn <= 0.f) return;
+  const float d = mb - ma;
+  const float f = nb / nn;
+  ma += d * f;
+  qa += qb + d * d * na * f;
+  na = nn;
+}
+
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ part, const void* __restrict__ gamma,
                                                          const void* __restrict__ beta, const void* __restrict__ pre_add,
                                                          float* __restrict__ ab, int HW, int C, int G, int ppb, int nb,
                                                          float eps, int wdt) {
-  // one 256-thread block per (n, g). Every channel of a pixel block shares that block's pixel count, so
-  // the group statistics are an exact two-pass combine of the per-(block, channel) (mean, M2) partials:
-  //   mean = sum n_b*mean_b / sum n_b,   M2 = sum M2_b + sum n_b*(mean_b - mean)^2
-  // (no per-item divisions or serial Chan chain: the partials are re-read from L2 in the second pass).
+  // one 256-thread block per (n, g): ONE pass over the per-(block, channel) (mean, M2) partials, each
+  // thread Chan-combining its items (all loads of a round issued before any combine), then a Chan tree
+  // over the wave (shuffles) and the 4 waves (LDS). (The two-pass form re-read every partial: at batch 1
+  // -- 1024 pixel blocks per image -- it was L2-latency bound at ~20 us per GroupNorm.)
   const int g = blockIdx.x;
   const int n = blockIdx.y;
   const int tid = threadIdx.x;
   const int Cg = C / G;
   const int items = Cg * nb;
-  __shared__ float red[2][4];
+  __shared__ float red[3][4];
   auto chan_shift = [&](int c) -> float {
     if (!pre_add) return 0.f;
     return (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
                              : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c]) : ((const float*)pre_add)[n * C + c]);
   };
-  auto block_sum2 = [&](float& a, float& b) {
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if ((tid & 63) == 0) { red[0][tid >> 6] = a; red[1][tid >> 6] = b; }
-    __syncthreads();
-    a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    __syncthreads();
-  };
-  float sw = 0.f, cntsum = 0.f;
-  // unrolled so several independent partial loads are in flight per thread (the loop is L2-latency
-  // bound: 64 blocks at batch 1, ~20 items per thread)
-#pragma unroll 8
-  for (int it = tid; it < items; it += 256) {
-    int b = it / Cg, cc = it - b * Cg;
-    int c = g * Cg + cc;
-    float n_b = (float)(min(HW, b * ppb + ppb) - b * ppb);
-    float mb = part[(((size_t)n * nb + b) * C + c) * 2] + chan_shift(c);
-    sw += n_b * mb;
-    cntsum += n_b;
+  float cnt = 0.f, mean = 0.f, m2 = 0.f;
+  constexpr int U = 8;
+  for (int it0 = tid; it0 < items; it0 += 256 * U) {
+    float2 v[U];
+    float nbv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int it = it0 + 256 * u;
+      v[u] = make_float2(0.f, 0.f);
+      nbv[u] = 0.f;
+      if (it < items) {
+        const int b = it / Cg, cc = it - b * Cg;
+        const int c = g * Cg + cc;
+        v[u] = *reinterpret_cast<const float2*>(part + (((size_t)n * nb + b) * C + c) * 2);
+        v[u].x += chan_shift(c);
+        nbv[u] = (float)(min(HW, b * ppb + ppb) - b * ppb);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) chan_merge(cnt, mean, m2, nbv[u], v[u].x, v[u].y);
   }
-  block_sum2(sw, cntsum);
-  const float mean = sw / fmaxf(cntsum, 1.f);
-  float m2 = 0.f, dummy = 0.f;
-#pragma unroll 8
-  for (int it = tid; it < items; it += 256) {
-    int b = it / Cg, cc = it - b * Cg;
-    int c = g * Cg + cc;
-    float n_b = (float)(min(HW, b * ppb + ppb) - b * ppb);
-    size_t o = (((size_t)n * nb + b) * C + c) * 2;
-    float d = part[o] + chan_shift(c) - mean;
-    m2 += part[o + 1] + n_b * d * d;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float on = __shfl_xor(cnt, off), om = __shfl_xor(mean, off), oq = __shfl_xor(m2, off);
+    chan_merge(cnt, mean, m2, on, om, oq);
   }
-  block_sum2(m2, dummy);
-  float var = m2 / fmaxf(cntsum, 1.f);
-  float rstd = rsqrtf(var + eps);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = cnt; red[1][tid >> 6] = mean; red[2][tid >> 6] = m2; }
+  __syncthreads();
+  cnt = red[0][0]; mean = red[1][0]; m2 = red[2][0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) chan_merge(cnt, mean, m2, red[0][w], red[1][w], red[2][w]);
+  const float var = m2 / fmaxf(cnt, 1.f);
+  const float rstd = rsqrtf(fmaxf(var, 0.f) + eps);
   for (int cc = tid; cc < Cg; cc += 256) {
     int c = g * Cg + cc;
     float gm = 1.f, bt = 0.f;
@@ -238,6 +246,9 @@ CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
   return (long long)N * nb * C * 2 * 4 + (long long)N * C * 2 * 4 + 256;
 }
 
+static int gn_apply_launch(const void* x, const void* x2, int C1, void* y, const float* ab, int N, int HW, int C,
+                           int silu, int dtype, hipStream_t stream);
+
 // x, y: [N, HW, C] (NHWC); gamma/beta [C] in the activation dtype; pre_add [N, C] (act dtype) or null.
 // ws: workspace of cgs_groupnorm_workspace() bytes (torch-allocated so it is graph-capturable).
 static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const void* gamma, const void* beta,
@@ -261,6 +272,11 @@ static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const 
   if (km == 1) { CGS_GN_PARTIAL(1) } else if (km == 2) { CGS_GN_PARTIAL(2) } else if (km == 3) { CGS_GN_PARTIAL(3) } else { CGS_GN_PARTIAL(4) }
 #undef CGS_GN_PARTIAL
   gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
+  return gn_apply_launch(x, x2, C1, y, ab, N, HW, C, silu, dtype, stream);
+}
+
+static int gn_apply_launch(const void* x, const void* x2, int C1, void* y, const float* ab, int N, int HW, int C,
+                           int silu, int dtype, hipStream_t stream) {
   const int cpr = C / 8;
   const long long rows_total = (long long)N * HW;
   if (rows_total == 0) return (int)hipGetLastError();
@@ -278,6 +294,17 @@ static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const 
     else gn_apply_kernel<CGS_F16, false><<<blocks, 256, 0, stream>>>((const u16*)x, (const u16*)x2, C1, (u16*)y, ab, (int)rows_total, rows_per_iter, HW, C);
   }
   return (int)hipGetLastError();
+}
+
+// GroupNorm whose statistics pass already ran in the producer's epilogue (cgs_conv2d_nhwc_gns): part =
+// [N, HW / ppb, C] (mean, M2) partials of ppb pixels each; only finalize + apply run. ab: N * C * 2 floats.
+CGS_EXPORT int cgs_groupnorm_nhwc_part(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,
+                                       const float* part, float* ab, int N, int HW, int C, int G, int ppb, float eps,
+                                       int silu, int dtype, hipStream_t stream) {
+  if (C % 8 || C % G || ppb <= 0 || HW % ppb || !part || !ab) return (int)hipErrorInvalidValue;
+  const int nb = HW / ppb;
+  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
+  return gn_apply_launch(x, nullptr, C, y, ab, N, HW, C, silu, dtype, stream);
 }
 
 CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,

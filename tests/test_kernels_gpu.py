@@ -872,3 +872,37 @@ def test_channel_affine_nhwc(cuda, N, H, W, C):
     assert ops.stats().get(("channel_affine", "hip"), 0) == 1
     ref = x.float() * (1 + a.float()[:, None, None, :]) + b.float()[:, None, None, :]
     assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,pre", [(2, 32, 32, 320, 320, True), (1, 16, 16, 640, 640, False),
+                                                 (2, 16, 32, 128, 160, True)])
+def test_conv_gn_stats_epilogue(cuda, N, H, W, Cin, Cout, pre):
+    """K06 second half (measured, not wired: profiles/r03/gn_stats_in_conv_epilogue.log): the v6 conv's
+    epilogue writes the GroupNorm partials of its bf16 output; finalize + apply from them == the GroupNorm
+    of the stored conv output (pre-add shift included)."""
+    torch.manual_seed(3)
+    lib = _native.load_kernels()
+    x = (torch.rand(N, H, W, Cin, device=cuda) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(Cout, 3, 3, Cin, device=cuda) * 2 - 1) / math.sqrt(Cin * 9)).to(torch.bfloat16)
+    b = (torch.randn(Cout, device=cuda) + 2).to(torch.bfloat16)
+    g = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    be = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    p = torch.randn(N, Cout, device=cuda).to(torch.bfloat16) if pre else None
+    out = torch.empty(N, H, W, Cout, device=cuda, dtype=torch.bfloat16)
+    HW = H * W
+    gnp = torch.full((N * (HW // 64) * Cout * 2,), float("nan"), device=cuda)
+    ab = torch.empty(N * Cout * 2, device=cuda)
+    y = torch.empty_like(out)
+    st = core._stream()
+    assert lib.cgs_conv2d_nhwc_gns(x.data_ptr(), None, Cin, w.data_ptr(), b.data_ptr(), None, out.data_ptr(), N, H, W,
+                                   Cin, Cout, 3, 3, 1, 1, H, W, 0, gnp.data_ptr(), st) == 0
+    assert lib.cgs_groupnorm_nhwc_part(out.data_ptr(), y.data_ptr(), g.data_ptr(), be.data_ptr(),
+                                       None if p is None else p.data_ptr(), gnp.data_ptr(), ab.data_ptr(), N, HW, Cout,
+                                       32, 64, 1e-5, 1, 1, st) == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(gnp).all()
+    conv_ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), b.float(), 1, 1)
+    assert _rel(out.permute(0, 3, 1, 2), conv_ref) < 1e-2
+    xf = out.permute(0, 3, 1, 2).float() + (p.float()[:, :, None, None] if pre else 0.0)
+    ref = F.silu(F.group_norm(xf, 32, g.float(), be.float(), 1e-5))
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2

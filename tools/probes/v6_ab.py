@@ -16,7 +16,7 @@ from comfy_gen_server_amd.ops import core  # noqa: E402
 
 lib = _native.load_kernels()
 dev = torch.device("cuda", 0)
-MODES = [0, 1, 3, 5, 7]
+MODES = [int(m) for m in os.environ.get("V6_MODES", "0,1,3").split(",")]
 
 
 def timeit(fn, iters=20):
