@@ -502,7 +502,7 @@ static int conv_num_cus() {
   return n;
 }
 
-int v6_ds();   // gemm.hip: v6 DMA placement (CGS_V6_DS / cgs_v6_set_mode)
+int v6_conv_ds();   // gemm.hip: v6 DMA placement for convs (CGS_V6_CONV_DS / cgs_v6_set_mode)
 
 template <bool FAST, int DS, bool GNS = false>
 static void conv_v6_launch(ConvArgs& a, int grid, hipStream_t stream) {
@@ -520,21 +520,23 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   a.tiles_n = (a.Cout + pq::BN - 1) / pq::BN;
   const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
   const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
-  const int ds = v6_ds();
+  const int ds = v6_conv_ds();
   auto go = [&](auto fc) {
     constexpr bool F = decltype(fc)::value;
     switch (ds) {
       case 0: conv_v6_launch<F, 0>(a, grid, stream); break;
       case 3: conv_v6_launch<F, 3>(a, grid, stream); break;
-      default: conv_v6_launch<F, 1>(a, grid, stream);
+      case 17: conv_v6_launch<F, 17>(a, grid, stream); break;
+      case 1: conv_v6_launch<F, 1>(a, grid, stream); break;
+      default: conv_v6_launch<F, 19>(a, grid, stream);
     }
   };
   if (a.gnp) {   // GroupNorm statistics epilogue (split-DMA main loop only)
     if (conv_fast_ok(a)) {
       conv_magic(a);
-      conv_v6_launch<true, 1, true>(a, grid, stream);
+      conv_v6_launch<true, 19, true>(a, grid, stream);
     } else {
-      conv_v6_launch<false, 1, true>(a, grid, stream);
+      conv_v6_launch<false, 19, true>(a, grid, stream);
     }
     return;
   }

@@ -565,12 +565,18 @@ static int num_cus() {
 // v6 DMA placement (pq::run DS): CGS_V6_DS at first use, cgs_v6_set_mode() after (in-process A/B).
 // Default 1 (A parts in phase 0, B parts in phase 1): +4..11 % over all-in-phase-0 on the SDXL
 // N = 640 / 1280 GEMMs and +2..4 % on the Cout = 320 convs (profiles/r03/v6_dma_split.log).
-static int g_v6_ds = -1;
+// Convs default to 19 (balanced split, phase 0 without the read drain: +1.5..6 % over 1 on the
+// Cout = 320 convs, profiles/r03/v6_phase0_nodrain.log); GEMMs keep 1 (19 / 17 within -6..+3 %).
+static int g_v6_ds = -1, g_v6_conv_ds = -1;
 int v6_ds() {
   if (g_v6_ds < 0) g_v6_ds = getenv("CGS_V6_DS") ? atoi(getenv("CGS_V6_DS")) : 1;
   return g_v6_ds;
 }
-CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; }
+int v6_conv_ds() {
+  if (g_v6_conv_ds < 0) g_v6_conv_ds = getenv("CGS_V6_CONV_DS") ? atoi(getenv("CGS_V6_CONV_DS")) : 19;
+  return g_v6_conv_ds;
+}
+CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; g_v6_conv_ds = m; }
 
 template <bool LN, int DS>
 static void gemm_v6_go(int grid, const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
@@ -600,6 +606,8 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
     switch (ds) {
       case 0: gemm_v6_go<L, 0>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
       case 3: gemm_v6_go<L, 3>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      case 17: gemm_v6_go<L, 17>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      case 19: gemm_v6_go<L, 19>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
       default: gemm_v6_go<L, 1>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs);
     }
   };

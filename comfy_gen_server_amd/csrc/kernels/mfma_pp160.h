@@ -347,7 +347,10 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       if constexpr ((DS & 4) != 0) stage_part(0, kst, slot2);
       read_frags(S, 0);
       if constexpr ((DS & 4) == 0) stage_part(0, kst, slot2);
-      pp::wait_lgkm0();
+      // DS & 16: phase 0 does not drain its fragment reads before the barrier (the MFMAs wait for them
+      // one by one). WAR-safe: slot kt is next restaged three phases on; phase 1 keeps the drain because
+      // the other group restages the slot it reads one segment later.
+      if constexpr ((DS & 16) == 0) pp::wait_lgkm0();
       pp::barrier();
       mma();
       pp::barrier();
