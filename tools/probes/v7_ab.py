@@ -57,6 +57,16 @@ for name, M, N, K, gg, res in SHAPES:
             e.record()
             torch.cuda.synchronize()
             res_t[v].append(s.elapsed_time(e) / 20)
+    outs = {}
+    for v in VARIANTS:
+        lib.cgs_v7_set_dbg(v)
+        out.fill_(0)
+        run()
+        torch.cuda.synchronize()
+        outs[v] = out.clone()
+    same = all(torch.equal(outs[v], outs[VARIANTS[0]]) for v in VARIANTS)
     lib.cgs_v7_set_dbg(0)
     line = " ".join(f"dbg{v}={2 * M * N * K / sorted(ts)[1] / 1e9:.0f}" for v, ts in res_t.items())
+    line += f" bitwise-equal={same}"
+    del outs
     print(f"{name:14s} M={M} N={N} K={K} TF/s (median of 3) {line}", flush=True)
