@@ -277,6 +277,27 @@ __device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x
   if constexpr (!MSUM) l_run += ps;
 }
 
+// O epilogue of the D = 64 kernels (T21): lanes l and l + 32 hold the same query row as 8-B halves of
+// each 16-B column group; one v_permlane32_swap per dword pairs them so every lane stores 16 B (4
+// instead of 8 store instructions per lane, full 32-B runs per lane pair). Needs 16-B aligned rows (al16).
+// Measured vs the 8-B form (profiles/r03/attn_t21_stores.log): level-2 self-attention +12 %, the
+// short-KV cross-attention +14..16 %, level-1 self-attention neutral; outputs bitwise equal.
+__device__ __forceinline__ void af_store_row64(u16* __restrict__ orow, const f32x16 (&ot)[2], float inv, int hf,
+                                               bool ok) {
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp) {
+      uint2 a = pack4_bf16(ot[dt][8 * rp] * inv, ot[dt][8 * rp + 1] * inv, ot[dt][8 * rp + 2] * inv,
+                           ot[dt][8 * rp + 3] * inv);
+      uint2 b = pack4_bf16(ot[dt][8 * rp + 4] * inv, ot[dt][8 * rp + 5] * inv, ot[dt][8 * rp + 6] * inv,
+                           ot[dt][8 * rp + 7] * inv);
+      auto rx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+      auto ry = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+      if (ok) *reinterpret_cast<uint4*>(orow + dt * 32 + 16 * rp + 8 * hf) = uint4{rx[0], ry[0], rx[1], ry[1]};
+    }
+}
+
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
 // workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
 template <int NW>
@@ -446,18 +467,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (lse && q_ok && hf == 0)
     lse[((long long)b * H + h) * Sq + q_row] = l_tot > 0.f ? (m_run + __log2f(l_tot)) * 0.69314718055994531f : -INFINITY;
-  if (q_ok) {
-    u16* orow = obase + (long long)q_row * oss;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        s16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(ot[dt][4 * r4 + j] * inv);
-        *reinterpret_cast<s16x4*>(orow + dt * 32 + 8 * r4 + 4 * hf) = w;
-      }
-  }
+  af_store_row64(obase + (long long)q_row * oss, ot, inv, hf, q_ok);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -738,18 +748,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
     }
   const float l_tot = ps + __shfl_xor(ps, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if (q_ok) {
-    u16* orow = obase + (long long)q_row * oss;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        s16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(ot[dt][4 * r4 + j] * inv);
-        *reinterpret_cast<s16x4*>(orow + dt * 32 + 8 * r4 + 4 * hf) = w;
-      }
-  }
+  af_store_row64(obase + (long long)q_row * oss, ot, inv, hf, q_ok);
 }
 
 // ------------------------------------------------------------------------------------------------
