@@ -527,16 +527,17 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
       case 0: conv_v6_launch<F, 0>(a, grid, stream); break;
       case 3: conv_v6_launch<F, 3>(a, grid, stream); break;
       case 17: conv_v6_launch<F, 17>(a, grid, stream); break;
+      case 19: conv_v6_launch<F, 19>(a, grid, stream); break;
       case 1: conv_v6_launch<F, 1>(a, grid, stream); break;
-      default: conv_v6_launch<F, 19>(a, grid, stream);
+      default: conv_v6_launch<F, 51>(a, grid, stream);
     }
   };
   if (a.gnp) {   // GroupNorm statistics epilogue (split-DMA main loop only)
     if (conv_fast_ok(a)) {
       conv_magic(a);
-      conv_v6_launch<true, 19, true>(a, grid, stream);
+      conv_v6_launch<true, 51, true>(a, grid, stream);
     } else {
-      conv_v6_launch<false, 19, true>(a, grid, stream);
+      conv_v6_launch<false, 51, true>(a, grid, stream);
     }
     return;
   }

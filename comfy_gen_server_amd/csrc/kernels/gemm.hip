@@ -565,15 +565,17 @@ static int num_cus() {
 // v6 DMA placement (pq::run DS): CGS_V6_DS at first use, cgs_v6_set_mode() after (in-process A/B).
 // Default 1 (A parts in phase 0, B parts in phase 1): +4..11 % over all-in-phase-0 on the SDXL
 // N = 640 / 1280 GEMMs and +2..4 % on the Cout = 320 convs (profiles/r03/v6_dma_split.log).
-// Convs default to 19 (balanced split, phase 0 without the read drain: +1.5..6 % over 1 on the
-// Cout = 320 convs, profiles/r03/v6_phase0_nodrain.log); GEMMs keep 1 (19 / 17 within -6..+3 %).
+// Convs default to 51 = 19 | 32 (balanced split, phase 0 without the read drain: +1.5..6 % over 1 on
+// the Cout = 320 convs, profiles/r03/v6_phase0_nodrain.log; 8-B column-tile-4 stores, which measured
+// 1.5..5 % faster there than the permlane16-paired 16-B stores the GEMMs use,
+// profiles/r03/v6_tile4_store_pairing.log); GEMMs keep 1 (19 / 17 within -6..+3 %).
 static int g_v6_ds = -1, g_v6_conv_ds = -1;
 int v6_ds() {
   if (g_v6_ds < 0) g_v6_ds = getenv("CGS_V6_DS") ? atoi(getenv("CGS_V6_DS")) : 1;
   return g_v6_ds;
 }
 int v6_conv_ds() {
-  if (g_v6_conv_ds < 0) g_v6_conv_ds = getenv("CGS_V6_CONV_DS") ? atoi(getenv("CGS_V6_CONV_DS")) : 19;
+  if (g_v6_conv_ds < 0) g_v6_conv_ds = getenv("CGS_V6_CONV_DS") ? atoi(getenv("CGS_V6_CONV_DS")) : 51;
   return g_v6_conv_ds;
 }
 CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; g_v6_conv_ds = m; }

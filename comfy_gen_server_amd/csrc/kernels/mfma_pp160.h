@@ -176,6 +176,16 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
     // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain
     auto colj = [&](int j) { return j < 4 ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : 64 + 4 * fq; };
+    // column tile 4 (8 B per lane and row): row blocks i / i+1 are paired with v_permlane16_swap so a
+    // lane stores 16 B (fq even: row block i, cols 64 + 8 (fq / 2) .. + 7; fq odd: row block i + 1)
+    auto store_t4 = [&](int i, uint2 a, uint2 b) {
+      const auto rx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+      const int row = m_w + 16 * (i + (fq & 1)) + fr;
+      const int col = n_w + 64 + 8 * (fq >> 1);
+      if (row < M && col < N)
+        *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{rx[0], ry[0], rx[1], ry[1]};
+    };
     float4 bv[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
@@ -251,9 +261,9 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
             *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) =
                 uint4{pk[i][2 * p].x, pk[i][2 * p].y, pk[i][2 * p + 1].x, pk[i][2 * p + 1].y};
         }
-        const int col = n_w + 64 + 4 * fq;
-        if (row < M && col < N) *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pk[i][4];
       }
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
       const int img = m_w / e.hw;
       const int nbk = e.hw >> 6;
       float* dst = e.gnp + (size_t)(img * nbk + ((m_w - img * e.hw) >> 6)) * N * 2;
@@ -293,9 +303,17 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         if (row < M && col < N)
           *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{lo.x, lo.y, hi.x, hi.y};
       }
-      const int col = n_w + 64 + 4 * fq;
-      const uint2 w4 = val(i, 4);
-      if (row < M && col < N) *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = w4;
+    }
+    if constexpr ((DS & 32) != 0) {   // A/B reference: 8-B stores for column tile 4
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m_w + 16 * i + fr, col = n_w + 64 + 4 * fq;
+        const uint2 w4 = val(i, 4);
+        if (row < M && col < N) *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = w4;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) store_t4(i, val(i, 4), val(i + 1, 4));
     }
   };
   using T0 = std::false_type;

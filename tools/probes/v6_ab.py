@@ -104,7 +104,8 @@ for name, N, H, W, Cin, Cout, k, s in CONVS:
         return lib.cgs_conv2d_nhwc_v(x.data_ptr(), None, Cin, w.data_ptr(), b.data_ptr(), None, out.data_ptr(), N, H, W,
                                      Cin, Cout, k, k, s, p, Ho, Wo, 0, variant, core._stream())
 
-    runs = {f"v6ds{m}": ((lambda m=m: lib.cgs_v6_set_mode(m)), (lambda: cv(6))) for m in MODES}
+    CMODES = [int(m) for m in os.environ.get("V6_CONV_MODES", ",".join(map(str, MODES))).split(",")]
+    runs = {f"v6ds{m}": ((lambda m=m: lib.cgs_v6_set_mode(m)), (lambda: cv(6))) for m in CMODES}
     runs["v5"] = ((lambda: None), (lambda: cv(5)))
     ab(name, 2.0 * N * Ho * Wo * Cout * Cin * k * k, runs, check)
     del x, w, out
