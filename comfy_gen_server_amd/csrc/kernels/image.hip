@@ -308,10 +308,17 @@ __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__
                                                          const u16* __restrict__ gamma, const u16* __restrict__ beta,
                                                          u16* __restrict__ y, long long chunks, int HW, int C) {
   __shared__ float inv_s[GRN_MAXN];
-  for (int n = threadIdx.x; n < N; n += 256) {
-    float t = 0.f;
-    for (int b = 0; b < nblk; ++b) t += bsum[(size_t)n * nblk + b];
-    inv_s[n] = 1.f / (t / (float)C + 1e-6f);
+  // one wave per image, one finalize-block sum per lane (nblk <= 64: C <= 16384), then a wave sum: one
+  // L2 round trip per block instead of nblk serial loads by one thread -- with one 16-B chunk per
+  // thread that serial prologue was most of the kernel (33.7 us average per call in r03zl)
+  {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (int n = wv; n < N; n += 4) {
+      float t = 0.f;
+      for (int b = ln; b < nblk; b += 64) t += bsum[(size_t)n * nblk + b];
+      t = wave_sum(t);
+      if (ln == 0) inv_s[n] = 1.f / (t / (float)C + 1e-6f);
+    }
   }
   __syncthreads();
   const unsigned cpr = (unsigned)C >> 3;
