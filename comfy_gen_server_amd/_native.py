@@ -149,6 +149,7 @@ KERNEL_SIGNATURES = {
     "cgs_v7_ws_bytes": [_I, _I, _I],
     "cgs_v7_set_dbg": [_I],
     "cgs_v6_set_mode": [_I],
+    "cgs_flash_attn_fwd_kv2": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _F, _P],
     "cgs_conv2d_nhwc_gns": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P],
     "cgs_groupnorm_nhwc_part": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],

@@ -298,14 +298,24 @@ __device__ __forceinline__ void af_store_row64(u16* __restrict__ orow, const f32
     }
 }
 
+// Second K/V source (TWO): keys [0, sk1) come from the kernel's k / v, keys [sk1, Sk) from k / v here
+// (same head stride). Stable Cascade's self-attention attends over cat([x, kv_mapped]) -- with two
+// sources neither the concat nor a separate K / V projection of it is materialised.
+struct KV2 {
+  const u16* k;
+  const u16* v;
+  int sk1;
+  long long ksb, kss, vsb, vss;
+};
+
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
 // workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
-template <int NW>
+template <int NW, bool TWO = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
     long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
-    float c, int nqb, float* __restrict__ lse = nullptr) {
+    float c, int nqb, float* __restrict__ lse = nullptr, KV2 kv2 = KV2{nullptr, nullptr, 0, 0, 0, 0, 0}) {
   __shared__ __attribute__((aligned(16))) u16 Ks[2][64 * 64];
   __shared__ __attribute__((aligned(16))) u16 Vs[2][64 * 64];
 
@@ -362,6 +372,29 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     }
     return r;
   };
+  // two-source loads: key -> (source, row) per lane (keys past Sk read the last key: masked later)
+  const u16* k2base = TWO ? kv2.k + b * kv2.ksb + h * ksh : nullptr;
+  const u16* v2base = TWO ? kv2.v + b * kv2.vsb + h * vsh : nullptr;
+  auto gload2 = [&](bool isk, int t) -> Stg {
+    Stg r;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int key = min(t * 64 + st_key[i], Sk - 1);
+      const u16* p = key < kv2.sk1 ? (isk ? kbase + (long long)key * kss : vbase + (long long)key * vss)
+                                   : (isk ? k2base + (long long)(key - kv2.sk1) * kv2.kss
+                                          : v2base + (long long)(key - kv2.sk1) * kv2.vss);
+      r.v[i] = *reinterpret_cast<const s16x8*>(p + st_c * 8);
+    }
+    return r;
+  };
+  auto ldk = [&](int t) -> Stg {
+    if constexpr (TWO) return gload2(true, t);
+    else return gload(kbase, kss, koff, kclamp, t);
+  };
+  auto ldv = [&](int t) -> Stg {
+    if constexpr (TWO) return gload2(false, t);
+    else return gload(vbase, vss, voff, vclamp, t);
+  };
   auto lds_put = [&](u16* tile, const int (&off)[LPT], const Stg& x) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) *reinterpret_cast<s16x8*>(&tile[off[i]]) = x.v[i];
@@ -417,9 +450,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
 
   // prologue: K(0) -> slot 0, K(1) -> slot 1, V(0) -> slot 0; S(0)
   {
-    const Stg k0 = gload(kbase, kss, koff, kclamp, 0);
-    const Stg k1 = gload(kbase, kss, koff, kclamp, n > 1 ? 1 : 0);
-    const Stg v0 = gload(vbase, vss, voff, vclamp, 0);
+    const Stg k0 = ldk(0);
+    const Stg k1 = ldk(n > 1 ? 1 : 0);
+    const Stg v0 = ldv(0);
     lds_put(Ks[0], k_woff, k0);
     lds_put(Ks[1], k_woff, k1);
     lds_put(Vs[0], v_woff, v0);
@@ -427,8 +460,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
   // two register stages: the K / V rows written to LDS at the end of tile t were loaded during tile
   // t - 1, so a global load has a whole tile of compute (not just the rest of its own tile) to land
   Stg kq[2], vq[2];
-  kq[0] = gload(kbase, kss, koff, kclamp, min(2, n - 1));
-  vq[0] = gload(vbase, vss, voff, vclamp, min(1, n - 1));
+  kq[0] = ldk(min(2, n - 1));
+  vq[0] = ldv(min(1, n - 1));
   __syncthreads();
   qk(Ks[0], sA);
 
@@ -437,8 +470,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
   auto body = [&](int t, f32x16 (&sCur)[2], f32x16 (&sNext)[2], auto ldc) {
     constexpr int LD = decltype(ldc)::value, WR = LD ^ 1;
     const int slot = t & 1;
-    kq[LD] = gload(kbase, kss, koff, kclamp, min(t + 3, n - 1));
-    vq[LD] = gload(vbase, vss, voff, vclamp, min(t + 2, n - 1));
+    kq[LD] = ldk(min(t + 3, n - 1));
+    vq[LD] = ldv(min(t + 2, n - 1));
     qk(Ks[slot ^ 1], sNext);
     af_softmax<false, true>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
     pv(Vs[slot], pf, ot);
@@ -1133,6 +1166,38 @@ CGS_EXPORT int cgs_flash_attn_fwd_v(const void* q, const void* k, const void* v,
                                  scale, nullptr, 0, nullptr, stream);
   g_attn_variant = saved;
   return rc;
+}
+
+// D = 64 attention over the key concat of two K / V sources (see KV2): keys [0, Sk1) from k1 / v1 ([B, Sk1]
+// rows), keys [Sk1, Sk1 + Sk2) from k2 / v2. Head stride D in every source; no mask.
+CGS_EXPORT int cgs_flash_attn_fwd_kv2(const void* q, const void* k1, const void* v1, const void* k2, const void* v2,
+                                      void* o, int B, int H, int Sq, int Sk1, int Sk2, long long qsb, long long qss,
+                                      long long k1sb, long long k1ss, long long v1sb, long long v1ss, long long k2sb,
+                                      long long k2ss, long long v2sb, long long v2ss, long long osb, long long oss,
+                                      float scale, hipStream_t stream) {
+  const int Sk = Sk1 + Sk2;
+  const bool al16 = ((qss | qsb | k1sb | k1ss | v1sb | v1ss | k2sb | k2ss | v2sb | v2ss | osb | oss) & 7) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k1) | reinterpret_cast<uintptr_t>(v1) |
+                      reinterpret_cast<uintptr_t>(k2) | reinterpret_cast<uintptr_t>(v2) | reinterpret_cast<uintptr_t>(o)) &
+                     15) == 0;
+  if (!al16 || Sk1 <= 0 || Sk2 <= 0 || Sq <= 0 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
+  const long long nwg256 = (long long)((Sq + 255) / 256) * B * H;
+  const bool small = nwg256 < num_cus_attn();
+  const int rows = small ? 128 : 256;
+  const int nqb2 = (Sq + rows - 1) / rows;
+  const long long nwg2 = (long long)nqb2 * B * H;
+  if (nwg2 > 0x7fffffff) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * 1.4426950408889634f;
+  const KV2 kv2{(const u16*)k2, (const u16*)v2, Sk1, k2sb, k2ss, v2sb, v2ss};
+  if (small)
+    attn_fwd_d64_kernel<4, true><<<dim3((unsigned)nwg2), 256, 0, stream>>>(
+        (const u16*)q, (const u16*)k1, (const u16*)v1, (u16*)o, H, Sq, Sk, qsb, qss, 64, k1sb, k1ss, 64, v1sb, v1ss, 64,
+        osb, oss, 64, sl2, nqb2, nullptr, kv2);
+  else
+    attn_fwd_d64_kernel<8, true><<<dim3((unsigned)nwg2), 512, 0, stream>>>(
+        (const u16*)q, (const u16*)k1, (const u16*)v1, (u16*)o, H, Sq, Sk, qsb, qss, 64, k1sb, k1ss, 64, v1sb, v1ss, 64,
+        osb, oss, 64, sl2, nqb2, nullptr, kv2);
+  return (int)hipGetLastError();
 }
 
 CGS_EXPORT int cgs_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,

@@ -118,7 +118,7 @@ class ResBlock(nn.Module):
         return self.channelwise(h, residual=x)
 
 
-class OptimizedAttention(nn.Module):
+class OptimizedAttention(nn.Module, DerivedMixin):
     def __init__(self, c, nhead, dtype=None, device=None):
         super().__init__()
         self.heads = nhead
@@ -127,9 +127,35 @@ class OptimizedAttention(nn.Module):
         self.to_v = Linear(c, c, dtype=dtype, device=device)
         self.out_proj = Linear(c, c, dtype=dtype, device=device)
 
+    def _fused(self, names, x):
+        """[W_a; W_b; ...] / [b_a; b_b; ...] in x's dtype (cached, dropped on weight patches)."""
+        def build():
+            mods = [getattr(self, n) for n in names]
+            w = torch.cat([_cast(m.weight, x) for m in mods], 0).contiguous()
+            b = torch.cat([_cast(m.bias, x) if m.bias is not None else
+                           torch.zeros(m.out_features, device=x.device, dtype=x.dtype) for m in mods], 0).contiguous()
+            return w, b
+        return self._derived_get(("fused",) + tuple(names) + (x.dtype, x.device), build)
+
     def forward(self, q, k, v, residual=None):
         o = ops.attention(self.to_q(q), self.to_k(k), self.to_v(v), self.heads)
         return self.out_proj(o, residual=residual)
+
+    def forward_self(self, xs, kv, residual=None):
+        """Stable Cascade self-attention: q from xs, keys / values over cat([xs, kv]) (common.py
+        Attention2D). One fused QKV GEMM over xs and one fused KV GEMM over kv; the attention kernel reads
+        the keys from the two projections directly, so neither the input nor the K / V concat is built."""
+        C = xs.shape[-1]
+        if xs.is_cuda and xs.dtype == torch.bfloat16 and C % 64 == 0 and C // self.heads == 64:
+            wq, bq = self._fused(("to_q", "to_k", "to_v"), xs)
+            wk, bk = self._fused(("to_k", "to_v"), xs)
+            qkv = ops.linear(xs, wq, bq)
+            kv2 = ops.linear(kv.to(xs.dtype), wk, bk)
+            o = ops.attention_kv2(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], kv2[..., :C], kv2[..., C:],
+                                  self.heads)
+            return self.out_proj(o, residual=residual)
+        kvc = torch.cat([xs, kv.to(xs.dtype)], dim=1)
+        return self.forward(xs, kvc, kvc, residual=residual)
 
 
 class Attention2D(nn.Module):
@@ -140,9 +166,9 @@ class Attention2D(nn.Module):
     def forward(self, x_norm, kv, self_attn=False, residual=None):
         B, H, W, C = x_norm.shape
         xs = x_norm.reshape(B, H * W, C)
-        if self_attn:
-            kv = torch.cat([xs, kv.to(xs.dtype)], dim=1)
         res = None if residual is None else residual.reshape(B, H * W, C)
+        if self_attn:
+            return self.attn.forward_self(xs, kv, residual=res).reshape(B, H, W, C)
         return self.attn(xs, kv, kv, residual=res).reshape(B, H, W, C)
 
 

@@ -344,6 +344,31 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     return attention_reference(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
 
 
+def attention_kv2(q: torch.Tensor, k1: torch.Tensor, v1: torch.Tensor, k2: torch.Tensor, v2: torch.Tensor,
+                  heads: int) -> torch.Tensor:
+    """``attention(q, cat([k1, k2], 1), cat([v1, v2], 1), heads)`` without materialising either concat:
+    the D = 64 kernel reads keys [0, S1) from k1 / v1 and [S1, S1 + S2) from k2 / v2 (Stable Cascade's
+    self-attention over cat([x, kv]), cascade/common.py Attention2D). Inputs may be strided views (last
+    dim contiguous), e.g. column slices of one fused QKV projection."""
+    B, Sq, HD = q.shape
+    D = HD // heads
+    ok = (D == 64 and q.is_cuda and q.dtype == torch.bfloat16 and all(
+        t.dtype == q.dtype and t.dim() == 3 and t.shape[0] == B and t.shape[2] == HD and t.stride(-1) == 1
+        for t in (k1, v1, k2, v2)) and k1.shape[1] == v1.shape[1] and k2.shape[1] == v2.shape[1]
+        and q.stride(-1) == 1 and backend_for("attention", q, "cgs_flash_attn_fwd_kv2") == "hip")
+    if ok:
+        o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
+        err = _lib().cgs_flash_attn_fwd_kv2(
+            q.data_ptr(), k1.data_ptr(), v1.data_ptr(), k2.data_ptr(), v2.data_ptr(), o.data_ptr(), B, heads, Sq,
+            k1.shape[1], k2.shape[1], q.stride(0), q.stride(1), k1.stride(0), k1.stride(1), v1.stride(0), v1.stride(1),
+            k2.stride(0), k2.stride(1), v2.stride(0), v2.stride(1), o.stride(0), o.stride(1), 1.0 / math.sqrt(D),
+            _stream())
+        if err == 0:
+            count("attention", "hip")
+            return o
+    return attention(q, torch.cat([k1, k2.to(k1.dtype)], dim=1), torch.cat([v1, v2.to(v1.dtype)], dim=1), heads)
+
+
 def attention_lse(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int):
     """Unmasked attention plus the natural-log log-sum-exp of the scaled scores per (b, h, query):
     ``(o [B, Sq, H*D] in q's dtype, lse fp32 [B, H, Sq])`` -- the partial result of one K/V block

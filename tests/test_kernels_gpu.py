@@ -906,3 +906,19 @@ def test_conv_gn_stats_epilogue(cuda, N, H, W, Cin, Cout, pre):
     xf = out.permute(0, 3, 1, 2).float() + (p.float()[:, :, None, None] if pre else 0.0)
     ref = F.silu(F.group_norm(xf, 32, g.float(), be.float(), 1e-5))
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,Sq,S2", [(2, 32, 576, 85), (1, 8, 300, 77), (2, 4, 1024, 8)])
+def test_attention_two_kv_sources(cuda, B, H, Sq, S2):
+    """Stable Cascade self-attention over cat([x, kv]) with the keys read from two (strided) sources:
+    == attention over the materialised concat; the HIP two-source kernel runs."""
+    torch.manual_seed(5)
+    C = H * 64
+    qkv = torch.randn(B, Sq, 3 * C, device=cuda).to(torch.bfloat16)
+    kv2 = torch.randn(B, S2, 2 * C, device=cuda).to(torch.bfloat16)
+    q, k1, v1 = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    k2, v2 = kv2[..., :C], kv2[..., C:]
+    o = ops.attention_kv2(q, k1, v1, k2, v2, H)
+    assert ops.stats().get(("attention", "hip"), 0) == 1
+    ref = core.attention_reference(q.float(), torch.cat([k1, k2], 1).float(), torch.cat([v1, v2], 1).float(), H)
+    assert _rel(o, ref) < 1e-2
