@@ -8,5 +8,5 @@ timeout -k 10 400 python -u -m pytest -q -x --timeout 120 --timeout-method threa
 tail -1 gpurun_out/r03ze_tests.log
 timeout -k 10 300 python -u tools/probes/gns_ab.py > gpurun_out/r03ze_gns.log 2>&1
 rc=$?; echo "gns rc=$rc"; grep -v amdgpu.ids gpurun_out/r03ze_gns.log; [ $rc = 0 ] || exit $rc
-V6_MODES=1,9 timeout -k 10 300 python -u tools/probes/v6_ab.py > gpurun_out/r03ze_v6ab.log 2>&1
+V6_MODES=1,17,19 timeout -k 10 300 python -u tools/probes/v6_ab.py > gpurun_out/r03ze_v6ab.log 2>&1
 rc=$?; echo "v6ab rc=$rc"; grep -v amdgpu.ids gpurun_out/r03ze_v6ab.log; exit $rc
