@@ -540,7 +540,7 @@ struct DenseA32 {
 
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
-template <bool LN = false, int DS = 0>
+template <bool LN = false, int DS = 0, bool GG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // (profiles/r03/v6_offsets32.log)
   DenseA8 al{A, lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
-  pq::run<DenseA8, LN, DS>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  pq::run<DenseA8, LN, DS, false, GG>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
 }
 static int num_cus() {
   static int n = 0;
@@ -580,17 +580,17 @@ int v6_conv_ds() {
 }
 CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; g_v6_conv_ds = m; }
 
-template <bool LN, int DS>
+template <bool LN, int DS, bool GG = false>
 static void gemm_v6_go(int grid, const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                        int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                        int tiles_m, int tiles_n, hipStream_t stream, const float* rs, const float* cs) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              pq::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
     attr_set = true;
   }
-  gemm_bf16_nt_v6_kernel<LN, DS><<<grid, pq::THREADS, pq::LDS, stream>>>(
+  gemm_bf16_nt_v6_kernel<LN, DS, GG><<<grid, pq::THREADS, pq::LDS, stream>>>(
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
       tiles_m, tiles_n, g_tile_group, rs, cs);
 }
@@ -603,6 +603,15 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
   const int ds = v6_ds();
+  if (epi & EPI_GEGLU) {   // GEGLU epilogue (pq::run GG): split-DMA main loop, N % 160 == 0 (host-checked)
+    if (epi & EPI_LNFOLD)
+      gemm_v6_go<true, 1, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n,
+                                stream, rs, cs);
+    else
+      gemm_v6_go<false, 1, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n,
+                                 stream, rs, cs);
+    return (int)hipGetLastError();
+  }
   auto go = [&](auto lnc) {
     constexpr bool L = decltype(lnc)::value;
     switch (ds) {
@@ -832,7 +841,8 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
       return (int)hipErrorInvalidValue;
     return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
   }
-  if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && !(epi & EPI_GEGLU) && ((uintptr_t)bias % 8 == 0))
+  if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && (!(epi & EPI_GEGLU) || (N % 160 == 0 && !(epi & EPI_RESIDUAL))) &&
+      ((uintptr_t)bias % 8 == 0))
     return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&
       ((uintptr_t)bias % 8 == 0) && (long long)M * lda * 2 < (1ll << 32) && (long long)N * ldw * 2 < (1ll << 32))
@@ -912,9 +922,9 @@ static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, 
   if (variant == 8 || (variant >= 10 && variant <= 14))
     return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, variant,
                           rs, cs);
-  const bool v6_ok = !(epi & EPI_GEGLU) && N % 160 == 0;
+  const bool v6_ok = N % 160 == 0;   // incl. GEGLU (pq::run GG)
   if (variant == 6 && !v6_ok) return (int)hipErrorInvalidValue;
-  if (variant == 6 || (variant < 0 && v6_ok && N <= 1280))
+  if (variant == 6 || (variant < 0 && v6_ok && !(epi & EPI_GEGLU) && N <= 1280))
     return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
   return gemm_v7_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, ws, ws_bytes, stream,
                         rs, cs);

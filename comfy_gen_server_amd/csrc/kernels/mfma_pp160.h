@@ -43,6 +43,14 @@ __device__ __forceinline__ int b_col160(int r) {
   return 80 * g + 32 * (j >> 1) + 8 * (q >> 2) + 4 * (j & 1) + (q & 3);
 }
 
+// GEGLU staging (run<..., GG>): staged B row r of group g = r / 80, tile j, row q in the tile -> output column
+// c = 40 g + 8 j + (q & 7) of the tile, 'a' (q < 8) or 'g' (q >= 8) weight row of the 16-row interleave.
+__device__ __forceinline__ int gg_row160(int r) {
+  const int g = r >= 80, l = r - 80 * g, j = l >> 4, q = l & 15;
+  const int c = 40 * g + 8 * j + (q & 7);
+  return 32 * (c >> 4) + (c & 15) + 16 * (q >> 3);
+}
+
 // AL: loader with setup(slot, global_row) for slots 0..3 (tile rows slot*64 + (tid >> 3)) and
 // src(slot, k0) -> this lane's 16-B source for K offset k0 (swizzled chunk already applied).
 //
@@ -59,7 +67,13 @@ __device__ __forceinline__ int b_col160(int r) {
 // 64-row block (one wave's rows) and column, (mean, M2) by an exact two-pass over the wave's registers
 // (DPP row sums) -- into e.gnp in the gn_partial layout with 64 pixels per block, so the next GroupNorm
 // skips its statistics pass over the tensor (host: rows per image % 256 == 0).
-template <class AL, bool LN = false, int DS = 0, bool GNS = false>
+// GG: GEGLU epilogue (out = a * gelu(g), N / 2 output columns) from the 16-row-interleaved weights of the
+// 256-wide kernels ([a0..a15, g0..g15, ...], geglu_interleave): the B staging puts, in every 16-column MFMA
+// tile, 8 'a' rows in lanes fq = 0, 1 and their 8 'g' rows in fq = 2, 3, so one v_permlane32_swap of row
+// blocks i / i + 1 hands every lane 4 (a, g) pairs (lower lanes: row block i, upper: i + 1). 160 weight
+// rows = 5 interleave groups = 80 output columns per tile (whole rounds where the 256-wide tiles leave a
+// partial one, e.g. SDXL batch 1: M = 2048, N = 10240 -> 512 tiles vs 320). Host: N % 160 == 0.
+template <class AL, bool LN = false, int DS = 0, bool GNS = false, bool GG = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -89,7 +103,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       const int r = g * 64 + lrow;
-      int n = n0 + b_col160(r < BN ? r : BN - 1);
+      int n = n0 + (GG ? gg_row160(r < BN ? r : BN - 1) : b_col160(r < BN ? r : BN - 1));
       n = n < N ? n : N - 1;
       bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
     }
@@ -174,8 +188,12 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   auto epilogue_t = [&](int m0, int n0, auto has_bias_c, auto has_res_c) {
     constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
     const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
-    // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain
-    auto colj = [&](int j) { return j < 4 ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : 64 + 4 * fq; };
+    // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain;
+    // GEGLU: the weight row of acc[.][j][0] relative to n_w (gg_row160 of staged row 16 j + 4 fq)
+    auto colj = [&](int j) {
+      if constexpr (GG) return gg_row160(grp * 80 + 16 * j + 4 * fq) - grp * 80;
+      return j < 4 ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : 64 + 4 * fq;
+    };
     // column tile 4 (8 B per lane and row): row blocks i / i+1 are paired with v_permlane16_swap so a
     // lane stores 16 B (fq even: row block i, cols 64 + 8 (fq / 2) .. + 7; fq odd: row block i + 1)
     auto store_t4 = [&](int i, uint2 a, uint2 b) {
@@ -245,6 +263,30 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
       return pack4_bf16(v0, v1, v2, v3);
     };
+    if constexpr (GG) {
+      // bias / LN already applied per weight row; pair row blocks (i, i+1) across the half-waves
+      const int oc0 = n0 / 2 + grp * 40 + 4 * (fq & 1);
+      const int Nout = N / 2;
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const int row = m_w + 16 * (i + (fq >> 1)) + fr;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          float o[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float bt = t == 0 ? bv[j].x : t == 1 ? bv[j].y : t == 2 ? bv[j].z : bv[j].w;
+            const float x0 = acc[i][j][t] * e.alpha + bt, x1 = acc[i + 1][j][t] * e.alpha + bt;
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
+            o[t] = __uint_as_float(r[0]) * gelu_sig(__uint_as_float(r[1]));
+          }
+          const int col = oc0 + 8 * j;
+          if (row < M && col < Nout)
+            *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = pack4_bf16(o[0], o[1], o[2], o[3]);
+        }
+      }
+      return;
+    }
     if constexpr (GNS) {
       uint2 pk[4][5];
 #pragma unroll

@@ -216,13 +216,15 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
             if K % 64 == 0:
                 if K >= 128:
                     cands.append(("v7", lambda: run_hip(7)))
+                    if N2 % 160 == 0:    # 256x160 tiles with the GEGLU epilogue (pq::run GG)
+                        cands.append(("v6", lambda: run_hip(6)))
                 cands.append(("v5", lambda: run_hip(5)))
             cands.append(("v4", lambda: run_hip(4)))
             if _underfilled(M, N2):
                 cands += [("v8", lambda: run_hip(8))] + [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
             cands.append(("hip", lambda: run_hip(-1)))
             choice = autotune.choose(("gemm_geglu", M, N2, K, epi), cands, default="hip")
-        variant = {"v7": 7, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
+        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N2 // 2)
     count("gemm_geglu", be)
     # reference path expects the *interleaved* weight too, undo it
@@ -1089,8 +1091,14 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
     variant = -1                  # v6 / v7 by shape
     if _underfilled(M, N) and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
+        if geglu and N % 160 == 0:    # 256x160 GEGLU (whole rounds where 256x256 leaves a partial one)
+            cands.append(("v6", lambda: run(6)))
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v7")
-        variant = {"v8": 8, **_SMALL_NAMES}.get(choice, -1)
+        variant = {"v8": 8, "v6": 6, **_SMALL_NAMES}.get(choice, -1)
+    elif geglu and N % 160 == 0 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), [("v7", lambda: run(7)), ("v6", lambda: run(6))],
+                                 default="v7")
+        variant = 6 if choice == "v6" else 7
     elif not geglu and N % 160 == 0 and N > 1280 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         # wide non-GEGLU projections (fused QKV): 256x160 tiles give whole rounds where 256x256 leave
         # a partial last round (N = 1920 / 3840 at M = 65536 / 16384) -- measured per shape

@@ -922,3 +922,63 @@ def test_attention_two_kv_sources(cuda, B, H, Sq, S2):
     assert ops.stats().get(("attention", "hip"), 0) == 1
     ref = core.attention_reference(q.float(), torch.cat([k1, k2], 1).float(), torch.cat([v1, v2], 1).float(), H)
     assert _rel(o, ref) < 1e-2
+
+
+def test_cascade_self_attention_two_source_path(cuda, monkeypatch):
+    """Stable Cascade Stage C (head dim 64) on the device: self-attention through the fused QKV / KV
+    projections and the two-source kernel == the concat path (cat([x, kv]) -> to_q / to_k / to_v)."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    cfg = dict(c_in=16, c_out=16, c_r=64, c_cond=128, c_hidden=[128, 128], nhead=[2, 2], blocks=[[1, 1], [1, 1]],
+               block_repeat=[[1, 1], [1, 1]], level_config=["CTA", "CTA"], c_clip_text=64, c_clip_text_pooled=64,
+               c_clip_img=768, c_clip_seq=2, switch_level=[False])
+    m = SC.StageC(**cfg)
+    init_random_(m, seed=11)
+    m = m.to(device=cuda, dtype=torch.bfloat16)
+    g = torch.Generator().manual_seed(1)
+    args = (torch.randn(2, 16, 12, 12, generator=g), torch.tensor([0.3, 0.7]), torch.randn(2, 7, 64, generator=g),
+            torch.randn(2, 1, 64, generator=g), torch.randn(2, 1, 768, generator=g))
+    args = tuple(a.to(cuda, torch.bfloat16 if a.dim() > 1 else torch.float32) for a in args)
+    with torch.inference_mode():
+        ops.reset_stats()
+        fast = m(*args).float()
+        n_fast = ops.stats().get(("attention", "hip"), 0)
+        monkeypatch.setattr(SC.OptimizedAttention, "forward_self",
+                            lambda self, xs, kv, residual=None: self.forward(
+                                xs, torch.cat([xs, kv.to(xs.dtype)], 1), torch.cat([xs, kv.to(xs.dtype)], 1),
+                                residual=residual))
+        slow = m(*args).float()
+    assert n_fast > 0
+    assert _rel(fast, slow) < 2e-2
+
+
+@pytest.mark.parametrize("M,N2,K,ln", [(2048, 10240, 1280, False), (600, 5120, 640, False), (333, 2560, 320, False),
+                                       (2048, 10240, 1280, True), (1000, 5120, 640, True)])
+def test_gemm_geglu_v6(cuda, M, N2, K, ln):
+    """GEGLU on the 256x160 kernel (pq::run GG: 16-row-interleaved weights staged so that one
+    v_permlane32_swap pairs a / g), plain and with the LayerNorm fold, vs the fp32 reference."""
+    torch.manual_seed(2)
+    lib = _native.load_kernels()
+    a = (torch.randn(M, K, device=cuda) * (3 if ln else 1) + (1.5 if ln else 0)).to(torch.bfloat16)
+    w = (torch.randn(N2, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N2, device=cuda).to(torch.bfloat16)
+    if ln:
+        gamma = (torch.rand(K, device=cuda) + 0.5).to(torch.bfloat16)
+        beta = (torch.randn(K, device=cuda) * 0.2).to(torch.bfloat16)
+        rs = ops.layernorm_stats(a, 1e-5)
+        w2, cs, b2 = ops.lnfold_weights(core.geglu_interleave(w), core.geglu_interleave(b), gamma, beta)
+        y = torch.empty(M, N2 // 2, device=cuda, dtype=torch.bfloat16)
+        assert lib.cgs_gemm_bf16_lnfold_v(a.data_ptr(), w2.data_ptr(), y.data_ptr(), b2.data_ptr(), rs.data_ptr(),
+                                          cs.data_ptr(), M, N2, K, K, K, N2 // 2, core.EPI_BIAS | core.EPI_GEGLU,
+                                          None, 0, 6, core._stream()) == 0
+        h = F.layer_norm(a.float(), (K,), gamma.float(), beta.float(), 1e-5) @ w.float().t() + b.float()
+    else:
+        lib.cgs_gemm_set_variant(6)
+        try:
+            y = ops.linear_geglu(a, core.geglu_interleave(w), core.geglu_interleave(b))
+        finally:
+            lib.cgs_gemm_set_variant(-1)
+        h = a.float() @ w.float().t() + b.float()
+    x1, g = h.chunk(2, dim=-1)
+    ref = x1 * F.gelu(g)
+    assert _rel(y, ref) < 1.5e-2
