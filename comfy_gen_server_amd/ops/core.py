@@ -1091,7 +1091,7 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
     variant = -1                  # v6 / v7 by shape
     if _underfilled(M, N) and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
-        if geglu and N % 160 == 0:    # 256x160 GEGLU (whole rounds where 256x256 leaves a partial one)
+        if N % 160 == 0:    # 256x160 tiles (plain or GEGLU): whole rounds where 256x256 leaves a partial one
             cands.append(("v6", lambda: run(6)))
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v7")
         variant = {"v8": 8, "v6": 6, **_SMALL_NAMES}.get(choice, -1)
