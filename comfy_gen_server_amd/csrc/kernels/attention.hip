@@ -310,7 +310,7 @@ struct KV2 {
 
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
 // workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
-template <int NW, bool TWO = false>
+template <int NW, bool TWO = false, bool PRIO = true>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
@@ -474,7 +474,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     vq[LD] = ldv(min(t + 2, n - 1));
     qk(Ks[slot ^ 1], sNext);
     af_softmax<false, true>(sCur, pf, ot, m_run, l_run, c, t * 64, Sk, hf, &lsum);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // the dependent P.V MFMAs ahead of the partner's VALU
     pv(Vs[slot], pf, ot);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     lds_put(Ks[slot], k_woff, kq[WR]);
     lds_put(Vs[slot ^ 1], v_woff, vq[WR]);
     __syncthreads();
@@ -1070,6 +1072,10 @@ static int num_cus_attn() {
   return n;
 }
 CGS_EXPORT void cgs_attn_set_variant(int v) { g_attn_variant = v; }
+// s_setprio(1) around the P.V MFMAs of the D = 64 kernel (default on: +1.5 / +2.2 % at SDXL levels 1 / 2,
+// profiles/r03/attn_setprio_pv.log); cgs_attn_set_prio(0) selects the 8-wave form without it (A/B)
+static bool g_attn_prio = true;
+CGS_EXPORT void cgs_attn_set_prio(int on) { g_attn_prio = on != 0; }
 
 static int flash_attn_impl(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, int D,
                            long long qsb, long long qss, long long qsh, long long ksb, long long kss, long long ksh,
@@ -1130,6 +1136,10 @@ static int flash_attn_impl(const void* q, const void* k, const void* v, void* o,
     if (nwg2 > 0x7fffffff) return (int)hipErrorInvalidValue;
     if (small)
       attn_fwd_d64_kernel<4><<<dim3((unsigned)nwg2), 256, 0, stream>>>(
+          (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
+          osb, oss, osh, sl2, nqb2, lse);
+    else if (!g_attn_prio)
+      attn_fwd_d64_kernel<8, false, false><<<dim3((unsigned)nwg2), 512, 0, stream>>>(
           (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh,
           osb, oss, osh, sl2, nqb2, lse);
     else
