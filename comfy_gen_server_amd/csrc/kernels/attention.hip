@@ -681,7 +681,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_d64r2_kernel(
 // The reference runs this shape through the same optimized_attention as self-attention
 // (comfy/ldm/modules/attention.py:352-383); the general flash kernel would pay a full 64-key
 // pipeline for 77 keys.
-template <int NKT>
+template <int NKT, bool PRIO = true>
 __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
@@ -763,6 +763,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
     }
   f32x16 ot[2] = {f32x16{}, f32x16{}};
   const int i16 = lane & 15;
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // P.V MFMAs ahead of co-resident waves' softmax VALU
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
@@ -781,6 +782,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
         ot[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt * 2 + st], ot[dt], 0, 0, 0);
       }
     }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   const float l_tot = ps + __shfl_xor(ps, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   af_store_row64(obase + (long long)q_row * oss, ot, inv, hf, q_ok);
@@ -1094,10 +1096,17 @@ static int flash_attn_impl(const void* q, const void* k, const void* v, void* o,
     const int nqb3 = (Sq + 127) / 128;
     const long long nwg3 = (long long)nqb3 * B * H;
     if (nwg3 > 0x7fffffff) return (int)hipErrorInvalidValue;
-#define SKV_LAUNCH(NKT)                                                                                            \
-  attn_fwd_d64_shortkv_kernel<NKT><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                                     \
-      (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, \
-      osb, oss, osh, sl2, nqb3)
+#define SKV_LAUNCH(NKT)                                                                                              \
+  do {                                                                                                              \
+    if (g_attn_prio)                                                                                                \
+      attn_fwd_d64_shortkv_kernel<NKT><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                                   \
+          (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss,   \
+          vsh, osb, oss, osh, sl2, nqb3);                                                                           \
+    else                                                                                                            \
+      attn_fwd_d64_shortkv_kernel<NKT, false><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                            \
+          (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss,   \
+          vsh, osb, oss, osh, sl2, nqb3);                                                                           \
+  } while (0)
     if (Sk <= 32) SKV_LAUNCH(1);
     else if (Sk <= 64) SKV_LAUNCH(2);
     else if (Sk <= 96) SKV_LAUNCH(3);
