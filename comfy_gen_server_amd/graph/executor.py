@@ -194,7 +194,10 @@ class PromptExecutor:
                 if r[0] is not True:
                     return r
         input_data_all = None
+        hook = self.node_hook
         try:
+            if hook is not None:
+                hook.node_begin()
             input_data_all = get_input_data(inputs, class_def, unique_id, self.outputs, prompt, extra_data)
             if self.server.client_id is not None:
                 self.server.last_node_id = unique_id
@@ -204,16 +207,13 @@ class PromptExecutor:
                 obj = class_def()
                 self.object_storage[(unique_id, class_type)] = obj
             t0 = time.perf_counter()
-            hook = self.node_hook
-            run_inputs = input_data_all if hook is None else hook.before(class_type, class_def, input_data_all)
             with telemetry.span(f"node:{class_type}:{unique_id}"):
                 telemetry.maybe_fault("node", class_type)
-                if run_inputs is None:          # SPMD: output node, runs on rank 0 only
-                    output_data, output_ui = [], {}
-                else:
-                    output_data, output_ui = get_output_data(obj, run_inputs)
-                    if hook is not None:
-                        output_data = hook.after(class_type, run_inputs, output_data)
+                if hook is None:
+                    output_data, output_ui = get_output_data(obj, input_data_all)
+                else:   # SPMD (sched/spmd.py): agreement points, unsharding, rank-0 output nodes
+                    output_data, output_ui = hook.execute(class_type, class_def, obj, input_data_all,
+                                                          get_output_data)
             dt = time.perf_counter() - t0
             self.node_timings[unique_id] = (class_type, dt)
             telemetry.record_node(class_type, dt)
@@ -233,9 +233,13 @@ class PromptExecutor:
                     self.server.send_sync("executed", {"node": unique_id, "output": output_ui, "prompt_id": prompt_id},
                                           self.server.client_id)
         except dm.InterruptProcessingException as iex:
+            if hook is not None:
+                hook.abort()
             logging.info("Processing interrupted")
             return False, {"node_id": unique_id}, iex
         except Exception as ex:
+            if hook is not None:
+                hook.abort()    # the peers are at this node's pending agreement point
             typ, _, tb = sys.exc_info()
             inputs_fmt = {}
             if input_data_all is not None:

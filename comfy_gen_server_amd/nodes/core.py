@@ -678,6 +678,7 @@ def common_ksampler(model, seed, steps, cfg, sampler_name, scheduler, positive, 
     the one-GPU batch."""
     from ..sched import spmd
     local, batch_inds, shard = spmd.shard_latent(latent)
+    positive, negative = spmd.shard_conds(positive, shard), spmd.shard_conds(negative, shard)
     model = spmd.latency_model(model)
     latent_image = local["samples"]
     if disable_noise:

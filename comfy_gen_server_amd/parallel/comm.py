@@ -31,6 +31,7 @@ class Comm:
         self.backend = None
         self.device = torch.device("cpu")
         self.ctrl = None      # Gloo group for host-side control traffic (None: the default group)
+        self.bytes_moved = 0  # tensor bytes this rank sent + received in gathers (serving metrics)
 
     degraded = False   # set by the DP engine after a rank failure: the process group is unusable
 
@@ -105,6 +106,7 @@ class Comm:
         t = t.contiguous()
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t)
+        self.bytes_moved += out.numel() * out.element_size()      # own shard out, every other shard in
         return out
 
     def gather(self, t, dst=0):
@@ -114,11 +116,14 @@ class Comm:
         if not self.enabled:
             return t
         t = t.contiguous()
+        nb = t.numel() * t.element_size()
         if self.rank == dst:
             parts = [torch.empty_like(t) for _ in range(self.world)]
             dist.gather(t, gather_list=parts, dst=dst)
+            self.bytes_moved += (self.world - 1) * nb
             return torch.cat(parts)
         dist.gather(t, dst=dst)
+        self.bytes_moved += nb
         return None
 
     def all_reduce_max(self, x: float) -> float:

@@ -347,7 +347,7 @@ def processing_interrupted():
 def throw_exception_if_processing_interrupted():
     global interrupt_processing
     from ..sched import spmd
-    if spmd.active() is not None:      # SPMD prompts stop only where every rank agrees (spmd.SPMD.before)
+    if spmd.active() is not None:      # SPMD prompts stop only where every rank agrees (spmd.SPMD.execute)
         return
     with interrupt_processing_mutex:
         if interrupt_processing:

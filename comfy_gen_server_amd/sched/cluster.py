@@ -36,6 +36,17 @@ import time
 from multiprocessing.connection import Client, Listener
 
 SAMPLER_TYPES = ("KSampler", "KSamplerAdvanced")
+GC_INTERVAL_S = 10.0          # the reference worker's model cleanup + GC cadence (main.py:139-146)
+MAX_RETRIES = 1               # re-runs of a prompt whose rank died under it
+
+
+def _housekeeping():
+    """Between prompts on every rank: drop models nobody holds, collect, return cached HBM."""
+    import gc
+    from ..runtime import device as dm
+    dm.cleanup_models()
+    gc.collect()
+    dm.soft_empty_cache()
 
 
 def _default(o):
@@ -62,16 +73,42 @@ def recv_msg(conn):
 
 
 def prompt_batch(prompt: dict) -> int:
-    """Largest image batch a prompt creates (latent constructors / repeats feeding its samplers)."""
+    """Image batch at the samplers' latent inputs, traced upstream through the graph: latent / image
+    constructors (``batch_size``), repeats (``amount`` x upstream), batch concatenations (sum of both
+    inputs), batch slices (``length``), and for every other node (VAEEncode / inpaint encoders, upscales,
+    masks, ...) the largest batch among its linked inputs. A node this cannot see through counts as 1:
+    an under-estimate only costs parallelism (the prompt runs on one rank), never correctness."""
+    memo: dict = {}
+
+    def batch_of(nid, depth=0):
+        if nid in memo:
+            return memo[nid]
+        node = prompt.get(nid)
+        if not isinstance(node, dict) or depth > 64:
+            return 1
+        memo[nid] = 1       # cycle guard
+        ct, inputs = node.get("class_type", ""), node.get("inputs", {})
+        links = {k: v[0] for k, v in inputs.items() if isinstance(v, list) and len(v) == 2}
+        up = [batch_of(v, depth + 1) for v in links.values()]
+        if isinstance(inputs.get("batch_size"), int):
+            b = inputs["batch_size"]
+        elif ct.startswith("Repeat") and isinstance(inputs.get("amount"), int):
+            b = inputs["amount"] * max(up, default=1)
+        elif ct.endswith("FromBatch") and isinstance(inputs.get("length"), int):
+            b = inputs["length"]
+        elif ct in ("LatentBatch", "ImageBatch"):
+            b = sum(up) if up else 1
+        else:
+            b = max(up, default=1)
+        memo[nid] = max(1, b)
+        return memo[nid]
+
     best = 1
     for node in prompt.values():
-        if not isinstance(node, dict):
-            continue
-        inputs = node.get("inputs", {})
-        for key in ("batch_size", "amount"):
-            v = inputs.get(key)
-            if isinstance(v, int) and node.get("class_type", "").endswith(("LatentImage", "LatentBatch", "Latent")):
-                best = max(best, v)
+        if isinstance(node, dict) and node.get("class_type") in SAMPLER_TYPES:
+            src = node.get("inputs", {}).get("latent_image")
+            if isinstance(src, list) and len(src) == 2:
+                best = max(best, batch_of(src[0]))
     return best
 
 
@@ -167,16 +204,31 @@ def worker_main(comm, address, authkey: bytes):
             else:
                 inbox.put(m)
     threading.Thread(target=reader, daemon=True).start()
+    last_gc, need_gc = time.perf_counter(), False
     while True:
-        m = inbox.get()
-        if m.get("op") == "stop":
+        try:
+            m = inbox.get(timeout=1.0)
+        except queue.Empty:
+            m = {"op": "idle"}
+        op = m.get("op")
+        if op == "stop":
             break
-        if m.get("op") != "run":
+        if op == "free":              # POST /free forwarded by rank 0 (same order as the prompts)
+            if m.get("unload_models") or m.get("free_memory"):
+                dm.unload_all_models()
+            if m.get("free_memory"):
+                ex_single.reset()
+                ex_spmd.reset()
+            need_gc, last_gc = True, 0.0
+        if op != "run":
+            if need_gc and time.perf_counter() - last_gc > GC_INTERVAL_S:
+                _housekeeping()
+                last_gc, need_gc = time.perf_counter(), False
             continue
         pid, extra = m["prompt_id"], m.get("extra_data") or {}
         server.last_prompt_id = pid
         t0 = time.perf_counter()
-        n0 = ctx.images_sampled
+        n0, b0 = ctx.images_sampled, comm.bytes_moved
         if m["mode"] in ("spmd", "latency"):
             with spmd.activate(ctx, m["mode"]):
                 ex_spmd.execute(m["prompt"], pid, {}, m["outputs"])
@@ -184,9 +236,11 @@ def worker_main(comm, address, authkey: bytes):
         else:
             ex_single.execute(m["prompt"], pid, extra, m["outputs"])
             ex = ex_single
+        need_gc = True
         send_msg(conn, {"op": "done", "prompt_id": pid, "rank": comm.rank, "success": ex.success,
                         "messages": ex.status_messages, "outputs_ui": ex.outputs_ui,
-                        "seconds": time.perf_counter() - t0, "images_sampled": ctx.images_sampled - n0}, lock)
+                        "seconds": time.perf_counter() - t0, "images_sampled": ctx.images_sampled - n0,
+                        "comm_bytes": comm.bytes_moved - b0}, lock)
     try:
         conn.close()
     except OSError:
@@ -210,8 +264,10 @@ class Coordinator:
         self.cv = threading.Condition()
         self.spmd_waiting: dict = {}  # prompt_id -> {rank: done message}
         self.ran_on: dict = {}        # prompt_id -> rank(s), for /history metrics and tests
-        self._inflight: dict = {}     # rank -> (queue item id, prompt id) of its single prompt
+        self._inflight: dict = {}     # rank -> (queue item id, prompt id, prompt, extra, outputs): its single prompt
         self._sids: dict = {}         # prompt id -> submitting client (WS)
+        self._retries: dict = {}      # prompt id -> re-runs after a rank death
+        self._last_gc, self._need_gc = time.perf_counter(), False
 
         def accept_all():
             while len(self.conns) < self.world - 1:
@@ -257,17 +313,33 @@ class Coordinator:
                     self.cv.notify_all()
 
     def _rank_died(self, r):
+        """A worker's connection dropped: mark it dead (no SPMD from now on: the process group lost a
+        member), re-run its single prompt on a survivor (once), unblock a waiting SPMD prompt."""
         logging.error("rank %d left the cluster", r)
+        retry = None
         with self.cv:
             self.dead.add(r)
+            try:    # SPMD agreements waiting on the dead rank fail within ~1 s (spmd.SPMD._agree)
+                st = self.comm.store()
+                if st is not None:
+                    st.set("cgs/dead", ",".join(str(x) for x in sorted(self.dead)))
+            except Exception:   # pragma: no cover - store already gone
+                pass
             pid = self.busy.pop(r, None)
             rec = self._inflight.pop(r, None)
             if rec is not None:
-                self._complete(rec[0], rec[1], {}, False,
-                               [("execution_error", {"prompt_id": pid, "exception_message": f"rank {r} died"})])
+                if self._retries.get(rec[1], 0) < MAX_RETRIES and self.live():
+                    self._retries[rec[1]] = self._retries.get(rec[1], 0) + 1
+                    retry = rec
+                else:
+                    self._complete(rec[0], rec[1], {}, False,
+                                   [("execution_error", {"prompt_id": pid, "exception_message": f"rank {r} died"})])
             for w in self.spmd_waiting.values():
-                w.setdefault(r, {"success": False, "messages": [], "outputs_ui": {}})
+                w.setdefault(r, {"success": False, "messages": [], "outputs_ui": {}, "dead": True})
             self.cv.notify_all()
+        if retry is not None:
+            logging.warning("re-running prompt %s (rank %d died under it)", retry[1], r)
+            threading.Thread(target=self._run_single, args=retry, daemon=True).start()
 
     def interrupt_all(self):
         for r in list(self.busy):
@@ -297,27 +369,54 @@ class Coordinator:
     def _finish_single(self, r, m):
         rec = self._inflight.pop(r, None)
         self.busy.pop(r, None)
+        self._need_gc = True
         if rec is None:
             return
-        item_id, pid = rec
+        item_id, pid = rec[0], rec[1]
         self._complete(item_id, pid, m.get("outputs_ui") or {}, bool(m.get("success")), m.get("messages") or [])
 
     # -------------------------------------------------------------- scheduling
     def run_forever(self, stop_event: threading.Event | None = None):
         while stop_event is None or not stop_event.is_set():
             got = self.q.get(timeout=1.0)
-            if got is None:
-                continue
-            item, item_id = got
-            prompt_id, prompt, extra, outputs = item[1], item[2], item[3] or {}, item[4]
-            sid = extra.get("client_id")
-            if sid is not None:
-                self._sids[prompt_id] = sid
-            mode = choose_mode(prompt, extra, len(self.live()), self.latency_default)
-            if mode in ("spmd", "latency") and len(self.live()) == self.world:
-                self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode)
-            else:
-                self._run_single(item_id, prompt_id, prompt, extra, outputs)
+            if got is not None:
+                item, item_id = got
+                prompt_id, prompt, extra, outputs = item[1], item[2], item[3] or {}, item[4]
+                sid = extra.get("client_id")
+                if sid is not None:
+                    self._sids[prompt_id] = sid
+                mode = choose_mode(prompt, extra, len(self.live()), self.latency_default)
+                if mode in ("spmd", "latency") and len(self.live()) == self.world:
+                    self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode)
+                else:
+                    self._run_single(item_id, prompt_id, prompt, extra, outputs)
+            self._housekeeping()
+
+    def _housekeeping(self):
+        """The reference worker's between-prompt duties (main.py:139-146) for the whole node: POST /free
+        flags (applied on rank 0 once it is idle, forwarded to every worker in prompt order) and the
+        periodic model cleanup + GC."""
+        from ..runtime import device as dm
+        flags = self.q.get_flags()
+        free_memory = flags.get("free_memory", False)
+        unload = flags.get("unload_models", free_memory)
+        if unload or free_memory:
+            self._wait(lambda: 0 not in self.busy)
+            dm.unload_all_models()
+            if free_memory:
+                self.ex_single.reset()
+                self.ex_spmd.reset()
+            for r in self.live():
+                if r != 0:
+                    try:
+                        send_msg(self.conns[r], {"op": "free", "unload_models": bool(unload),
+                                                 "free_memory": bool(free_memory)}, self.locks[r])
+                    except OSError:
+                        self._rank_died(r)
+            self._need_gc, self._last_gc = True, 0.0
+        if self._need_gc and 0 not in self.busy and time.perf_counter() - self._last_gc > GC_INTERVAL_S:
+            _housekeeping()
+            self._last_gc, self._need_gc = time.perf_counter(), False
 
     def _wait(self, pred):
         with self.cv:
@@ -330,7 +429,7 @@ class Coordinator:
             idle = [r for r in self.live() if r not in self.busy]
             r = max(idle)             # workers first: rank 0 also serves HTTP / WS
             self.busy[r] = prompt_id
-            self._inflight[r] = (item_id, prompt_id)
+            self._inflight[r] = (item_id, prompt_id, prompt, extra, outputs)
             self.ran_on[prompt_id] = r
         if r == 0:
             threading.Thread(target=self._local_single, args=(prompt_id, prompt, extra, outputs), daemon=True).start()
@@ -343,11 +442,20 @@ class Coordinator:
 
     def _local_single(self, prompt_id, prompt, extra, outputs):
         self.server.last_prompt_id = prompt_id
-        self.ex_single.execute(prompt, prompt_id, extra, outputs)
-        with self.cv:
-            self._finish_single(0, {"success": self.ex_single.success, "messages": self.ex_single.status_messages,
-                                    "outputs_ui": self.ex_single.outputs_ui})
-            self.cv.notify_all()
+        msg = {"success": False, "messages": [("execution_error", {"prompt_id": prompt_id,
+                                                                   "exception_message": "executor raised"})],
+               "outputs_ui": {}}
+        try:
+            self.ex_single.execute(prompt, prompt_id, extra, outputs)
+            msg = {"success": self.ex_single.success, "messages": self.ex_single.status_messages,
+                   "outputs_ui": self.ex_single.outputs_ui}
+        except Exception as ex:     # the executor handles node errors itself: this is a bug, not a node error
+            logging.exception("rank 0 executor raised")
+            msg["messages"][0][1]["exception_message"] = str(ex)
+        finally:
+            with self.cv:
+                self._finish_single(0, msg)
+                self.cv.notify_all()
 
     def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd"):
         from . import spmd
@@ -362,12 +470,13 @@ class Coordinator:
             if r != 0:
                 send_msg(self.conns[r], msg, self.locks[r])
         self.server.last_prompt_id = prompt_id
-        n0 = self.ctx.images_sampled
+        n0, b0 = self.ctx.images_sampled, self.comm.bytes_moved
         with spmd.activate(self.ctx, mode):
             self.ex_spmd.execute(prompt, prompt_id, extra, outputs)
-        mine = self.ctx.images_sampled - n0
+        mine, mine_b = self.ctx.images_sampled - n0, self.comm.bytes_moved - b0
         self._wait(lambda: all(r in self.spmd_waiting[prompt_id] for r in self.live() if r != 0)
                    or len(self.live()) < self.world)
+        retry = False
         with self.cv:
             done = self.spmd_waiting.pop(prompt_id)
             ok = self.ex_spmd.success and all(bool(m.get("success")) for m in done.values())
@@ -378,13 +487,26 @@ class Coordinator:
             for r in list(self.busy):
                 if self.busy[r] == prompt_id:
                     del self.busy[r]
-            self._complete(item_id, prompt_id, self.ex_spmd.outputs_ui, ok, msgs)
+            self._need_gc = True
+            # a rank died under the prompt: run it again whole on a survivor (noise is keyed by global
+            # image index, so the images are the ones the split run would have produced)
+            lost = any(m.get("dead") for m in done.values()) or len(self.live()) < self.world
+            if not ok and lost and self.live() and self._retries.get(prompt_id, 0) < MAX_RETRIES:
+                self._retries[prompt_id] = self._retries.get(prompt_id, 0) + 1
+                retry = True
+            else:
+                self._complete(item_id, prompt_id, self.ex_spmd.outputs_ui, ok, msgs)
             with self.q.mutex:
                 h = self.q.history.get(prompt_id)
                 if h is not None:   # images sampled per rank (the batch split)
                     h["metrics"]["images_per_rank"] = {0: mine, **{r: m.get("images_sampled", 0)
                                                                    for r, m in done.items()}}
+                    h["metrics"]["comm_bytes_per_rank"] = {0: mine_b, **{r: m.get("comm_bytes", 0)
+                                                                         for r, m in done.items()}}
             self.cv.notify_all()
+        if retry:
+            logging.warning("re-running prompt %s on a surviving rank", prompt_id)
+            self._run_single(item_id, prompt_id, prompt, extra, outputs)
 
     def shutdown(self):
         for r, conn in self.conns.items():

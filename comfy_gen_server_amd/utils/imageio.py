@@ -56,27 +56,37 @@ def _claim(folder, filename, counter):
             counter += 1
 
 
-def save_png_batch(images, folder, filename, counter, metadata=None, compress_level=4):
-    arrs = to_uint8_cpu(images)
+def reserve_png_names(folder, filename, counter, count):
+    """Claim ``count`` consecutive free ``{filename}_{counter:05}_.png`` names (empty files)."""
+    os.makedirs(folder, exist_ok=True)
     names = []
-    jobs = []
-    for i, arr in enumerate(arrs):
+    for _ in range(count):
         name, counter = _claim(folder, filename, counter)
         counter += 1
         names.append(name)
-        path = os.path.join(folder, name)
+    return names
 
-        def work(a=arr, p=path):
-            img = Image.fromarray(a)
-            info = None
-            if metadata:
-                info = PngInfo()
-                for k, v in metadata.items():
-                    info.add_text(k, v)
-            img.save(p, pnginfo=info, compress_level=compress_level)
-        jobs.append(_pool().submit(work))
+
+def write_png_files(images, paths, metadata=None, compress_level=4):
+    """Encode ``images`` (B, H, W, C float in [0, 1]) to ``paths`` on the thread pool."""
+    arrs = to_uint8_cpu(images)
+
+    def work(a, p):
+        img = Image.fromarray(a)
+        info = None
+        if metadata:
+            info = PngInfo()
+            for k, v in metadata.items():
+                info.add_text(k, v)
+        img.save(p, pnginfo=info, compress_level=compress_level)
+    jobs = [_pool().submit(work, a, p) for a, p in zip(arrs, paths)]
     for j in jobs:
         j.result()
+
+
+def save_png_batch(images, folder, filename, counter, metadata=None, compress_level=4):
+    names = reserve_png_names(folder, filename, counter, images.shape[0])
+    write_png_files(images, [os.path.join(folder, n) for n in names], metadata, compress_level)
     return names
 
 

@@ -10,8 +10,10 @@
   HBM allocated / reserved; exported through ``/metrics`` (Prometheus text) and ``/system_stats``.
 * **Fault injection.** ``CGS_FAULT`` = comma list of ``node:<ClassType>`` (raise inside that
   node), ``oom:<ClassType>`` (raise an out-of-memory error there), ``step:<n>`` (raise at sampler
-  step n), ``rank_exit:<rank>`` (that DP rank exits at its next heartbeat). Each entry fires once
-  per process unless suffixed ``!`` (always). Used by the failure-handling tests.
+  step n), ``rank_exit:<rank>`` (that DP rank exits at its next heartbeat), ``node_exit:<ClassType>``
+  (the process dies inside that node). ``<key>@<rank>`` limits an entry to one rank of a multi-rank
+  job (``RANK``). Each entry fires once per process unless suffixed ``!`` (always). Used by the
+  failure-handling tests.
 """
 from __future__ import annotations
 
@@ -210,8 +212,15 @@ def maybe_fault(site: str, key: str):
     if "CGS_FAULT" not in os.environ:
         return
     for kind, arg, always, item in _faults():
+        if "@" in arg:   # "<key>@<rank>": only on that rank of a multi-rank job (RANK env)
+            arg, _, on_rank = arg.partition("@")
+            if os.environ.get("RANK", "0") != on_rank:
+                continue
         if arg != key:
             continue
+        if site == "node" and kind == "node_exit":     # the process dies inside the node (lost rank)
+            logging.error("injected process exit in node %s", key)
+            os._exit(17)
         if not always and item in _fired:
             continue
         if site == "node" and kind == "node":

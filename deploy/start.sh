@@ -2,9 +2,13 @@
 # Container entry point (parity: reference build_files/start.sh:88-126).
 #   MODEL_CACHE=tmpfs  copy $MODEL_SRC into /dev/shm (fast cold start; 288 GB HBM holds the stacks)
 #   MODEL_CACHE=nfs    use $MODEL_SRC in place through an extra_model_paths.yaml
-#   GPUS=N             number of GPU workers (default: all visible), one server per GPU on 8188+i,
-#                      nginx on :3001 spreads clients over them (WS upgrade, sticky per client IP)
-#   GRPC=1             also serve comfy_request.v1 over gRPC on 50051+i
+#   GPUS=N             GPUs to serve (default: all visible)
+#   SERVE=node         (default) ONE API for the whole node: `main.py --gpus $GPUS` -- rank 0 serves HTTP/WS
+#                      on 8188 and coordinates, a prompt's image batch is split over all GPUs, independent
+#                      prompts run concurrently on idle GPUs (sched/cluster.py)
+#   SERVE=per-gpu      one independent server per GPU on 8188+i, nginx spreads clients (sticky per IP)
+#   LATENCY=1          (node mode) batch-1 prompts split CFG / token parallel over the GPUs
+#   GRPC=1             also serve comfy_request.v1 over gRPC (50051, or 50051+i per GPU)
 set -euo pipefail
 cd /gen-server
 MODEL_SRC=${MODEL_SRC:-/runpod-volume/models}
@@ -37,13 +41,22 @@ else
 fi
 
 upstreams=""
-for ((i = 0; i < GPUS; i++)); do
-  port=$((8188 + i))
+if [ "${SERVE:-node}" = "node" ]; then
   grpc=""
-  if [ "${GRPC:-0}" = "1" ]; then grpc="--grpc-port $((50051 + i))"; fi
-  HIP_VISIBLE_DEVICES=$i python main.py --listen 0.0.0.0 --port "$port" --disable-metadata $EXTRA $grpc &
-  upstreams="$upstreams    server 127.0.0.1:$port;\n"
-done
+  if [ "${GRPC:-0}" = "1" ]; then grpc="--grpc-port 50051"; fi
+  lat=""
+  if [ "${LATENCY:-0}" = "1" ]; then lat="--latency-mode"; fi
+  MASTER_ADDR=127.0.0.1 python main.py --listen 0.0.0.0 --port 8188 --gpus "$GPUS" --disable-metadata $EXTRA $grpc $lat &
+  upstreams="    server 127.0.0.1:8188;\n"
+else
+  for ((i = 0; i < GPUS; i++)); do
+    port=$((8188 + i))
+    grpc=""
+    if [ "${GRPC:-0}" = "1" ]; then grpc="--grpc-port $((50051 + i))"; fi
+    HIP_VISIBLE_DEVICES=$i python main.py --listen 0.0.0.0 --port "$port" --disable-metadata $EXTRA $grpc &
+    upstreams="$upstreams    server 127.0.0.1:$port;\n"
+  done
+fi
 sed -i "s|# UPSTREAMS|$upstreams|" /etc/nginx/nginx.conf
 nginx
 wait -n

@@ -135,6 +135,12 @@ def test_batch_prompt_split_over_ranks_matches_one_rank(cluster):
     assert h[b]["status"]["status_str"] == "success", h[b]["status"]
     assert h[a]["metrics"]["ranks"] == "all" and isinstance(h[b]["metrics"]["ranks"], int)
     assert h[a]["metrics"]["images_per_rank"] == {"0": 2, "1": 2, "2": 2}, h[a]["metrics"]
+    # SaveImage of the sharded batch: every rank writes its own PNGs (rank 0 only names them), so a
+    # worker moves at most its own third of the images' bytes -- no all-gather of fp32 IMAGEs
+    img_bytes = 6 * 64 * 64 * 3 * 4
+    for r, nb in h[a]["metrics"]["comm_bytes_per_rank"].items():
+        if r != "0":
+            assert nb <= (1 / 3 + 0.05) * img_bytes, (r, nb)
     ia, ib = _images(base, h[a]), _images(base, h[b])
     assert len(ia) == len(ib) == 6
     for x, y in zip(ia, ib):
