@@ -100,8 +100,32 @@ def get_free_memory(dev=None, torch_free_too=False):
     reserved = st.get("reserved_bytes.all.current", 0)
     active = st.get("active_bytes.all.current", 0)
     f_torch = reserved - active
-    total_free = free + f_torch
+    # the weight arena's slab is one "active" allocation to torch; its unused part is free for weights
+    total_free = free + f_torch + _arena_free(dev)
     return (total_free, f_torch) if torch_free_too else total_free
+
+
+def _arena_free(dev) -> int:
+    from . import arena
+    a = arena._ARENAS.get(dev.index if dev.index is not None else torch.cuda.current_device())
+    if a is None:
+        return 0
+    s = a.stats()
+    return int(s["capacity"] - s["used"])
+
+
+def _hbm_bytes(m) -> int:
+    """HBM a resident model holds outside the weight arena (arena blocks are inside the slab, which
+    _evict_for charges once, whole)."""
+    from . import arena
+    if not arena._ARENAS:
+        return m.size()
+    owners = list(arena._ARENAS.values())
+    n = 0
+    for t in list(m.model.model.parameters()) + list(m.model.model.buffers()):
+        if not any(a.owns(t) for a in owners):
+            n += t.numel() * t.element_size()
+    return n
 
 
 def hbm_budget(dev=None) -> int:
@@ -252,17 +276,22 @@ current_loaded_models: list[LoadedModel] = []
 def _evict_for(need: int, device, keep):
     if device.type != "cuda":
         return
+    from . import arena
     budget = hbm_budget(device)
-    used = sum(m.size() for m in current_loaded_models if m.device == device)
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    slab = arena._ARENAS[key].slab.numel() if key in arena._ARENAS else 0
+    # the slab counts once, whole; arena-resident weights live inside it (not charged twice)
+    used = slab + sum(_hbm_bytes(m) for m in current_loaded_models if m.device == device)
     if used + need <= budget:
         return
     cands = sorted([m for m in current_loaded_models if m.device == device and m not in keep and not m.pinned],
                    key=lambda m: m.last_used)
     for m in cands:
         logging.info("evicting %s to make room", m.model.model.__class__.__name__)
+        freed = _hbm_bytes(m)
         m.model.unpatch_model(m.model.offload_device)
         current_loaded_models.remove(m)
-        used -= m.size()
+        used -= freed
         if used + need <= budget:
             break
     soft_empty_cache(True)
@@ -288,6 +317,8 @@ def load_models_gpu(models, memory_required=0, force_patch_weights=False):
                     other.model.unpatch_model(other.device)
                     current_loaded_models.remove(other)
             need = 0 if p.is_resident_on(lm.device) else p.model_size()
+            if need and lm.device.type == "cuda":    # what the arena's free space will take is already paid
+                need = max(0, need - _arena_free(lm.device))
             _evict_for(need + memory_required, lm.device, keep)
             p.patch_model(lm.device)
             current_loaded_models.insert(0, lm)
