@@ -125,6 +125,23 @@ class Gligen(nn.Module):
         return func
 
     def set_position(self, latent_image_shape, position_params, device):
+        """Memoised per (shape, boxes, phrase embeddings, device): the host-built box / mask tensors and
+        the position-net output are made once (eagerly), so a captured sampler step (run_graph.py) reads
+        device tensors only -- no host-to-device copy inside the capture."""
+        key = (tuple(latent_image_shape), str(device),
+               tuple((id(p[0]),) + tuple(float(v) for v in p[1:]) for p in position_params))
+        cache = self.__dict__.setdefault("_pos_cache", {})
+        hit = cache.get(key)
+        if hit is not None:
+            return hit[1]
+        func = self._build_position(latent_image_shape, position_params, device)
+        if len(cache) >= 16:
+            cache.pop(next(iter(cache)))
+        # the entry holds the embeddings: their ids in the key cannot be reused while it lives
+        cache[key] = ([p[0] for p in position_params], func)
+        return func
+
+    def _build_position(self, latent_image_shape, position_params, device):
         batch, _, h, w = latent_image_shape
         masks = torch.zeros([self.max_objs])
         boxes, embs = [], []

@@ -18,6 +18,9 @@ the seed and first index from a device tensor while the run is captured (``ops.r
 replay with another seed produces that seed's noise. The graphs then replay back to back; after graph
 i the progress callback of the eager loop runs with that step's x / denoised (previews included).
 
+ControlNet chains (any sampler) run inside the captured steps with their original hints as static inputs;
+GLIGEN position conditioning is part of the plan key (its per-box tensors are memoised on the eager run).
+
 Plan life cycle: the first run of a key is eager (autotune, lazy layouts), the second captures then
 replays, later runs replay. A capture that hits a host sync or an unsupported op marks the key failed
 (eager from then on; ``stats["ineligible"]`` counts every reason). ``CGS_RUN_GRAPHS=0`` disables.
@@ -79,6 +82,40 @@ def _walk(obj, tensors, sig, depth=0):
         raise TypeError(f"unsupported cond value {type(obj).__name__}")
 
 
+def _control_chain(c):
+    out = []
+    while c is not None:
+        out.append(c)
+        c = c.previous_controlnet
+    return out
+
+
+def _control_inputs(ctrl, tensors, sig):
+    """A ControlNet chain inside a captured run: each net's ORIGINAL hint is a static input (the
+    resize / cast / batch broadcast that get_control() does on first use is captured with the step it
+    first runs in, reading that static tensor, so every replay rebuilds the hint of its own job); the
+    net, its weights, strength, window and pooling are part of the plan key (the window gates per
+    step on host sigmas, which the key already fixes)."""
+    from ..models import layers
+    from ..runtime.controlnet import ControlNet
+    for cn in _control_chain(ctrl):
+        if type(cn) is not ControlNet or not torch.is_tensor(cn.cond_hint_original):
+            raise TypeError(f"control {type(cn).__name__} (only plain ControlNet chains are captured)")
+        if cn.cond_hint is not None:   # a cached hint from an earlier run would be read, not rebuilt
+            raise TypeError("controlnet hint already prepared")
+        sig.append(("CN", id(cn.control_model), layers.module_epoch(cn.control_model), float(cn.strength),
+                    tuple(cn.timestep_percent_range), bool(cn.global_average_pooling), cn.upscale_algorithm,
+                    cn.compression_ratio))
+        _walk(cn.cond_hint_original, tensors, sig)
+
+
+def _gligen_key(g, sig):
+    """GLIGEN position conditioning: the model and its boxes / phrase embeddings are part of the plan key
+    (Gligen.set_position memoises its device tensors per key, built on the eager first run)."""
+    kind, model, params = g[0], g[1], (g[2] if len(g) > 2 else [])
+    sig.append(("G", kind, id(model), tuple((id(p[0]),) + tuple(float(v) for v in p[1:]) for p in params)))
+
+
 def _static_inputs(guider, mk, x, extra_args):
     tensors, sig = [], []
     _walk(x, tensors, sig)
@@ -89,8 +126,14 @@ def _static_inputs(guider, mk, x, extra_args):
     for name, cl in (guider.conds or {}).items():
         if cl is None:
             continue
-        conds[name] = [{k: v for k, v in c.items() if k not in ("control",)} for c in cl]
+        conds[name] = [{k: v for k, v in c.items() if k not in ("control", "gligen")} for c in cl]
     _walk(conds, tensors, sig)
+    for name in sorted(guider.conds or {}, key=str):
+        for c in guider.conds[name] or []:
+            if c.get("control") is not None:
+                _control_inputs(c["control"], tensors, sig)
+            if c.get("gligen") is not None:
+                _gligen_key(c["gligen"], sig)
     return tensors, tuple(sig)
 
 
@@ -160,12 +203,6 @@ def try_run(ksampler, guider, mk, x, sigmas, extra_args, callback):
     index0, contiguous = rng.contiguous_inds(inds)
     if not contiguous or len(inds) != x.shape[0]:
         return _ineligible("non-contiguous noise indices")
-    for cl in (guider.conds or {}).values():
-        for c in cl or []:
-            if c.get("control") is not None:
-                return _ineligible("controlnet outside the fused Euler-family graph")
-            if c.get("gligen") is not None:
-                return _ineligible("gligen")
     try:
         tensors, sig = _static_inputs(guider, mk, x, extra_args)
     except TypeError as e:
@@ -202,7 +239,8 @@ def try_run(ksampler, guider, mk, x, sigmas, extra_args, callback):
                 dst.copy_(src)
     plan.key_t.copy_(torch.tensor([int(seed) & 0x7FFFFFFFFFFFFFFF, index0], dtype=torch.int64))
     for g, rec in zip(plan.graphs, plan.records + [None]):
-        g.replay()
+        if g is not None:             # None: a segment that captured no work (nothing to replay)
+            g.replay()
         stats["replay_steps"] += 1
         if rec is not None and callback is not None:
             callback(dict(rec))
@@ -234,9 +272,21 @@ def _capture(ksampler, mk, x, sigmas, extra_args, tensors, seed, index0):
     torch.cuda.synchronize()
     cur = [torch.cuda.CUDAGraph()]
 
+    def end_segment():
+        """capture_end; a segment that recorded no kernels (e.g. after the last progress callback of a
+        sampler whose final update ran before it) is kept as None and skipped on replay."""
+        import warnings
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            cur[0].capture_end()
+        if any("empty" in str(x.message).lower() for x in w):
+            stats["empty_segments"] = stats.get("empty_segments", 0) + 1
+            _graveyard.append(cur[0])
+            return None
+        return cur[0]
+
     def cut(d):                       # the sampler's per-step callback: end this step's graph
-        cur[0].capture_end()
-        p.graphs.append(cur[0])
+        p.graphs.append(end_segment())
         p.records.append({k: v for k, v in d.items()})
         cur[0] = torch.cuda.CUDAGraph()
         cur[0].capture_begin(pool=p.pool)
@@ -249,9 +299,8 @@ def _capture(ksampler, mk, x, sigmas, extra_args, tensors, seed, index0):
             capturing = True
             out = ksampler.sampler_function(mk, x, sig_cpu, extra_args=extra_args, callback=cut, disable=True,
                                             **ksampler.extra_options)
-            cur[0].capture_end()
             capturing = False
-            p.graphs.append(cur[0])
+            p.graphs.append(end_segment())
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
     except Exception as e:

@@ -390,3 +390,138 @@ def test_run_graph_with_model_patches(cuda, monkeypatch, patch):
     for got, want in ((g6, ref6), (g5, ref5)):
         err = ((got - want).norm() / want.norm()).item()
         assert err < 1e-2, (patch, err)
+
+
+def _tiny_controlnet(cuda, seed=7):
+    import copy
+    from comfy_gen_server_amd.models.cldm import ControlNet as CN
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    from comfy_gen_server_amd.tools.synth import TINY_UNET
+    cfg = copy.deepcopy(TINY_UNET)
+    cfg.update(num_heads=2, num_head_channels=-1)
+    cm = CN(hint_channels=3, dtype=torch.bfloat16, device=cuda, **cfg)
+    init_random_fast_(cm, seed=seed)
+    return cm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampler", ["dpmpp_2m_sde", "heun"])
+def test_run_graph_with_controlnet_matches_eager(cuda, monkeypatch, sampler):
+    """ControlNet under a sampler outside the fused Euler family replays from the per-step run graphs:
+    the original hint is a static input, so three jobs with three different hints (eager, capture,
+    replay) equal the eager loop of the same hints, with a timestep window gating the net."""
+    from comfy_gen_server_amd.graph import registry
+    from comfy_gen_server_amd.parallel.dp import encode_prompt
+    from comfy_gen_server_amd.runtime import controlnet as rcn
+    from comfy_gen_server_amd.sampling import run_graph, sample as S
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    registry.init_nodes(custom_nodes=False)
+    NM = registry.NODE_CLASS_MAPPINGS
+    monkeypatch.setenv("CGS_GRAPHS", "1")
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        cm = _tiny_controlnet(cuda)
+        pos = encode_prompt(clip, "a house", 64, 64)
+        neg = encode_prompt(clip, "blurry", 64, 64)
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_RUN_GRAPHS", mode)
+            before = dict(run_graph.stats)
+            outs = []
+            for j in range(3):
+                g = torch.Generator().manual_seed(j)
+                hint = torch.rand(1, 64, 64, 3, generator=g).to(cuda)
+                cnet = rcn.ControlNet(cm, load_device=cuda)
+                pc, nc = NM["ControlNetApplyAdvanced"]().apply_controlnet(pos, neg, cnet, hint, 0.8, 0.0, 0.6)
+                latent = torch.zeros([2, 4, 8, 8])
+                noise = S.prepare_noise(latent, 5)
+                outs.append(S.sample(patcher, noise, 5, 5.0, sampler, "normal", pc, nc, latent, seed=5).float())
+            res[mode] = outs
+        torch.cuda.synchronize()
+    assert run_graph.stats["capture"] - before["capture"] == 1, run_graph.stats
+    assert run_graph.stats["replay_runs"] - before["replay_runs"] == 2, run_graph.stats
+    for a, b in zip(res["0"], res["1"]):
+        err = ((a - b).norm() / a.norm()).item()
+        assert err < 1e-2, err
+    assert ((res["1"][1] - res["1"][2]).norm() / res["1"][1].norm()).item() > 1e-3   # the hint reached the replay
+
+
+@pytest.mark.gpu
+def test_run_graph_with_gligen_matches_eager(cuda, monkeypatch):
+    """GLIGEN position conditioning (gated self-attention in every transformer block) replays from the
+    per-step run graphs: the boxes and phrase embedding are part of the plan key, the device tensors are
+    memoised on the eager run, and replay equals the eager loop."""
+    from comfy_gen_server_amd.graph import registry
+    from comfy_gen_server_amd.models.gligen import GatedSelfAttentionDense, PositionNet, gligen_from_state_dict
+    from comfy_gen_server_amd.models.layers import init_random_
+    from comfy_gen_server_amd.parallel.dp import encode_prompt
+    from comfy_gen_server_amd.runtime.patcher import ModelPatcher
+    from comfy_gen_server_amd.sampling import run_graph, sample as S
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    registry.init_nodes(custom_nodes=False)
+    NM = registry.NODE_CLASS_MAPPINGS
+    monkeypatch.setenv("CGS_GRAPHS", "1")
+    sd = {}
+    for part, b, dim in [("input_blocks", 1, 32), ("input_blocks", 3, 64), ("middle_block", 1, 64),
+                         ("output_blocks", 0, 64), ("output_blocks", 1, 64), ("output_blocks", 2, 32),
+                         ("output_blocks", 3, 32)]:
+        g = GatedSelfAttentionDense(dim, 64, 2, dim // 2)
+        init_random_(g, seed=b)
+        for k, v in g.state_dict().items():
+            sd[f"model.diffusion_model.{part}.{b}.1.transformer_blocks.0.fuser.{k}"] = v
+    pn = PositionNet(64, 64)
+    init_random_(pn, seed=9)
+    for k, v in pn.state_dict().items():
+        sd[f"position_net.{k}"] = v
+    with torch.inference_mode():
+        gl = gligen_from_state_dict(sd)
+        for m in gl.modules():           # gates open so the boxes change the image
+            for nm in ("alpha_attn", "alpha_dense"):
+                if hasattr(m, nm):
+                    getattr(m, nm).fill_(0.5)
+        gl.to(device=cuda, dtype=torch.bfloat16)
+        gp = ModelPatcher(gl, load_device=cuda, offload_device=cuda)
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        pos = encode_prompt(clip, "a park", 64, 64)
+        neg = encode_prompt(clip, "blurry", 64, 64)
+        cond = NM["GLIGENTextBoxApply"]().append(pos, clip, gp, "a dog", 32, 32, 0, 0)[0]
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CGS_RUN_GRAPHS", mode)
+            before = dict(run_graph.stats)
+            outs = []
+            for seed in (5, 6, 5):
+                latent = torch.zeros([2, 4, 8, 8])
+                noise = S.prepare_noise(latent, seed)
+                outs.append(S.sample(patcher, noise, 4, 5.0, "euler_ancestral", "normal", cond, neg, latent,
+                                     seed=seed).float())
+            res[mode] = outs
+        torch.cuda.synchronize()
+    assert run_graph.stats["capture"] - before["capture"] == 1, run_graph.stats
+    assert run_graph.stats["replay_runs"] - before["replay_runs"] == 2, run_graph.stats
+    for a, b in zip(res["0"], res["1"]):
+        err = ((a - b).norm() / a.norm()).item()
+        assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+def test_run_graph_skips_empty_segments(cuda, monkeypatch):
+    """A sampler whose last update runs before its last progress callback leaves an empty final segment:
+    it is dropped at capture (no "CUDA Graph is empty" replay) and the run still equals the eager loop."""
+    import warnings
+    from comfy_gen_server_amd.sampling import run_graph
+    from comfy_gen_server_amd.tools.synth import build_pipeline
+    monkeypatch.setenv("CGS_GRAPHS", "1")
+    with torch.inference_mode():
+        patcher, clip, vae = build_pipeline("tiny", device=cuda, dtype=torch.bfloat16, seed=2)
+        monkeypatch.setenv("CGS_RUN_GRAPHS", "0")
+        (ref,) = _run_jobs(patcher, clip, vae, "dpmpp_2m_sde", [5])
+        monkeypatch.setenv("CGS_RUN_GRAPHS", "1")
+        e0 = run_graph.stats.get("empty_segments", 0)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            _, got = _run_jobs(patcher, clip, vae, "dpmpp_2m_sde", [5, 5])
+    assert not [x for x in w if "empty" in str(x.message).lower()], [str(x.message) for x in w]
+    assert run_graph.stats.get("empty_segments", 0) > e0, run_graph.stats
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
