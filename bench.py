@@ -21,6 +21,29 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 
+_FAMILY_NAMES = {"sdxl": "SDXL-base", "sd15": "SD1.5", "sd21": "SD2.1", "cascade": "Stable Cascade", "tiny": "tiny test"}
+
+
+def _labels(args):
+    """(metric, data, model) strings for the family actually run: the BASELINE metric string names SDXL
+    1024 20-step Euler-a, so it is used only for that config; every other run names what it measured."""
+    fam = _FAMILY_NAMES.get(args.family, args.family)
+    headline = args.family == "sdxl" and args.res == 1024 and args.sampler_steps == 20 and \
+        args.sampler == "euler_ancestral"
+    metric = None
+    if headline:
+        try:
+            with open(os.path.join(HERE, "BASELINE.json")) as f:
+                metric = json.load(f)["metric"]
+        except Exception:
+            metric = None
+    if metric is None:
+        metric = f"images/sec (whole node), {fam} {args.res} {args.sampler_steps}-step {args.sampler}"
+    data = f"synthetic prompts, random-init weights (exact {fam} architecture)"
+    model = f"{args.family}-base" if args.family == "sdxl" else args.family
+    return metric, data, model
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,11 +174,7 @@ def main():
     ms_per_step = dt * 1000.0 / max(1, args.steps)
     imgs_per_sec = global_batch * args.steps / dt
     if comm.rank == 0:
-        try:
-            with open(os.path.join(HERE, "BASELINE.json")) as f:
-                metric = json.load(f)["metric"]
-        except Exception:
-            metric = "images/sec (whole node), SDXL 1024 20-step Euler-a"
+        metric, data_s, model_s = _labels(args)
         res = {
             "metric": metric,
             "value": round(imgs_per_sec, 4),
@@ -170,10 +189,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32" if args.cpu else "bf16",
-            "data": "synthetic prompts, random-init weights (exact SDXL-base architecture)",
+            "data": data_s,
             "sec_per_image": round(dt / (global_batch * args.steps), 4),
             "sec_per_image_per_gpu": round(dt * N / (global_batch * args.steps), 4),
-            "config": {"model": f"{args.family}-base" if args.family == "sdxl" else args.family,
+            "config": {"model": model_s,
                        "global_batch": global_batch, "seq_len": (args.res // 8) ** 2,
                        "resolution": args.res, "sampler_steps": args.sampler_steps, "sampler": args.sampler,
                        "cfg": args.cfg, "unet_batch_per_gpu": 2 * args.batch_per_gpu,
@@ -244,20 +263,16 @@ def _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log):
     comm.barrier()
     dt = comm.all_reduce_max(time.perf_counter() - t1)
     if comm.rank == 0:
-        try:
-            with open(os.path.join(HERE, "BASELINE.json")) as f:
-                metric = json.load(f)["metric"]
-        except Exception:
-            metric = "images/sec (whole node), SDXL 1024 20-step Euler-a"
+        metric, data_s, model_s = _labels(args)
         saved = sum(1 for f in os.listdir(out_dir) if f.endswith(".png"))
         res = {"metric": metric, "value": round(global_batch * args.steps / dt, 4), "unit": "images/s",
                "n_gpus": comm.world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(dt * 1000.0 / max(1, args.steps), 2), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if args.cpu else "bf16",
-               "data": "synthetic prompts, random-init weights (exact SDXL-base architecture)",
+               "data": data_s,
                "path": "workflow JSON -> validate_prompt -> PromptExecutor (SaveImage PNGs included)",
                "pngs_written": saved,
-               "config": {"model": f"{args.family}-base" if args.family == "sdxl" else args.family,
+               "config": {"model": model_s,
                           "global_batch": global_batch, "seq_len": (args.res // 8) ** 2, "resolution": args.res,
                           "sampler_steps": args.sampler_steps, "sampler": args.sampler, "cfg": args.cfg,
                           "parallelism": f"dp{comm.world}"},
@@ -299,12 +314,13 @@ def _bench_latency(args, comm, gen, job, t0, t_build, log):
     comm.barrier()
     dt = comm.all_reduce_max(time.perf_counter() - t1)
     if comm.rank == 0:
+        _, data_s, model_s = _labels(args)
         res = {"metric": "sec/image, one image per node (latency mode)", "value": round(dt / max(1, args.steps), 4),
                "unit": "s/image", "n_gpus": comm.world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(dt * 1000.0 / max(1, args.steps), 2), "higher_is_better": False,
                "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if args.cpu else "bf16",
-               "data": "synthetic prompts, random-init weights (exact SDXL-base architecture)",
-               "config": {"model": f"{args.family}-base" if args.family == "sdxl" else args.family, "global_batch": 1,
+               "data": data_s,
+               "config": {"model": model_s, "global_batch": 1,
                           "resolution": args.res, "sampler_steps": args.sampler_steps, "sampler": args.sampler,
                           "cfg": args.cfg, "parallelism": f"cfg{lat.G}xtoken{lat.Q}"},
                "unet_calls_on_rank0": lat.calls, "build_s": round(t_build, 1)}

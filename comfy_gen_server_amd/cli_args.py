@@ -38,6 +38,11 @@ class EnumAction(argparse.Action):
         setattr(namespace, self.dest, self._enum(values))
 
 
+# The reference's module-level mutually-exclusive groups by name (``comfy/cli_args.py``: cm_group,
+# fp_group, ...); custom nodes import them to add their own flags to the same group.
+GROUPS: dict = {}
+
+
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="comfy_gen_server_amd: MI355X-native ComfyUI-compatible generation server")
     # network
@@ -61,25 +66,25 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--latency-mode", action="store_true",
                    help="with --gpus N: prompts whose batch is smaller than N run on all ranks with every UNet "
                         "call split CFG-/token-parallel (one image sooner) instead of on one idle rank")
-    cm = p.add_mutually_exclusive_group()
+    cm = GROUPS["cm_group"] = p.add_mutually_exclusive_group()
     cm.add_argument("--cuda-malloc", action="store_true")
     cm.add_argument("--disable-cuda-malloc", action="store_true")
     p.add_argument("--dont-upcast-attention", action="store_true")
     # precision
-    fp = p.add_mutually_exclusive_group()
+    fp = GROUPS["fp_group"] = p.add_mutually_exclusive_group()
     fp.add_argument("--force-fp32", action="store_true")
     fp.add_argument("--force-fp16", action="store_true")
-    fpu = p.add_mutually_exclusive_group()
+    fpu = GROUPS["fpunet_group"] = p.add_mutually_exclusive_group()
     fpu.add_argument("--bf16-unet", action="store_true")
     fpu.add_argument("--fp16-unet", action="store_true")
     fpu.add_argument("--fp8_e4m3fn-unet", action="store_true")
     fpu.add_argument("--fp8_e5m2-unet", action="store_true")
-    fpv = p.add_mutually_exclusive_group()
+    fpv = GROUPS["fpvae_group"] = p.add_mutually_exclusive_group()
     fpv.add_argument("--fp16-vae", action="store_true")
     fpv.add_argument("--fp32-vae", action="store_true")
     fpv.add_argument("--bf16-vae", action="store_true")
     p.add_argument("--cpu-vae", action="store_true")
-    fpt = p.add_mutually_exclusive_group()
+    fpt = GROUPS["fpte_group"] = p.add_mutually_exclusive_group()
     fpt.add_argument("--fp8_e4m3fn-text-enc", action="store_true")
     fpt.add_argument("--fp8_e5m2-text-enc", action="store_true")
     fpt.add_argument("--fp16-text-enc", action="store_true")
@@ -89,13 +94,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--disable-ipex-optimize", action="store_true")
     p.add_argument("--preview-method", type=LatentPreviewMethod, default=LatentPreviewMethod.NoPreviews,
                    action=EnumAction)
-    attn = p.add_mutually_exclusive_group()
+    attn = GROUPS["attn_group"] = p.add_mutually_exclusive_group()
     attn.add_argument("--use-split-cross-attention", action="store_true")
     attn.add_argument("--use-quad-cross-attention", action="store_true")
     attn.add_argument("--use-pytorch-cross-attention", action="store_true")
     p.add_argument("--disable-xformers", action="store_true")
     # VRAM
-    vram = p.add_mutually_exclusive_group()
+    vram = GROUPS["vram_group"] = p.add_mutually_exclusive_group()
     vram.add_argument("--gpu-only", action="store_true")
     vram.add_argument("--highvram", action="store_true")
     vram.add_argument("--normalvram", action="store_true")

@@ -392,18 +392,7 @@ def _b_utils():
 
 def _b_ops():
     from .models import layers
-
-    def cast_bias_weight(s, input):
-        """(weight, bias) of layer ``s`` on ``input``'s device / dtype (``comfy/ops.py:22``)."""
-        w = s.weight.to(device=input.device, dtype=input.dtype)
-        b = None if s.bias is None else s.bias.to(device=input.device, dtype=input.dtype)
-        return w, b
-
-    class CastWeightBiasOp:
-        comfy_cast_weights = False
-        weight_function = None
-        bias_function = None
-    return {"cast_bias_weight": cast_bias_weight, "CastWeightBiasOp": CastWeightBiasOp}
+    return {"cast_bias_weight": layers.cast_bias_weight, "CastWeightBiasOp": layers.CastWeightBiasOp}
 
 
 def _b_sd():
@@ -559,10 +548,8 @@ async def _send_socket_catch_exception(function, message):
 
 def _cli_names():
     from . import cli_args
-    p = cli_args.parser if hasattr(cli_args, "parser") else None
-    groups = [g for g in getattr(p, "_mutually_exclusive_groups", [])] if p is not None else []
-    names = ["cm_group", "fp_group", "fpunet_group", "fpvae_group", "fpte_group", "attn_group", "vram_group"]
-    out = {n: (groups[i] if i < len(groups) else None) for i, n in enumerate(names)}
+    out = dict(cli_args.GROUPS)     # the reference's mutually-exclusive group names, by name
+    out["parser"] = cli_args.parser
     import logging
     out["logging_level"] = logging.DEBUG if getattr(cli_args.args, "verbose", False) else logging.INFO
     return out

@@ -62,7 +62,33 @@ def invalidate_all(module: nn.Module):
             m.invalidate_derived()
 
 
-class Linear(nn.Module, DerivedMixin):
+class CastWeightBiasOp:
+    """Per-layer weight / bias hooks (``comfy/ops.py:34``): custom nodes set ``weight_function`` /
+    ``bias_function`` on a layer to transform its parameters on every forward (on-the-fly LoRA,
+    dequantisation, ...); ``cast_bias_weight`` applies them after the device / dtype cast."""
+    comfy_cast_weights = False
+    weight_function = None
+    bias_function = None
+
+
+def cast_bias_weight(s, input):
+    """(weight, bias) of layer ``s`` cast to ``input``'s device / dtype, hooks applied (``comfy/ops.py:22``)."""
+    bias = None
+    if s.bias is not None:
+        bias = s.bias.to(device=input.device, dtype=input.dtype)
+        if s.bias_function is not None:
+            bias = s.bias_function(bias)
+    weight = s.weight.to(device=input.device, dtype=input.dtype)
+    if s.weight_function is not None:
+        weight = s.weight_function(weight)
+    return weight, bias
+
+
+def _hooked(s) -> bool:
+    return s.weight_function is not None or s.bias_function is not None
+
+
+class Linear(nn.Module, DerivedMixin, CastWeightBiasOp):
     def __init__(self, in_features, out_features, bias=True, dtype=None, device=None):
         super().__init__()
         self.in_features = in_features
@@ -75,6 +101,9 @@ class Linear(nn.Module, DerivedMixin):
             self.register_parameter("bias", None)
 
     def forward(self, x, residual=None):
+        if _hooked(self):
+            w, b = cast_bias_weight(self, x)
+            return ops.linear(x, w, b, residual=residual)
         w, b = self.weight, self.bias
         if w.dtype == torch.float8_e4m3fn and w.device == x.device and x.dtype == torch.bfloat16 and x.is_cuda:
             # fp8-stored weights go to the fp8-weight GEMM as they are (widened inside the kernel)
@@ -85,7 +114,7 @@ class Linear(nn.Module, DerivedMixin):
         return ops.linear(x, w, b, residual=residual)
 
 
-class Conv2d(nn.Module, DerivedMixin):
+class Conv2d(nn.Module, DerivedMixin, CastWeightBiasOp):
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True,
                  groups=1, dtype=None, device=None, padding_mode="zeros"):
         super().__init__()
@@ -109,6 +138,12 @@ class Conv2d(nn.Module, DerivedMixin):
 
     def forward(self, x, residual=None, upsample2x=False, x2=None):
         """``x2``: convolve cat([x, x2], 1) without materialising the concat (K14)."""
+        if _hooked(self):    # per-call weight / bias hooks: transformed weights, no cached layouts
+            if x2 is not None:
+                x = torch.cat([x, x2], dim=1)
+            w, b = cast_bias_weight(self, x)
+            return ops.conv2d(x, w, b, self.stride, self.padding, residual=residual, groups=self.groups,
+                              upsample2x=upsample2x)
         w, b = self.weight, self.bias
         wn = None
         if x2 is not None:
