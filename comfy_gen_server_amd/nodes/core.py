@@ -436,6 +436,24 @@ class EmptyLatentImage:
         return ({"samples": latent},)
 
 
+def _cycle_batch(t, n):
+    """``t`` tiled along dim 0 to exactly ``n`` entries (a per-image tensor matched to a batch)."""
+    reps = -(-n // t.shape[0])
+    return t.repeat((reps,) + (1,) * (t.dim() - 1))[:n]
+
+
+def _pixel_target(w0, h0, width, height):
+    """Pixel size of a latent resize to (width, height) from a latent of (w0, h0): a 0 side follows the
+    aspect ratio; every side at least 64 px."""
+    if width == 0:
+        height = max(64, height)
+        return max(64, round(w0 * height / h0)), height
+    if height == 0:
+        width = max(64, width)
+        return width, max(64, round(h0 * width / w0))
+    return max(64, width), max(64, height)
+
+
 class LatentFromBatch:
     @classmethod
     def INPUT_TYPES(s):
@@ -446,24 +464,19 @@ class LatentFromBatch:
     CATEGORY = "latent/batch"
 
     def frombatch(self, samples, batch_index, length):
-        s = samples.copy()
-        s_in = samples["samples"]
-        batch_index = min(s_in.shape[0] - 1, batch_index)
-        length = min(s_in.shape[0] - batch_index, length)
-        s["samples"] = s_in[batch_index:batch_index + length].clone()
+        """Images [start, stop) of the batch (clamped into it); a per-image noise mask is cycled to the
+        batch first, a single mask kept; ``batch_index`` records the images' global indices."""
+        src = samples["samples"]
+        n = src.shape[0]
+        start = min(batch_index, n - 1)
+        stop = start + min(length, n - start)
+        out = dict(samples, samples=src[start:stop].clone())
         if "noise_mask" in samples:
-            masks = samples["noise_mask"]
-            if masks.shape[0] == 1:
-                s["noise_mask"] = masks.clone()
-            else:
-                if masks.shape[0] < s_in.shape[0]:
-                    masks = masks.repeat(math.ceil(s_in.shape[0] / masks.shape[0]), 1, 1, 1)[:s_in.shape[0]]
-                s["noise_mask"] = masks[batch_index:batch_index + length].clone()
-        if "batch_index" not in s:
-            s["batch_index"] = [x for x in range(batch_index, batch_index + length)]
-        else:
-            s["batch_index"] = samples["batch_index"][batch_index:batch_index + length]
-        return (s,)
+            mask = samples["noise_mask"]
+            out["noise_mask"] = mask.clone() if mask.shape[0] == 1 else _cycle_batch(mask, n)[start:stop].clone()
+        prev = samples.get("batch_index")
+        out["batch_index"] = list(range(start, stop)) if prev is None else prev[start:stop]
+        return (out,)
 
 
 class RepeatLatentBatch:
@@ -475,18 +488,19 @@ class RepeatLatentBatch:
     CATEGORY = "latent/batch"
 
     def repeat(self, samples, amount):
-        s = samples.copy()
-        s_in = samples["samples"]
-        s["samples"] = s_in.repeat((amount, 1, 1, 1))
-        if "noise_mask" in samples and samples["noise_mask"].shape[0] > 1:
-            masks = samples["noise_mask"]
-            if masks.shape[0] < s_in.shape[0]:
-                masks = masks.repeat(math.ceil(s_in.shape[0] / masks.shape[0]), 1, 1, 1)[:s_in.shape[0]]
-            s["noise_mask"] = samples["noise_mask"].repeat((amount, 1, 1, 1))
-        if "batch_index" in s:
-            offset = max(s["batch_index"]) - min(s["batch_index"]) + 1
-            s["batch_index"] = s["batch_index"] + [x + (i * offset) for i in range(1, amount) for x in s["batch_index"]]
-        return (s,)
+        """The batch tiled ``amount`` times; a per-image mask is tiled with it (as the reference does, the
+        mask's own batch is tiled, not first matched to the latent's); each copy of ``batch_index``
+        is shifted past the previous copy's span."""
+        src = samples["samples"]
+        out = dict(samples, samples=src.repeat((amount,) + (1,) * (src.dim() - 1)))
+        mask = samples.get("noise_mask")
+        if mask is not None and mask.shape[0] > 1:
+            out["noise_mask"] = mask.repeat((amount,) + (1,) * (mask.dim() - 1))
+        inds = samples.get("batch_index")
+        if inds is not None:
+            span = max(inds) - min(inds) + 1
+            out["batch_index"] = [x + k * span for k in range(amount) for x in inds]
+        return (out,)
 
 
 class LatentUpscale:
@@ -504,21 +518,12 @@ class LatentUpscale:
     CATEGORY = "latent"
 
     def upscale(self, samples, upscale_method, width, height, crop):
+        """Resize to a pixel size (0 on one side: keep the aspect ratio; both 0: unchanged)."""
         if width == 0 and height == 0:
-            s = samples
-        else:
-            s = samples.copy()
-            if width == 0:
-                height = max(64, height)
-                width = max(64, round(samples["samples"].shape[3] * height / samples["samples"].shape[2]))
-            elif height == 0:
-                width = max(64, width)
-                height = max(64, round(samples["samples"].shape[2] * width / samples["samples"].shape[3]))
-            else:
-                width = max(64, width)
-                height = max(64, height)
-            s["samples"] = U.common_upscale(samples["samples"], width // 8, height // 8, upscale_method, crop)
-        return (s,)
+            return (samples,)
+        lat = samples["samples"]
+        w, h = _pixel_target(lat.shape[3], lat.shape[2], width, height)
+        return (dict(samples, samples=U.common_upscale(lat, w // 8, h // 8, upscale_method, crop)),)
 
 
 class LatentUpscaleBy:
@@ -565,12 +570,10 @@ class LatentFlip:
     CATEGORY = "latent/transform"
 
     def flip(self, samples, flip_method):
-        s = samples.copy()
-        if flip_method.startswith("x"):
-            s["samples"] = torch.flip(samples["samples"], dims=[2])
-        elif flip_method.startswith("y"):
-            s["samples"] = torch.flip(samples["samples"], dims=[3])
-        return (s,)
+        dim = {"x": 2, "y": 3}.get(flip_method[:1])     # x-axis: rows (vertical), y-axis: columns
+        if dim is None:
+            return (dict(samples),)
+        return (dict(samples, samples=torch.flip(samples["samples"], dims=[dim])),)
 
 
 class LatentComposite:
