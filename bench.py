@@ -322,8 +322,13 @@ def _bench_latency(args, comm, gen, job, t0, t_build, log):
                "data": data_s,
                "config": {"model": model_s, "global_batch": 1,
                           "resolution": args.res, "sampler_steps": args.sampler_steps, "sampler": args.sampler,
-                          "cfg": args.cfg, "parallelism": f"cfg{lat.G}xtoken{lat.Q}"},
-               "unet_calls_on_rank0": lat.calls, "build_s": round(t_build, 1)}
+                          "cfg": args.cfg,
+                          "parallelism": f"cfg{lat.G}x{'rows' if lat.spatial_calls else 'token'}{lat.Q}"},
+               "unet_calls_on_rank0": lat.calls, "build_s": round(t_build, 1),
+               # row-sharded UNet calls (parallel/spatial.py): every layer on 1/Q of the rows per rank
+               "spatial_unet_calls": lat.spatial_calls,
+               "unet_rows_per_rank": (1.0 / lat.Q) if lat.spatial_calls else 1.0,
+               "spatial_stats": None if lat.spatial is None else dict(lat.spatial.stats)}
         res["op_backends"] = {f"{k[0]}:{k[1]}": v for k, v in sorted(ops.stats().items())}
         print(json.dumps(res), flush=True)
     comm.shutdown()

@@ -377,10 +377,14 @@ class SpatialTransformer(nn.Module):
         if not isinstance(context, list):
             context = [context] * len(self.transformer_blocks)
         sp = to.get("sp")
-        if sp is not None and sp.P > 1 and not to.get("patches") and not to.get("patches_replace") \
+        from ..parallel import spatial
+        if spatial.current() is not None:
+            pass     # row-sharded UNet: x is already this rank's token band; sp does the self-attention
+        elif sp is not None and sp.P > 1 and not to.get("patches") and not to.get("patches_replace") \
                 and (x.shape[2] * x.shape[3]) % sp.P == 0 and all(bk._plain for bk in self.transformer_blocks):
             return self._forward_sp(x, context, to, sp)
-        to = dict(to, sp=None) if sp is not None else to
+        else:
+            to = dict(to, sp=None) if sp is not None else to
         b, c, h, w = x.shape
         x_in = x
         x = self.norm(x)

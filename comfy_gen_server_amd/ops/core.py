@@ -552,7 +552,11 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
     ResBlock timestep-embedding add (openaimodel.py:245-264) is fused into the GroupNorm kernel.
     ``x2``: normalise ``cat([x, x2], 1)`` without materialising the concat (K14, the UNet decoder's
     skip connection, openaimodel.py:879); the kernel reads each 8-channel vector from its source.
+    Inside a row-sharded UNet call (parallel/spatial.py) the statistics are summed over the ranks.
     """
+    sc = _spatial()
+    if sc is not None and x.dim() == 4:
+        return sc.group_norm(x, groups, weight, bias, eps, silu=silu, pre_add=pre_add, x2=x2)
     be = backend_for("groupnorm", x, "cgs_groupnorm_nhwc_ws")
     Ct = x.shape[1] + (0 if x2 is None else x2.shape[1])
     if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16) and \
@@ -624,9 +628,31 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor 
 # ----------------------------------------------------------------------------------------------
 # Convolution
 # ----------------------------------------------------------------------------------------------
+def _spatial():
+    from ..parallel import spatial
+    return spatial.current()
+
+
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
            residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
            groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
+    """2-D convolution; inside a row-sharded UNet call (latency mode, parallel/spatial.py) the halo rows
+    come from the neighbouring ranks and the residual is added to the kept interior."""
+    sc = _spatial()
+    if sc is None:
+        return _conv2d(x, weight, bias, stride, padding, residual, weight_nhwc, groups, upsample2x, x2)
+    st = stride[0] if isinstance(stride, (tuple, list)) else stride
+    pd = padding[0] if isinstance(padding, (tuple, list)) else padding
+    y = sc.conv2d(lambda xx, _: _conv2d(xx, weight, bias, st, pd, None, weight_nhwc, groups, upsample2x, None),
+                  x, weight.shape[2], st, pd, upsample2x, x2)
+    if residual is not None:
+        y = y + residual
+    return y.contiguous(memory_format=torch.channels_last) if y.is_cuda else y
+
+
+def _conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
+            residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
+            groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
     """2-D convolution (K09/K10/K12). Device path: implicit-GEMM NHWC kernel on MFMA
     (csrc/kernels/conv.hip) with fused bias + residual epilogue; ``weight_nhwc`` = weight permuted
     to [Cout, kh, kw, Cin]. ``upsample2x`` reads the input through a nearest-2x upsample inside the

@@ -8,10 +8,15 @@ ranks as
 * **batch split** (CFG parallel): the P ranks form G = gcd(P, B) batch groups; group g evaluates rows
   [g*B/G, (g+1)*B/G) -- for one image at P = 2, rank 0 the conditional pass and rank 1 the
   unconditional one -- and the outputs are all-gathered (one collective per UNet call);
-* **token parallel** inside a group of P/G ranks (``SeqParallel``): every SpatialTransformer keeps
-  only the rank's token shard through its blocks (self-attention via Ulysses all-to-all or K/V
-  all-gather, cross-attention local), then all-gathers the tokens back for the ResBlocks, which run
-  replicated.
+* **spatial parallel** inside a group of Q = P/G ranks (``spatial.py``, the default when the latent
+  height divides into Q bands at every UNet level and no model patch is installed): every layer of
+  the UNet -- ResBlocks included -- runs on the rank's band of rows (halo rows for 3 x 3 convs,
+  group-summed GroupNorm statistics, self-attention over the whole image through ``SeqParallel``),
+  and the output rows are all-gathered: ~1/Q of the UNet FLOPs per rank;
+* otherwise **token parallel** in the group (``SeqParallel``): every SpatialTransformer keeps only the
+  rank's token shard through its blocks (self-attention via Ulysses all-to-all or K/V all-gather,
+  cross-attention local), then all-gathers the tokens back for the ResBlocks, which run replicated.
+  ``CGS_LATENCY_SPATIAL=0`` forces this form.
 
 Every rank runs the same sampler loop on the same latents (same seed, same noise: the per-image
 Philox streams of ``sampling/rng.py``), so the results are bit-compatible with each other and match
@@ -21,10 +26,12 @@ the single-GPU run to kernel-rounding. The whole mode is a ``model_function_wrap
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
 
+from . import spatial
 from .sp import SeqParallel
 
 
@@ -53,7 +60,38 @@ class LatencyParallel:
                 if q == self.rank % self.Q:
                     self.cross_group = pg
         self.sp = SeqParallel(self.tok_group) if self.Q > 1 else None
+        self.spatial = None
+        if self.Q > 1:
+            ranks = [self.bg * self.Q + q for q in range(self.Q)]
+            self.spatial = spatial.SpatialShard(self.tok_group, self.Q, self.rank % self.Q, ranks)
+        self.spatial_calls = 0
         self.calls = 0
+
+    def _spatial_ok(self, x, c):
+        """Row sharding applies: a band per rank at every level (height divisible by Q * 8: up to three
+        2x downsamples, >= 1 row per band), no model patches (their hooks see whole images)."""
+        if self.spatial is None or os.environ.get("CGS_LATENCY_SPATIAL", "1") == "0":
+            return False
+        to = c.get("transformer_options", {})
+        if to.get("patches") or to.get("patches_replace"):
+            return False
+        return x.dim() == 4 and x.shape[2] % (self.Q * 8) == 0
+
+    def _apply_spatial(self, apply_model, x, t, c):
+        """One UNet call on this rank's band of rows (latent, c_concat and ControlNet residuals cut to
+        the band), the output rows all-gathered over the token group."""
+        sc = self.spatial
+        c = dict(c)
+        if torch.is_tensor(c.get("c_concat")) and c["c_concat"].dim() == 4:
+            c["c_concat"] = sc.shard_rows(c["c_concat"])
+        ctrl = c.get("control")
+        if isinstance(ctrl, dict):
+            c["control"] = {k: [sc.shard_rows(v) if torch.is_tensor(v) and v.dim() == 4 else v for v in vs]
+                            for k, vs in ctrl.items()}
+        self.spatial_calls += 1
+        with spatial.active(sc):
+            out = apply_model(sc.shard_rows(x).contiguous(), t, **c)
+        return sc.gather_rows(out)
 
     # --------------------------------------------------------------------------------------------
     def _slice(self, v, B, lo, hi):
@@ -75,10 +113,16 @@ class LatencyParallel:
             to["sp"] = self.sp
         c["transformer_options"] = to
         if self.G == 1 or B % self.G:
+            if self._spatial_ok(x, c):
+                return self._apply_spatial(apply_model, x, t, c)
             return apply_model(x, t, **c)
         n = B // self.G
         lo, hi = self.bg * n, (self.bg + 1) * n
-        out = apply_model(x[lo:hi], t[lo:hi], **self._slice(c, B, lo, hi))
+        cs = self._slice(c, B, lo, hi)
+        if self._spatial_ok(x, cs):
+            out = self._apply_spatial(apply_model, x[lo:hi], t[lo:hi], cs)
+        else:
+            out = apply_model(x[lo:hi], t[lo:hi], **cs)
         parts = [torch.empty_like(out) for _ in range(self.G)]
         dist.all_gather(parts, out.contiguous(), group=self.cross_group)
         return torch.cat(parts, 0)

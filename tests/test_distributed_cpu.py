@@ -303,7 +303,8 @@ lay = int(os.environ["CGS_TEST_LAYOUT_BATCH"])
 with torch.inference_mode():
     patcher, clip, vae = build_pipeline("tiny", device=torch.device("cpu"), dtype=torch.float32, seed=5)
     lp = LatencyParallel(c, batch=lay)
-    job = Job(batch=1, steps=4, width=64, height=64, seed=21)
+    res = int(os.environ.get("CGS_TEST_RES", "64"))
+    job = Job(batch=1, steps=4, width=res, height=res, seed=21)
     ref = generate_local(patcher, clip, vae, job, 0, 1, decode=False)
     got = generate_local(lp.patch(patcher), clip, vae, job, 0, 1, decode=False)
 assert lp.calls >= 4, lp.calls
@@ -313,6 +314,11 @@ if lp.Q > 1:
     mode = os.environ.get("CGS_SP_ATTN", "auto")
     if mode in ("ring", "kvgather"):
         assert st[mode] > 0, st
+if os.environ.get("CGS_TEST_EXPECT_SPATIAL") == "1":
+    # every UNet call row-sharded: halo exchanges, group-summed GroupNorms, no whole-image fallback conv
+    assert lp.spatial_calls == lp.calls, (lp.spatial_calls, lp.calls)
+    st = lp.spatial.stats
+    assert st["halo"] > 0 and st["gn"] > 0 and st["gather_fallback"] == 0, st
 d = (got - ref).abs().max().item()
 print("layout", lay, "G", lp.G, "Q", lp.Q, "maxdiff", d, "sp", None if lp.sp is None else lp.sp.stats, flush=True)
 # the batch split changes CPU BLAS blocking (reduction order): fp32 round-off, scaled to the latent
@@ -321,16 +327,23 @@ c.shutdown()
 '''
 
 
-@pytest.mark.parametrize("world,layout_batch,attn", [(2, 2, "auto"), (2, 1, "auto"), (2, 1, "kvgather"),
-                                                     (4, 2, "auto"), (2, 1, "ring")])
-def test_latency_mode_matches_single_gpu(tmp_path, world, layout_batch, attn):
+@pytest.mark.parametrize("world,layout_batch,attn,res", [(2, 2, "auto", 64), (2, 1, "auto", 64),
+                                                         (2, 1, "kvgather", 64), (4, 2, "auto", 64),
+                                                         (2, 1, "ring", 64), (2, 1, "auto", 128),
+                                                         (4, 1, "auto", 256), (4, 2, "kvgather", 128)])
+def test_latency_mode_matches_single_gpu(tmp_path, world, layout_batch, attn, res):
     """Latency mode (parallel/latency.py) on gloo: CFG/batch split (G groups) x token-parallel
     SpatialTransformers (Q ranks: Ulysses / K-V all-gather / ring attention) sample the same
-    latents as the plain single-process sampler."""
+    latents as the plain single-process sampler. At 128^2 / 256^2 the latent divides into Q row bands
+    at every level, so the whole UNet runs row-sharded (parallel/spatial.py: halo exchange per 3x3
+    conv, group-summed GroupNorm statistics) -- still equal to the single process."""
     script = tmp_path / "lat_worker.py"
     script.write_text(_LAT_WORKER)
     env = _env()
-    env.update(MASTER_ADDR="127.0.0.1", CGS_TEST_LAYOUT_BATCH=str(layout_batch), CGS_SP_ATTN=attn)
+    env.update(MASTER_ADDR="127.0.0.1", CGS_TEST_LAYOUT_BATCH=str(layout_batch), CGS_SP_ATTN=attn,
+               CGS_TEST_RES=str(res))
+    if res >= 128:
+        env["CGS_TEST_EXPECT_SPATIAL"] = "1"
     port = str(_free_port())
     procs = [subprocess.Popen([sys.executable, str(script)], cwd=ROOT,
                               env=dict(env, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r), MASTER_PORT=port),
