@@ -170,7 +170,7 @@ KERNEL_SIGNATURES = {
     "cgs_abort_stream_capture": [_P],
     "cgs_channel_affine2": [_P, _P, _P, _L, _P, _I, _I, _I, _F, _I, _P],
     # "w4" GEMM (gemm_w4.hip, one wave per SIMD): A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, rs, cs
-    "cgs_gemm_bf16_w4": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _P, _P],
+    "cgs_gemm_bf16_w4": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _P, _I, _P],
     "cgs_w4_set_group": [_I],
 }
 

@@ -32,7 +32,7 @@ def main(argv):
                 return
             if var == "w4":
                 err = lib.cgs_gemm_bf16_w4(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K, K, K, N, 0,
-                                           0, 1.0, None, None, core._stream())
+                                           0, 1.0, None, None, 0, core._stream())
             else:
                 err = lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K, K, K, N, 0,
                                           0, 1.0, int(var), core._stream())
