@@ -83,6 +83,10 @@ KERNEL_SIGNATURES = {
     # per-call kernel variant (op-layer autotune): ..., scale, variant, stream
     "cgs_flash_attn_fwd_v": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _F,
                              _I, _P],
+    # generic kernel + additive fp32 bias [H,Sq,Sk] and window mask [nW,Sq,Sk] (Swin family): ..., scale, bias,
+    # mask, nW, hscale [H] fp32 or null, stream
+    "cgs_flash_attn_fwd_bias": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L,
+                                _F, _P, _P, _I, _P, _P],
     # same + fp32 LSE [B, H, Sq] out (ring attention merge): q,k,v,o,lse, B,H,Sq,Sk,D, 12 strides, scale
     "cgs_flash_attn_fwd_lse": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L,
                                _F, _P],

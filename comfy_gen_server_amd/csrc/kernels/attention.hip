@@ -21,13 +21,25 @@
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-template <int DP>
+// Additive fp32 score terms of the generic kernel (Swin-family window attention, K04): ``bias`` [H, Sq, Sk]
+// (relative-position bias, shared by every batch entry) and ``mask`` [nW, Sq, Sk] for batch entry b taken at
+// b % nW (shifted-window mask; -inf blocks a key). Both are added to the scaled scores before the softmax.
+// ``hscale`` [H] (optional) multiplies head h's scores first (SwinV2's learned logit scale on cosine scores).
+struct AttnBias {
+  const float* bias;
+  const float* mask;
+  const float* hscale;
+  int nW;
+};
+
+template <int DP, bool BIAS = false>
 __global__ __launch_bounds__(256, (DP >= 160 ? 1 : 2)) void flash_fwd_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int B, int H, int Sq, int Sk, int D,
     long long qsb, long long qss, long long qsh, long long ksb, long long kss, long long ksh,
     long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
-    float scale_log2, const signed char* __restrict__ key_mask, int causal, int nqb, float* __restrict__ lse) {
+    float scale_log2, const signed char* __restrict__ key_mask, int causal, int nqb, float* __restrict__ lse,
+    AttnBias ab = AttnBias{nullptr, nullptr, nullptr, 1}) {
   constexpr int KS = DP / 16;        // k-steps of the QK product
   constexpr int NDT = DP / 32;       // 32-wide d tiles of the output
   constexpr int LDW = DP + 8;        // padded LDS row (elements)
@@ -77,6 +89,7 @@ __global__ __launch_bounds__(256, (DP >= 160 ? 1 : 2)) void flash_fwd_kernel(
   float m_run = -INFINITY;
   float l_run = 0.f;
 
+  if (BIAS && ab.hscale) scale_log2 *= ab.hscale[h];
   const int ntiles = (Sk + ATT_KV - 1) / ATT_KV;
   int tiles_end = ntiles;
   if (causal) {
@@ -138,6 +151,13 @@ __global__ __launch_bounds__(256, (DP >= 160 ? 1 : 2)) void flash_fwd_kernel(
         bool valid = key < Sk;
         if (key_mask) valid = valid && key_mask[(long long)b * Sk + min(key, Sk - 1)] != 0;
         if (causal) valid = valid && key <= q_row;
+        if (BIAS) {
+          // LOG2E: the scores live in the exp2 domain
+          const long long qk = (long long)min(q_row, Sq - 1) * Sk + min(key, Sk - 1);
+          float add = ab.bias[(long long)h * Sq * Sk + qk];
+          if (ab.mask) add += ab.mask[(long long)(b % ab.nW) * Sq * Sk + qk];
+          v = fmaf(add, 1.4426950408889634f, v);
+        }
         v = valid ? v : -INFINITY;
         s[kt][r] = v;
         tmax = fmaxf(tmax, v);
@@ -1216,6 +1236,34 @@ CGS_EXPORT int cgs_flash_attn_fwd_kv2(const void* q, const void* k1, const void*
     attn_fwd_d64_kernel<8, true><<<dim3((unsigned)nwg2), 512, 0, stream>>>(
         (const u16*)q, (const u16*)k1, (const u16*)v1, (u16*)o, H, Sq, Sk, qsb, qss, 64, k1sb, k1ss, 64, v1sb, v1ss, 64,
         osb, oss, 64, sl2, nqb2, nullptr, kv2);
+  return (int)hipGetLastError();
+}
+
+// Generic flash kernel with additive fp32 score terms (AttnBias): bias [H, Sq, Sk] contiguous, mask
+// [nW, Sq, Sk] contiguous or null (batch entry b uses mask b % nW), per-head score multiplier hscale [H] or
+// null. D <= 160, D % 8 == 0.
+CGS_EXPORT int cgs_flash_attn_fwd_bias(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
+                                       int Sk, int D, long long qsb, long long qss, long long qsh, long long ksb,
+                                       long long kss, long long ksh, long long vsb, long long vss, long long vsh,
+                                       long long osb, long long oss, long long osh, float scale, const float* bias,
+                                       const float* mask, int nW, const float* hscale, hipStream_t stream) {
+  if (D % 8 || D > 160 || !bias || nW <= 0 || B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
+  const int nqb = (Sq + ATT_QB - 1) / ATT_QB;
+  const long long nwg = (long long)nqb * B * H;
+  if (nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * 1.4426950408889634f;
+  const AttnBias ab{bias, mask, hscale, nW};
+  dim3 grid((unsigned)nwg);
+#define ATTB_LAUNCH(DPV)                                                                                          \
+  flash_fwd_kernel<DPV, true><<<grid, 256, 0, stream>>>((const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, B, H, \
+                                                        Sq, Sk, D, qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh, osb, \
+                                                        oss, osh, sl2, nullptr, 0, nqb, nullptr, ab)
+  if (D <= 32) ATTB_LAUNCH(32);
+  else if (D <= 64) ATTB_LAUNCH(64);
+  else if (D <= 96) ATTB_LAUNCH(96);
+  else if (D <= 128) ATTB_LAUNCH(128);
+  else ATTB_LAUNCH(160);
+#undef ATTB_LAUNCH
   return (int)hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import ops
 from .layers import Conv2d, LayerNorm, Linear
 from .swin_sr import _resi_conv, _Upsample, _to_img, _to_tokens
 
@@ -86,13 +87,9 @@ class _RectWindowAttention(nn.Module):
             return t.transpose(1, 2)
 
         qw, kw, vw = win(q), win(k), win(v)
-        s = ((qw * self.scale) @ kw.transpose(-2, -1)).float()
         bias = self.pos(self.rpe_tab.to(self.pos.pos_proj.weight.dtype)).float()[self.rel_idx.reshape(-1)]
-        s = s + bias.view(N, N, h).permute(2, 0, 1)
-        if mask is not None:
-            nW = mask.shape[0]
-            s = (s.view(-1, nW, h, N, N) + mask[None, :, None]).view(-1, h, N, N)
-        o = (torch.softmax(s, -1).to(vw.dtype) @ vw).transpose(1, 2).reshape(-1, N, C)
+        bias = bias.view(N, N, h).permute(2, 0, 1)
+        o = ops.attention_bias(qw, kw, vw, bias, mask, scale=self.scale).transpose(1, 2).reshape(-1, N, C)
         return o.view(B, H // wh, W // ww, wh, ww, C).permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, C)
 
 

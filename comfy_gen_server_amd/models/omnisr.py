@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import ops
 from .layers import Conv2d, LayerNorm, Linear
 from .swin_sr import _rel_index
 
@@ -75,9 +76,8 @@ class _WinAttention(nn.Module):
         Bw, N, C = t.shape
         h = self.heads
         q, k, v = self.to_qkv(t).view(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4).unbind(0)
-        s = ((q * self.scale) @ k.transpose(-2, -1)).float()
-        s = s + self.rel_pos_bias.weight.float()[self.rel_idx].permute(2, 0, 1)
-        o = (torch.softmax(s, -1).to(v.dtype) @ v).transpose(1, 2).reshape(Bw, N, C)
+        bias = self.rel_pos_bias.weight.float()[self.rel_idx].permute(2, 0, 1)
+        o = ops.attention_bias(q, k, v, bias, scale=self.scale).transpose(1, 2).reshape(Bw, N, C)
         return self.to_out(o)
 
 

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import ops
 from .layers import Conv2d, LayerNorm, Linear
 
 
@@ -118,17 +119,14 @@ class WindowAttention(nn.Module):
         else:
             qkv = self.qkv(x)
         q, k, v = qkv.view(Bw, N, 3, h, C // h).permute(2, 0, 3, 1, 4).unbind(0)
-        if self.v2:
-            s = F.normalize(q.float(), dim=-1) @ F.normalize(k.float(), dim=-1).transpose(-2, -1)
-            s = s * torch.clamp(self.logit_scale.float(), max=math.log(100.0)).exp()
+        if self.v2:     # cosine scores: unit q / k, the per-head logit scale on the fp32 scores
+            q = F.normalize(q.float(), dim=-1).to(v.dtype)
+            k = F.normalize(k.float(), dim=-1).to(v.dtype)
+            o = ops.attention_bias(q, k, v, self.position_bias(), mask, scale=1.0,
+                                   head_scale=torch.clamp(self.logit_scale.float(), max=math.log(100.0)).exp())
         else:
-            s = (q * self.scale) @ k.transpose(-2, -1)
-        s = s.float() + self.position_bias()
-        if mask is not None:
-            nW = mask.shape[0]
-            s = (s.view(Bw // nW, nW, h, N, N) + mask[None, :, None]).view(Bw, h, N, N)
-        p = torch.softmax(s, dim=-1).to(v.dtype)
-        return self.proj((p @ v).transpose(1, 2).reshape(Bw, N, C))
+            o = ops.attention_bias(q, k, v, self.position_bias(), mask, scale=self.scale)
+        return self.proj(o.transpose(1, 2).reshape(Bw, N, C))
 
 
 class _Mlp(nn.Module):
@@ -465,8 +463,7 @@ class OCAB(nn.Module):
         vh = kv[1].view(-1, ows * ows, h, d).transpose(1, 2)
         bias = self.relative_position_bias_table.float()[self.rel_index.reshape(-1)]
         bias = bias.view(ws * ws, ows * ows, h).permute(2, 0, 1)
-        s = ((qh * self.scale) @ kh.transpose(-2, -1)).float() + bias
-        o = (torch.softmax(s, -1).to(vh.dtype) @ vh).transpose(1, 2).reshape(-1, ws * ws, C)
+        o = ops.attention_bias(qh, kh, vh, bias, scale=self.scale).transpose(1, 2).reshape(-1, ws * ws, C)
         x = self.proj(_reverse(o, ws, B, H, W).reshape(B, L, C)) + x
         return x + self.mlp(self.norm2(x))
 
@@ -607,13 +604,9 @@ class _WMSA(nn.Module):
             x = torch.roll(x, (-(p // 2), -(p // 2)), (1, 2))
         win = _partition(x, p)                                          # [B*nW, N, C]
         q, k, v = self.embedding_layer(win).view(win.shape[0], p * p, 3, h, self.hd).permute(2, 0, 3, 1, 4).unbind(0)
-        s = ((q * self.hd ** -0.5) @ k.transpose(-2, -1)).float()
-        s = s + self.relative_position_params.float()[:, self.rel[..., 0], self.rel[..., 1]]
-        if self.shifted:
-            nW = (H // p) * (W // p)
-            m = _scunet_mask(H // p, W // p, p, x.device)
-            s = s.view(B, nW, h, p * p, p * p).masked_fill(m[None, :, None], float("-inf")).view_as(s)
-        o = (torch.softmax(s, -1).to(v.dtype) @ v).transpose(1, 2).reshape(-1, p * p, C)
+        bias = self.relative_position_params.float()[:, self.rel[..., 0], self.rel[..., 1]]
+        m = _scunet_mask(H // p, W // p, p, x.device) if self.shifted else None     # bool, True = blocked
+        o = ops.attention_bias(q, k, v, bias, m, scale=self.hd ** -0.5).transpose(1, 2).reshape(-1, p * p, C)
         y = _reverse(self.linear(o), p, B, H, W)
         if self.shifted:
             y = torch.roll(y, (p // 2, p // 2), (1, 2))

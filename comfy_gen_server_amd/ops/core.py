@@ -371,6 +371,63 @@ def attention_kv2(q: torch.Tensor, k1: torch.Tensor, v1: torch.Tensor, k2: torch
     return attention(q, torch.cat([k1, k2.to(k1.dtype)], dim=1), torch.cat([v1, v2.to(v1.dtype)], dim=1), heads)
 
 
+def attention_bias(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, bias: torch.Tensor,
+                   mask: torch.Tensor | None = None, scale: float | None = None,
+                   head_scale: torch.Tensor | None = None) -> torch.Tensor:
+    """Head-major windowed attention with additive score terms (Swin-family upscalers: SwinIR / Swin2SR /
+    HAT / DAT / OmniSR / SCUNet, reference ``comfy_extras/chainner_models/architecture/SwinIR.py:176-186``):
+
+        softmax(scale * head_scale[h] * q k^T + bias[h] + mask[b % nW]) v        (fp32 scores and softmax)
+
+    q [B, H, Sq, D], k / v [B, H, Sk, D] (last dim contiguous), ``bias`` [H, Sq, Sk], ``mask`` [nW, Sq, Sk]
+    additive float (or bool, True = blocked) with B % nW == 0 -- the window index of batch entry b is
+    b % nW, the (image, window) flattening of ``_partition``. ``head_scale`` [H] (SwinV2's clamped, exponentiated
+    logit scale on cosine scores) is applied to the fp32 scores. Returns [B, H, Sq, D] in q's dtype.
+    bf16 on the GPU runs the generic flash kernel with the terms added in its softmax loop (no [B, H, Sq,
+    Sk] score tensor); head dims that are not a multiple of 8 (Swin's 30) are zero-padded."""
+    B, H, Sq, D = q.shape
+    Sk = k.shape[2]
+    scale = D ** -0.5 if scale is None else float(scale)
+    if mask is not None and mask.dtype == torch.bool:
+        mask = torch.zeros(mask.shape, device=mask.device, dtype=torch.float32).masked_fill(mask, float("-inf"))
+    nW = 1 if mask is None else mask.shape[0]
+    ok = (q.is_cuda and q.dtype == torch.bfloat16 and k.dtype == q.dtype and v.dtype == q.dtype and D <= 160
+          and B % nW == 0 and tuple(bias.shape) == (H, Sq, Sk)
+          and (mask is None or tuple(mask.shape[1:]) == (Sq, Sk))
+          and backend_for("attention", q, "cgs_flash_attn_fwd_bias") == "hip")
+    if ok:
+        Dp = (D + 7) // 8 * 8
+
+        def prep(t):
+            if Dp != D:
+                return F.pad(t, (0, Dp - D))
+            return t if t.stride(-1) == 1 and t.stride(2) % 8 == 0 and t.stride(1) % 8 == 0 and t.stride(0) % 8 == 0 \
+                and t.data_ptr() % 16 == 0 else t.contiguous()
+        qp, kp, vp = prep(q), prep(k), prep(v)
+        bias_f = bias.float().contiguous()
+        mask_f = None if mask is None else mask.float().contiguous()
+        hs = None if head_scale is None else head_scale.float().reshape(H).contiguous()
+        o = torch.empty((B, Sq, H, Dp), device=q.device, dtype=q.dtype)
+        _check(_lib().cgs_flash_attn_fwd_bias(
+            qp.data_ptr(), kp.data_ptr(), vp.data_ptr(), o.data_ptr(), B, H, Sq, Sk, Dp,
+            qp.stride(0), qp.stride(2), qp.stride(1), kp.stride(0), kp.stride(2), kp.stride(1),
+            vp.stride(0), vp.stride(2), vp.stride(1), o.stride(0), o.stride(1), o.stride(2),
+            scale, bias_f.data_ptr(), _ptr(mask_f), nW, _ptr(hs), _stream()), "cgs_flash_attn_fwd_bias")
+        count("attention", "hip")
+        return o[..., :D].transpose(1, 2)
+    if q.device.type != "cpu":
+        vendor_fallback("attention", f"bias attention dtype {q.dtype}, head dim {D}")
+    else:
+        count("attention", "torch")
+    s = ((q * scale) @ k.transpose(-2, -1)).float()                      # the models' own eager math
+    if head_scale is not None:
+        s = s * head_scale.float().reshape(H, 1, 1)
+    s = s + bias.float()
+    if mask is not None:
+        s = (s.view(B // nW, nW, H, Sq, Sk) + mask.float()[None, :, None]).view(B, H, Sq, Sk)
+    return torch.softmax(s, -1).to(v.dtype) @ v
+
+
 def attention_lse(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int):
     """Unmasked attention plus the natural-log log-sum-exp of the scaled scores per (b, h, query):
     ``(o [B, Sq, H*D] in q's dtype, lse fp32 [B, H, Sq])`` -- the partial result of one K/V block

@@ -112,6 +112,46 @@ def test_flash_attention_causal_and_spike(cuda):
     assert _rel(o, ref) < 2e-2
 
 
+@pytest.mark.parametrize("Bw,H,Sq,Sk,D,nW,kind", [
+    (32, 6, 64, 64, 30, 4, "float"),       # SwinIR / HAT: 8x8 windows, head dim 30 (zero-padded), shift mask
+    (8, 6, 256, 576, 30, 0, "none"),       # HAT overlapping cross-attention: 16x16 queries, 24x24 keys
+    (16, 4, 64, 64, 32, 8, "bool"),        # SCUNet: -inf blocks from a bool mask
+    (6, 3, 64, 64, 60, 2, "v2"),           # Swin2SR: cosine scores x per-head logit scale
+    (2, 2, 130, 130, 64, 0, "none"),       # ragged query / key tiles
+])
+def test_attention_bias(cuda, Bw, H, Sq, Sk, D, nW, kind):
+    """Additive bias + window mask in the flash kernel's softmax vs the fp32 math of the Swin models."""
+    torch.manual_seed(3)
+    q = torch.randn(Bw, H, Sq, D, device=cuda)
+    k = torch.randn(Bw, H, Sk, D, device=cuda)
+    v = torch.randn(Bw, H, Sk, D, device=cuda)
+    bias = torch.randn(H, Sq, Sk, device=cuda) * 2
+    hs = None
+    if kind == "v2":
+        q, k = F.normalize(q, dim=-1), F.normalize(k, dim=-1)
+        hs = torch.tensor([10.0, 25.0, 100.0], device=cuda)
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    mask = None
+    if kind == "float":
+        mask = torch.where(torch.rand(nW, Sq, Sk, device=cuda) < 0.3, -100.0, 0.0)
+    elif kind == "bool":
+        mask = torch.rand(nW, Sq, Sk, device=cuda) < 0.4
+        mask[..., 0] = False                                  # every query keeps a key
+    scale = 1.0 if kind == "v2" else D ** -0.5
+    o = ops.attention_bias(q, k, v, bias, mask, scale=scale, head_scale=hs)
+    assert ops.stats().get(("attention", "hip"), 0) == 1
+    s = (q.float() @ k.float().transpose(-2, -1)) * scale
+    if hs is not None:
+        s = s * hs[:, None, None]
+    s = s + bias
+    if mask is not None:
+        m = mask if mask.dtype != torch.bool else torch.zeros(mask.shape, device=cuda).masked_fill(mask, -math.inf)
+        s = (s.view(Bw // nW, nW, H, Sq, Sk) + m[None, :, None]).view(Bw, H, Sq, Sk)
+    ref = torch.softmax(s, -1) @ v.float()
+    assert o.shape == ref.shape
+    assert _rel(o, ref) < 2e-2
+
+
 @pytest.mark.parametrize("N,H,W,C,k,rep", [(2, 24, 24, 64, 3, False), (1, 17, 9, 2048, 3, False),
                                             (1, 32, 31, 192, 3, True), (2, 8, 8, 16, 5, False)])
 def test_depthwise_conv_nhwc(cuda, N, H, W, C, k, rep):

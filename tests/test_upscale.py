@@ -231,6 +231,7 @@ def test_swin_family_gpu(cuda, kind):
         ops.reset_stats()
         y = g(x.to(cuda, torch.bfloat16)).float().cpu()
     assert ops.stats().get(("gemm", "hip"), 0) + ops.stats().get(("gemm", "lib"), 0) > 0
+    assert ops.stats().get(("attention", "hip"), 0) > 0          # window attention on the flash kernel
     assert ((y - ref).norm() / ref.norm()).item() < 3e-2
 
 
