@@ -119,6 +119,10 @@ KERNEL_SIGNATURES = {
     "cgs_resize": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],        # x, y, NC, H, W, Ho, Wo, mode, align
     "cgs_vq_nearest": [_P, _P, _P, _P, _I, _I, _I, _I, _P],            # z, codebook, idx(i64), q, M, n, D
     "cgs_grn_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P],          # x, gamma, beta, y, ws, N, HW, C
+    # GRN statistics only (gx / block sums in the v2 ws layout): x, ws, N, HW, C, pre_gelu, dtype
+    "cgs_grn_stats": [_P, _P, _I, _I, _I, _I, _I, _P],
+    # per-image GRN-scaled weights of the next Linear: W, gamma, ws(stats), N, HW, O, K, Wn
+    "cgs_grn_scale_weight": [_P, _P, _P, _I, _I, _I, _I, _P, _P],
     # host (mmap) -> device upload through pinned double buffers (csrc/kernels/io.hip)
     "cgs_h2d_upload": [_P, _P, _L, _L, _I, _P],                        # src, dst, nbytes, chunk, threads
     "cgs_softmax_rows": [_P, _P, _L, _I, _F, _I, _P],                  # x, y(f32), rows, cols, scale, dtype

@@ -26,6 +26,7 @@
 #define EPI_GEGLU 4
 #define EPI_LNFOLD 8
 #define EPI_F32OUT 16   // fp32 C (v7 only; attention scores of the wide-head path)
+#define EPI_GELU 32     // GELU(acc * alpha + bias) before the residual: v6 (ACT kernel), mc::tile kernels, skinny
 
 // fp8 e4m3fn (OCP) -> bf16 bits, exact (every e4m3 value is a bf16 value); NaN stays NaN.
 __device__ __forceinline__ u16 fp8e4m3_to_bf16(uint32_t b) {
@@ -540,7 +541,7 @@ struct DenseA32 {
 
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
-template <bool LN = false, int DS = 0, bool GG = false>
+template <bool LN = false, int DS = 0, bool GG = false, bool ACT = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // (profiles/r03/v6_offsets32.log)
   DenseA8 al{A, lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
-  pq::run<DenseA8, LN, DS, false, GG>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  pq::run<DenseA8, LN, DS, false, GG, ACT>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
 }
 static int num_cus() {
   static int n = 0;
@@ -580,17 +581,17 @@ int v6_conv_ds() {
 }
 CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; g_v6_conv_ds = m; }
 
-template <bool LN, int DS, bool GG = false>
+template <bool LN, int DS, bool GG = false, bool ACT = false>
 static void gemm_v6_go(int grid, const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                        int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                        int tiles_m, int tiles_n, hipStream_t stream, const float* rs, const float* cs) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
     attr_set = true;
   }
-  gemm_bf16_nt_v6_kernel<LN, DS, GG><<<grid, pq::THREADS, pq::LDS, stream>>>(
+  gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT><<<grid, pq::THREADS, pq::LDS, stream>>>(
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
       tiles_m, tiles_n, g_tile_group, rs, cs);
 }
@@ -603,6 +604,12 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
   const int ds = v6_ds();
+  if (epi & EPI_GELU) {    // GELU epilogue: plain (no GEGLU / LayerNorm fold) form only
+    if (epi & (EPI_GEGLU | EPI_LNFOLD)) return (int)hipErrorInvalidValue;
+    gemm_v6_go<false, 1, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n,
+                                      stream, rs, cs);
+    return (int)hipGetLastError();
+  }
   if (epi & EPI_GEGLU) {   // GEGLU epilogue (pq::run GG): split-DMA main loop, N % 160 == 0 (host-checked)
     if (epi & EPI_LNFOLD)
       gemm_v6_go<true, 1, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n,
@@ -784,6 +791,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(const u16* _
       const int row = mr * 16 + fq * 4 + r;
       if (row < M && col < N) {
         float o = v[r] * alpha + bv;
+        if (epi & EPI_GELU) o = gelu_sig(o);
         if (epi & EPI_RESIDUAL) o += bf2f(R[(long long)row * ldr + col]);
         C[(long long)row * ldc + col] = f2bf(o);
       }
@@ -823,6 +831,26 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   if (K % 8 || lda % 8 || ldw % 8) return (int)hipErrorInvalidValue;
   if ((epi & EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
+  if (epi & EPI_GELU) {
+    // GELU epilogue kernels: skinny (M <= 128), v6 (variant 6), the mc::tile family (v3 / v4, v8 and the
+    // small tiles; auto = v8). No GEGLU / LayerNorm-fold / fp32-out combination.
+    if (epi & (EPI_GEGLU | EPI_LNFOLD | EPI_F32OUT)) return (int)hipErrorInvalidValue;
+    const bool ok = (K % 32 == 0) && (N % 8 == 0) && (ldc % 8 == 0) && (!(epi & EPI_RESIDUAL) || ldr % 8 == 0) &&
+                    ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16 == 0);
+    if (!ok) return (int)hipErrorInvalidValue;
+    if (M <= 128 && (variant == -1 || variant == 9))
+      return gemm_skinny_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    if (variant == 6) {
+      if (K % 64 || K < 128 || ((uintptr_t)bias % 8)) return (int)hipErrorInvalidValue;
+      return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    }
+    if (variant == 3 || variant == 4)
+      return gemm_v3_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, variant == 3 ? 4 : 8, stream);
+    if (variant == -1 || variant == 8 || (variant >= 10 && variant <= 14))
+      return gemm_v8_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream,
+                            variant == -1 ? 8 : variant);
+    return (int)hipErrorInvalidValue;
+  }
   // v2 needs K % 64 == 0 and 16-B aligned rows; it pays off once there are >= ~256 big tiles'
   // worth of work (otherwise the 128x128 kernel keeps more CUs busy).
   bool v2_ok = (K % 64 == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M >= 256 && N >= 128 &&

@@ -883,6 +883,88 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
   return (int)hipGetLastError();
 }
 
+// GRN statistics only (passes 1-2 of cgs_grn_nhwc_v2, same ws layout): gx = ws + N * S * C ([N, C]) and the
+// finalize block sums bsum = gx + N * C ([N, ceil(C / 256)]), for a consumer that folds the GRN scale into
+// the next GEMM's weights (cgs_grn_scale_weight) instead of rewriting the activation.
+CGS_EXPORT int cgs_grn_stats(const void* x, float* ws, int N, int HW, int C, int pre_gelu, int dtype,
+                             hipStream_t stream) {
+  if (N <= 0 || HW <= 0) return 0;
+  if (C % 8 || dtype == CGS_F32 || ((uintptr_t)x & 15) || N > GRN_MAXN) return (int)hipErrorInvalidValue;
+  const int S = cgs_grn_slices(N, HW, C);
+  const int rows_per = (HW + S - 1) / S;
+  float* part = ws;
+  float* gx = ws + (size_t)N * S * C;
+  const int nblk = (C + 255) / 256;
+  float* bsum = gx + (size_t)N * C;
+  dim3 g1((unsigned)((C / 8 + 63) / 64), (unsigned)S, (unsigned)N);
+#define CGS_GRNS(DTV, GV)                                                                      \
+  grn2_sumsq_kernel<DTV, GV><<<g1, 256, 0, stream>>>((const u16*)x, part, HW, C, rows_per, S); \
+  grn2_finalize_kernel<<<dim3((unsigned)nblk, (unsigned)N), 256, 0, stream>>>(part, gx, bsum, C, S)
+  if (dtype == CGS_BF16) {
+    if (pre_gelu) { CGS_GRNS(CGS_BF16, true); } else { CGS_GRNS(CGS_BF16, false); }
+  } else {
+    if (pre_gelu) { CGS_GRNS(CGS_F16, true); } else { CGS_GRNS(CGS_F16, false); }
+  }
+#undef CGS_GRNS
+  return (int)hipGetLastError();
+}
+
+// GRN folded into the following Linear (Cascade ChannelMLP: GRN -> Linear): for image n,
+//   (beta + a * (1 + gamma * nx_n)) W^T = a (W * s_n)^T + W beta,   s_n[k] = 1 + gamma[k] * nx_n[k]
+// so Wn[n] = W * s_n (bf16, [N, O, K]) replaces the rewrite of the [N, HW, K] activation -- the cheaper
+// pass whenever O < HW. nx_n = gx[n] / (mean_k gx[n] + 1e-6) from cgs_grn_stats. One thread per 8-wide K
+// chunk of W, looping over the images (W read once).
+__global__ void __launch_bounds__(256) grn_scale_weight_kernel(const u16* __restrict__ W, const u16* __restrict__ gamma,
+                                                               const float* __restrict__ gx,
+                                                               const float* __restrict__ bsum, int nblk, int N,
+                                                               u16* __restrict__ Wn, long long chunks, int K) {
+  __shared__ float inv_s[GRN_MAXN];
+  {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (int n = wv; n < N; n += 4) {
+      float t = 0.f;
+      for (int b = ln; b < nblk; b += 64) t += bsum[(size_t)n * nblk + b];
+      t = wave_sum(t);
+      if (ln == 0) inv_s[n] = 1.f / (t / (float)K + 1e-6f);
+    }
+  }
+  __syncthreads();
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= chunks) return;
+  const unsigned kc = (unsigned)(K >> 3);
+  const int k0 = (int)((unsigned long long)i % kc) * 8;
+  const s16x8 w = reinterpret_cast<const s16x8*>(W)[i];
+  const s16x8 gm = *reinterpret_cast<const s16x8*>(gamma + k0);
+  float wf[8], gf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { wf[j] = bf2f((u16)w[j]); gf[j] = bf2f((u16)gm[j]); }
+  for (int n = 0; n < N; ++n) {
+    const float4* gp = reinterpret_cast<const float4*>(gx + (size_t)n * K + k0);
+    const float4 g0 = gp[0], g1 = gp[1];
+    const float iv = inv_s[n];
+    const float nv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    s16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(wf[j] * (1.f + gf[j] * nv[j] * iv));
+    reinterpret_cast<s16x8*>(Wn)[(size_t)n * chunks + i] = o;
+  }
+}
+
+// W [O, K] bf16 (K % 8 == 0), gamma [K] bf16, stats = the ws of cgs_grn_stats(x, ws, N, HW, K, ...) -> Wn [N, O, K].
+CGS_EXPORT int cgs_grn_scale_weight(const void* W, const void* gamma, const float* ws, int N, int HW, int O, int K,
+                                    void* Wn, hipStream_t stream) {
+  if (N <= 0 || O <= 0) return 0;
+  if (K % 8 || N > GRN_MAXN || (((uintptr_t)W | (uintptr_t)gamma | (uintptr_t)Wn) & 15)) return (int)hipErrorInvalidValue;
+  const int S = cgs_grn_slices(N, HW, K);
+  const float* gx = ws + (size_t)N * S * K;
+  const int nblk = (K + 255) / 256;
+  const float* bsum = gx + (size_t)N * K;
+  const long long chunks = (long long)O * (K / 8);
+  grn_scale_weight_kernel<<<(unsigned)((chunks + 255) / 256), 256, 0, stream>>>(
+      (const u16*)W, (const u16*)gamma, gx, bsum, nblk, N, (u16*)Wn, chunks, K);
+  return (int)hipGetLastError();
+}
+
 // Per-(image, channel) affine on NHWC straight from a [N, ld] activation-dtype coefficient tensor:
 // y = x * (add + s[n][c]) + t[n][c] (Stable Cascade TimestepBlock x * (1 + a) + b with a, b the two
 // halves of the mapper GEMM output, comfy/ldm/cascade/common.py TimestepBlock) -- no fp32 cast /

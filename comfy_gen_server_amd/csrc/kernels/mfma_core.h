@@ -25,6 +25,7 @@ typedef __attribute__((address_space(3))) void mc_lds_void;
 #define MC_EPI_GEGLU 4
 #define MC_EPI_LNFOLD 8   // y = rstd_r * (acc - mean_r * cs[c]) + bias[c]  (LayerNorm folded into the GEMM)
 #define MC_EPI_F32OUT 16  // v7 only: C is fp32 (ldc in floats), no GEGLU / residual (attention scores, K22)
+#define MC_EPI_GELU 32    // GELU(acc * alpha + bias) before the residual (mc::tile, pq::run ACT, skinny; no GEGLU)
 
 namespace mc {
 
@@ -263,28 +264,36 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
       });
     });
   } else {
+    // plain / GELU (MC_EPI_GELU) forms as two straight-line paths: the flag is wave-uniform
+    auto plain = [&](auto act_c) {
+      constexpr bool ACT = decltype(act_c)::value;
 #pragma unroll
-    for (int j = 0; j < C::NJ; ++j) {
-      const int oc = 32 * j + ecol;
-      const int col = n0 + wn + oc;
-      const float bv = ((e.flags & MC_EPI_BIAS) && col < N) ? bf2f(e.bias[col]) : 0.f;
-      const float csl = (lnf && col < N) ? e.cs[col] : 0.f;
+      for (int j = 0; j < C::NJ; ++j) {
+        const int oc = 32 * j + ecol;
+        const int col = n0 + wn + oc;
+        const float bv = ((e.flags & MC_EPI_BIAS) && col < N) ? bf2f(e.bias[col]) : 0.f;
+        const float csl = (lnf && col < N) ? e.cs[col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < C::NI; ++i) {
-        const f32x16 t = acc[i][j];
+        for (int i = 0; i < C::NI; ++i) {
+          const f32x16 t = acc[i][j];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          int row = 32 * i + (r & 3) + 8 * (r >> 2) + erow;
-          float v = t[r] * e.alpha;
-          if (lnf) {
-            const float2 st = ln_row(row);
-            v = st.y * (t[r] - st.x * csl);
+          for (int r = 0; r < 16; ++r) {
+            int row = 32 * i + (r & 3) + 8 * (r >> 2) + erow;
+            float v = t[r] * e.alpha;
+            if (lnf) {
+              const float2 st = ln_row(row);
+              v = st.y * (t[r] - st.x * csl);
+            }
+            v += bv;
+            if constexpr (ACT) v = gelu_sig(v);
+            *reinterpret_cast<u16*>(region + row * pitch + 16 * ((oc >> 3) ^ (row & (CPR - 1))) + 2 * (oc & 7)) =
+                f2bf(v);
           }
-          *reinterpret_cast<u16*>(region + row * pitch + 16 * ((oc >> 3) ^ (row & (CPR - 1))) + 2 * (oc & 7)) =
-              f2bf(v + bv);
         }
       }
-    }
+    };
+    if (e.flags & MC_EPI_GELU) plain(std::true_type{});
+    else plain(std::false_type{});
   }
   // wave-local region: only this wave's LDS writes must land before its reads (lgkmcnt wait is
   // inserted by the compiler); then 16-B row-wise reads -> (+ residual) -> 16-B global stores.

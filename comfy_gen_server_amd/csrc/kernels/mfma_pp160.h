@@ -73,7 +73,8 @@ __device__ __forceinline__ int gg_row160(int r) {
 // blocks i / i + 1 hands every lane 4 (a, g) pairs (lower lanes: row block i, upper: i + 1). 160 weight
 // rows = 5 interleave groups = 80 output columns per tile (whole rounds where the 256-wide tiles leave a
 // partial one, e.g. SDXL batch 1: M = 2048, N = 10240 -> 512 tiles vs 320). Host: N % 160 == 0.
-template <class AL, bool LN = false, int DS = 0, bool GNS = false, bool GG = false>
+// ACT: GELU on (acc * alpha + bias) before the residual add (MC_EPI_GELU: Cascade's ChannelMLP Linear -> GELU).
+template <class AL, bool LN = false, int DS = 0, bool GNS = false, bool GG = false, bool ACT = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -257,6 +258,10 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     auto val = [&](int i, int j) {
       float v0 = acc[i][j][0] * e.alpha + bv[j].x, v1 = acc[i][j][1] * e.alpha + bv[j].y;
       float v2 = acc[i][j][2] * e.alpha + bv[j].z, v3 = acc[i][j][3] * e.alpha + bv[j].w;
+      if constexpr (ACT) {
+        const f32x2_t g01 = gelu_sig2(f32x2_t{v0, v1}), g23 = gelu_sig2(f32x2_t{v2, v3});
+        v0 = g01.x; v1 = g01.y; v2 = g23.x; v3 = g23.y;
+      }
       if (HR) {
         const float4 rv = unpack4_bf16(rw[i][j]);
         v0 += rv.x; v1 += rv.y; v2 += rv.z; v3 += rv.w;

@@ -100,18 +100,29 @@ class Linear(nn.Module, DerivedMixin, CastWeightBiasOp):
         else:
             self.register_parameter("bias", None)
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, act=None):
+        """``act="gelu"``: GELU fused into the GEMM epilogue (before the residual)."""
         if _hooked(self):
             w, b = cast_bias_weight(self, x)
-            return ops.linear(x, w, b, residual=residual)
+            return ops.linear(x, w, b, residual=residual, act=act)
         w, b = self.weight, self.bias
         if w.dtype == torch.float8_e4m3fn and w.device == x.device and x.dtype == torch.bfloat16 and x.is_cuda:
             # fp8-stored weights go to the fp8-weight GEMM as they are (widened inside the kernel)
-            return ops.linear(x, w, None if b is None else b.to(dtype=x.dtype), residual=residual)
+            return ops.linear(x, w, None if b is None else b.to(dtype=x.dtype), residual=residual, act=act)
         if w.dtype != x.dtype or w.device != x.device:  # manual cast (comfy/ops.py:22-32)
             w = w.to(device=x.device, dtype=x.dtype)
             b = None if b is None else b.to(device=x.device, dtype=x.dtype)
-        return ops.linear(x, w, b, residual=residual)
+        return ops.linear(x, w, b, residual=residual, act=act)
+
+    def weight_bias_for(self, x):
+        """(weight, bias) as the forward would use them for ``x`` (hooks applied, cast to x's dtype)."""
+        if _hooked(self):
+            return cast_bias_weight(self, x)
+        w, b = self.weight, self.bias
+        if w.dtype != x.dtype or w.device != x.device:
+            w = w.to(device=x.device, dtype=x.dtype)
+            b = None if b is None else b.to(device=x.device, dtype=x.dtype)
+        return w, b
 
 
 class Conv2d(nn.Module, DerivedMixin, CastWeightBiasOp):

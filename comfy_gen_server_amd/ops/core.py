@@ -24,6 +24,7 @@ EPI_BIAS = 1
 EPI_RESIDUAL = 2
 EPI_GEGLU = 4
 EPI_SILU_IN = 8   # reserved
+EPI_GELU = 32     # GELU(acc + bias) before the residual (v6 ACT kernel, mc::tile family, skinny)
 
 # hipBLASLt (through ATen) as a GEMM autotune candidate: off unless explicitly requested -- the
 # hand-written MFMA kernels (v5/v6/v7) are the device GEMMs; profiles/r02_gemm_table_v7.md has the
@@ -70,13 +71,19 @@ def _v7_ws(M: int, N: int, K: int, device):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
-           residual: torch.Tensor | None = None) -> torch.Tensor:
-    """y = x @ weight^T (+ bias) (+ residual). ``residual`` has y's shape (fused epilogue add).
+           residual: torch.Tensor | None = None, act: str | None = None,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """y = act(x @ weight^T (+ bias)) (+ residual). ``residual`` has y's shape (fused epilogue add);
+    ``act="gelu"`` fuses the GELU into the epilogue (Cascade ChannelMLP Linear -> GELU); ``out``: a
+    contiguous [rows, N] destination for the device path (e.g. one image's slice of a batch).
 
     Device path: the HIP GEMM family (v7 persistent ping-pong 256x256x64 with a register epilogue,
     v6 persistent 256x160, v5 ping-pong 256x256, v3 8-wave 32x32 MFMA, v1 128x128), the kernel picked
     per shape by ``ops.autotune`` (hipBLASLt joins the candidates only with ``CGS_GEMM_LIB=1``)."""
+    assert act in (None, "gelu"), act
     if weight.dtype == torch.float8_e4m3fn:
+        if act is not None:
+            return linear(x, weight.to(x.dtype), None if bias is None else bias.to(x.dtype), residual, act, out)
         return _linear_w8(x, weight, bias, residual)
     be = backend_for("gemm", x, "cgs_gemm_bf16")
     # K % 8: the kernels' 16-byte row loads (a K=2 coordinate MLP is not GEMM-shaped work anyway)
@@ -96,20 +103,26 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             r = residual.reshape(M, N)
             if not r.is_contiguous():
                 r = r.contiguous()
+        gelu = act == "gelu"
+        if gelu:
+            epi |= EPI_GELU
         w = weight if weight.is_contiguous() else weight.contiguous()
+        dst = out
+        if dst is not None:
+            assert dst.is_contiguous() and dst.numel() == M * N and dst.dtype == x.dtype, "out: contiguous [M, N]"
 
         def run_hip(variant):
-            out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+            o = dst if dst is not None else torch.empty((M, N), device=x.device, dtype=x.dtype)
             ws = _v7_ws(M, N, K, x.device) if variant == 7 else None
             if ws is not None:
-                _check(_lib().cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
+                _check(_lib().cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),
                                                  M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
                                                  ws.data_ptr(), ws.numel(), _stream()), "cgs_gemm_bf16_v7ws")
-                return out
-            _check(_lib().cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), _ptr(bias), _ptr(r),
+                return o
+            _check(_lib().cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),
                                           M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
                                           variant, _stream()), "cgs_gemm_bf16")
-            return out
+            return o
 
         def run_lib():
             y = F.linear(a, w, bias)
@@ -121,19 +134,23 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         if M * N * K >= (1 << 27) and (M > 128 or K % 32):
             cands = []
             if K % 64 == 0 and N % 8 == 0:
-                if K >= 128:
+                if K >= 128 and not gelu:
                     cands.append(("v7", lambda: run_hip(7)))
-                cands.append(("v5", lambda: run_hip(5)))
-                cands.append(("v6", lambda: run_hip(6)))
+                if not gelu:
+                    cands.append(("v5", lambda: run_hip(5)))
+                if K >= 128 or not gelu:
+                    cands.append(("v6", lambda: run_hip(6)))
             if K % 32 == 0 and N % 8 == 0:
                 cands.append(("v4", lambda: run_hip(4)))
                 cands.append(("v8", lambda: run_hip(8)))      # 128 x 128 tiles (short M / N grids)
                 if _underfilled(M, N):    # 64x128 / 128x64 tiles, 4- and 6-stage rings (batch-1 grids)
                     cands += [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
             cands.append(("hip", lambda: run_hip(-1)))
-            if _LIB_GEMM:     # vendor GEMM only as an explicit opt-in (CGS_GEMM_LIB=1)
+            if _LIB_GEMM and not gelu and dst is None:     # vendor GEMM only as an explicit opt-in
                 cands.append(("lib", run_lib))
             choice = autotune.choose(("gemm", M, N, K, epi), cands, default="hip")
+        if choice == "lib" and (gelu or dst is not None):
+            choice = "hip"
         if choice == "lib":
             count("gemm", "lib")     # explicit opt-in (CGS_GEMM_LIB=1)
             return run_lib().view(*x.shape[:-1], N)
@@ -146,12 +163,20 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         vendor_fallback("gemm", f"dtype {x.dtype}/{weight.dtype}, K={x.shape[-1]}")
     if be == "torch":
         y = F.linear(x.float(), weight.float(), None if bias is None else bias.float())
+        if act == "gelu":
+            y = F.gelu(y)
         if residual is not None:
             y = y + residual.float()
-        return y.to(x.dtype)
-    y = F.linear(x, weight, bias)
-    if residual is not None:
-        y = y + residual
+        y = y.to(x.dtype)
+    else:
+        y = F.linear(x, weight, bias)
+        if act == "gelu":
+            y = F.gelu(y)
+        if residual is not None:
+            y = y + residual
+    if out is not None:
+        out.view(y.shape).copy_(y)
+        return out.view(y.shape)
     return y
 
 
@@ -1410,6 +1435,36 @@ def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, pre_gelu:
     nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
     scale = (1.0 + gamma.float().reshape(1, 1, 1, C) * nx).to(x.dtype)
     return torch.addcmul(beta.to(x.dtype).reshape(1, 1, 1, C), x, scale)
+
+
+def grn_fold_weight(h: torch.Tensor, weight: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
+    """The GlobalResponseNorm over ``h`` [N, H, W, K] (already GELU'd) folded into the next Linear's
+    weight [O, K]: returns per-image weights Wn [N, O, K] = W * (1 + gamma * nx_n), nx_n =
+    ||h_n||_HW / mean_K ||h_n||_HW, so that GRN(h) W^T = h_n Wn[n]^T + W beta per image (K28 fused with
+    the ChannelMLP's second GEMM, Cascade ``common.py:77-87``). Cheaper than rewriting h whenever O < H * W.
+    Device path: the GRN statistics passes + one weight-scaling pass (W read once for all images)."""
+    N, H, W_, K = h.shape
+    O = weight.shape[0]
+    be = backend_for("grn", h, "cgs_grn_scale_weight")
+    if (be == "hip" and h.dtype == torch.bfloat16 and weight.dtype == h.dtype and K % 8 == 0 and N <= 64
+            and weight.shape[1] == K):
+        count("grn", "hip")
+        hc = h.contiguous()
+        S = int(_lib().cgs_grn_slices(N, H * W_, K))
+        ws = torch.empty(N * ((S + 1) * K + (K + 255) // 256), device=h.device, dtype=torch.float32)
+        _check(_lib().cgs_grn_stats(hc.data_ptr(), ws.data_ptr(), N, H * W_, K, 0, _DT[h.dtype], _stream()),
+               "cgs_grn_stats")
+        wc = weight.contiguous()
+        g = gamma.to(h.dtype).reshape(-1).contiguous()
+        out = torch.empty((N, O, K), device=h.device, dtype=h.dtype)
+        _check(_lib().cgs_grn_scale_weight(wc.data_ptr(), g.data_ptr(), ws.data_ptr(), N, H * W_, O, K,
+                                           out.data_ptr(), _stream()), "cgs_grn_scale_weight")
+        return out
+    count("grn", "torch")
+    gx = torch.linalg.vector_norm(h.float(), dim=(1, 2))                        # [N, K]
+    nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
+    s = 1.0 + gamma.float().reshape(1, K) * nx
+    return (weight.float()[None] * s[:, None, :]).to(weight.dtype)
 
 
 def softmax_rows(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:

@@ -1022,3 +1022,53 @@ def test_gemm_geglu_v6(cuda, M, N2, K, ln):
     x1, g = h.chunk(2, dim=-1)
     ref = x1 * F.gelu(g)
     assert _rel(y, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("M,N,K,variant", [(1000, 320, 128, 6), (4096, 1280, 320, 6), (1152, 8192, 256, 8),
+                                           (300, 640, 96, 10), (64, 512, 256, -1), (2048, 256, 512, 4),
+                                           (577, 264, 64, 14)])
+@pytest.mark.parametrize("res", [False, True])
+def test_gemm_gelu_epilogue(cuda, M, N, K, variant, res):
+    """EPI_GELU: out = gelu(A W^T + b) (+ R) in the v6 ACT kernel, the mc::tile family and skinny."""
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16)
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if res else None
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    epi = core.EPI_BIAS | core.EPI_GELU | (core.EPI_RESIDUAL if res else 0)
+    rc = _native.load_kernels().cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(),
+                                                 None if r is None else r.data_ptr(), M, N, K, K, K, N,
+                                                 N if res else 0, epi, 1.0, variant, core._stream())
+    assert rc == 0
+    ref = F.gelu(a.float() @ w.float().t() + b.float()) + (r.float() if res else 0.0)
+    assert _rel(out, ref) < 1e-2
+    # the op-level entry point (autotuned kernel choice) agrees
+    y = ops.linear(a, w, b, residual=r, act="gelu")
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,c", [(2, 16, 16, 64), (2, 6, 6, 64), (1, 32, 24, 128)])
+def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c):
+    """Cascade ChannelMLP on the device -- GELU epilogue, then the GRN either as a pass over h (H W <= c)
+    or folded into per-image second-GEMM weights (H W > c) -- vs the fp32 NCHW reference math."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    torch.manual_seed(6)
+    m = SC._ChannelMLP(c, 4 * c, c)
+    init_random_(m, seed=3)
+    with torch.no_grad():
+        m[2].gamma.normal_(0, 0.5)
+        m[2].beta.normal_(0, 0.5)
+    x = torch.randn(N, H, W, c)
+    res = torch.randn(N, H, W, c)
+    h = F.gelu(F.linear(x, m[0].weight, m[0].bias))
+    gx = torch.norm(h, p=2, dim=(1, 2), keepdim=True)
+    nx = gx / (gx.mean(dim=-1, keepdim=True) + 1e-6)
+    h = m[2].gamma * (h * nx) + m[2].beta + h
+    ref = F.linear(h, m[4].weight, m[4].bias) + res
+    g = m.to(device=cuda, dtype=torch.bfloat16)
+    with torch.no_grad():
+        y = g(x.to(cuda, torch.bfloat16), residual=res.to(cuda, torch.bfloat16))
+    assert ops.stats().get(("grn", "hip"), 0) == 1 and ops.stats().get(("gemm", "hip"), 0) >= 2
+    assert _rel(y.cpu(), ref) < 2e-2
