@@ -604,10 +604,14 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
   const int ds = v6_ds();
-  if (epi & EPI_GELU) {    // GELU epilogue: plain (no GEGLU / LayerNorm fold) form only
-    if (epi & (EPI_GEGLU | EPI_LNFOLD)) return (int)hipErrorInvalidValue;
-    gemm_v6_go<false, 1, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n,
-                                      stream, rs, cs);
+  if (epi & EPI_GELU) {    // GELU epilogue: plain or LayerNorm-folded form (no GEGLU)
+    if (epi & EPI_GEGLU) return (int)hipErrorInvalidValue;
+    if (epi & EPI_LNFOLD)
+      gemm_v6_go<true, 1, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m,
+                                       tiles_n, stream, rs, cs);
+    else
+      gemm_v6_go<false, 1, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m,
+                                        tiles_n, stream, rs, cs);
     return (int)hipGetLastError();
   }
   if (epi & EPI_GEGLU) {   // GEGLU epilogue (pq::run GG): split-DMA main loop, N % 160 == 0 (host-checked)
@@ -946,6 +950,13 @@ static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, 
       ((uintptr_t)rs % 8) || (long long)M * lda * 2 >= (1ll << 32) || (long long)N * ldw * 2 >= (1ll << 32))
     return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
+  if (epi & EPI_GELU) {    // LayerNorm -> Linear -> GELU (Cascade ChannelMLP): v6 ACT or the mc::tile kernels
+    if ((epi & EPI_GEGLU) || variant == 7) return (int)hipErrorInvalidValue;
+    if (variant == 6 || (variant < 0 && N % 160 == 0))
+      return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
+    return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream,
+                          variant < 0 ? 8 : variant, rs, cs);
+  }
   // v6 (256x160) for the N = 640 / 1280 projections (the cross-attention query), v7 otherwise
   if (variant == 8 || (variant >= 10 && variant <= 14))
     return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, variant,

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from . import layers
 from .layers import Conv2d, DerivedMixin, LayerNorm, Linear, module_epoch
 
 
@@ -101,12 +102,31 @@ class _ChannelMLP(nn.Sequential):
         if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
             h = ops.grn_nhwc(self[0](x), _cast(grn.gamma, x), _cast(grn.beta, x), pre_gelu=True)
             return self[4](h, residual=residual)
-        # device: GELU in the first GEMM's epilogue; then either the GRN pass over h, or -- when the output
-        # width is below the pixel count, i.e. rewriting W2 per image moves fewer bytes than rewriting h
-        # (Stage B's 64^2..256^2 levels) -- the GRN scale folded into per-image copies of W2 and
-        # W2 beta folded into the bias (ops.grn_fold_weight)
+        return self._grn_linear2(self[0](x, act="gelu"), x, residual)
+
+    def lnfold_ok(self, x) -> bool:
+        """LayerNorm (no affine) of ``x`` can fold into the first GEMM (device bf16, unhooked weights)."""
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not layers._hooked(self[0])
+                and self[0].weight.dtype == torch.bfloat16 and ops.lnfold_available(x, x.shape[-1]))
+
+    def forward_ln(self, x, eps=1e-6, residual=None):
+        """``forward(LN(x))`` with the LayerNorm folded into the first GEMM: only the per-pixel statistics
+        pass reads ``x``; the normalised tensor is never written (K07 as in the SDXL transformer)."""
+        if not self.lnfold_ok(x):
+            return self(_ln(x, eps), residual=residual)
+        lin1 = self[0]
+        w2, cs, b2 = lin1._derived_get(("lnfold_noaffine", x.device), lambda: ops.lnfold_weights(
+            _cast(lin1.weight, x), _cast(lin1.bias, x), None, None))
+        h = ops.linear_lnfold(x, ops.layernorm_stats(x, eps), w2, cs, b2, act="gelu")
+        return self._grn_linear2(h, x, residual)
+
+    def _grn_linear2(self, h, x, residual):
+        # device: GELU already in the first GEMM's epilogue; then either the GRN pass over h, or -- when the
+        # output width is below the pixel count, i.e. rewriting W2 per image moves fewer bytes than
+        # rewriting h (Stage B's 64^2..256^2 levels) -- the GRN scale folded into per-image copies of W2
+        # and W2 beta folded into the bias (ops.grn_fold_weight)
+        grn = self[2]
         N, H, W, _ = x.shape
-        h = self[0](x, act="gelu")
         lin2 = self[4]
         if lin2.out_features < H * W and N <= 64 and h.shape[-1] % 8 == 0:
             w2, b2 = lin2.weight_bias_for(h)
@@ -130,9 +150,10 @@ class ResBlock(nn.Module):
         self.channelwise = _ChannelMLP(c + c_skip, c * 4, c, dtype=dtype, device=device)
 
     def forward(self, x, x_skip=None):
-        h = _ln(self.depthwise.forward_nhwc(x))
-        if x_skip is not None:
-            h = torch.cat([h, x_skip.to(h.dtype)], dim=-1)
+        d = self.depthwise.forward_nhwc(x)
+        if x_skip is None:
+            return self.channelwise.forward_ln(d, residual=x)
+        h = torch.cat([_ln(d), x_skip.to(d.dtype)], dim=-1)
         return self.channelwise(h, residual=x)
 
 
@@ -208,7 +229,7 @@ class FeedForwardBlock(nn.Module):
         self.channelwise = _ChannelMLP(c, c * 4, c, dtype=dtype, device=device)
 
     def forward(self, x):
-        return self.channelwise(_ln(x), residual=x)
+        return self.channelwise.forward_ln(x, residual=x)
 
 
 class TimestepBlock(nn.Module):

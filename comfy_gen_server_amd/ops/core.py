@@ -1174,10 +1174,11 @@ def lnfold_weights(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch
 
 
 def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch.Tensor, b2: torch.Tensor,
-                  geglu: bool = False) -> torch.Tensor:
+                  geglu: bool = False, act: str | None = None) -> torch.Tensor:
     """``LN(x) @ W^T + b`` (or the GEGLU of it, with interleaved W' rows) from the raw rows ``x``, the
     row statistics ``rs`` and ``lnfold_weights`` -- the LayerNorm never materialises (K07 folded
-    into the GEMM epilogue of the v7 kernel)."""
+    into the GEMM epilogue of the v7 kernel). ``act="gelu"``: GELU of it (Cascade's LayerNorm ->
+    ChannelMLP Linear -> GELU), on the v6 ACT / mc::tile kernels."""
     K = x.shape[-1]
     a = x.reshape(-1, K)
     if not a.is_contiguous():
@@ -1186,6 +1187,23 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
     nout = N // 2 if geglu else N
     epi = EPI_BIAS | (EPI_GEGLU if geglu else 0)
     count("gemm_geglu" if geglu else "gemm", "hip")
+    if act == "gelu":
+        assert not geglu
+        epi |= EPI_GELU
+
+        def run_g(variant):
+            out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+            _check(_lib().cgs_gemm_bf16_lnfold_v(a.data_ptr(), w2.data_ptr(), out.data_ptr(), b2.data_ptr(),
+                                                 rs.data_ptr(), cs.data_ptr(), M, N, K, K, K, N, epi, None, 0,
+                                                 variant, _stream()), "cgs_gemm_bf16_lnfold_v")
+            return out
+        cands = [("v8", lambda: run_g(8))]
+        if N % 160 == 0:
+            cands.append(("v6", lambda: run_g(6)))
+        if _underfilled(M, N):
+            cands += [(f"v{v}", (lambda v=v: run_g(v))) for v in _SMALL_TILE]
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v6" if N % 160 == 0 else "v8")
+        return run_g({"v6": 6, "v8": 8, **_SMALL_NAMES}.get(choice, -1)).view(*x.shape[:-1], N)
 
     def run(variant):
         out = torch.empty((M, nout), device=x.device, dtype=x.dtype)

@@ -1072,3 +1072,26 @@ def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c):
         y = g(x.to(cuda, torch.bfloat16), residual=res.to(cuda, torch.bfloat16))
     assert ops.stats().get(("grn", "hip"), 0) == 1 and ops.stats().get(("gemm", "hip"), 0) >= 2
     assert _rel(y.cpu(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W,c", [(2, 16, 16, 128), (2, 6, 6, 128), (1, 8, 8, 256)])
+def test_cascade_resblock_lnfold(cuda, N, H, W, c):
+    """Cascade ResBlock / FeedForwardBlock on the device: LayerNorm folded into the first GEMM together with
+    the GELU epilogue (ops.linear_lnfold act="gelu"), GRN pass or GRN weight fold, vs the fp32 CPU blocks."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    torch.manual_seed(7)
+    for blk in (SC.ResBlock(c), SC.FeedForwardBlock(c)):
+        init_random_(blk, seed=4)
+        grn = blk.channelwise[2]
+        with torch.no_grad():
+            grn.gamma.normal_(0, 0.5)
+            grn.beta.normal_(0, 0.5)
+        x = torch.randn(N, H, W, c)
+        with torch.no_grad():
+            ref = blk(x)
+            g = blk.to(device=cuda, dtype=torch.bfloat16)
+            ops.reset_stats()
+            y = g(x.to(cuda, torch.bfloat16)).float().cpu()
+        assert ops.stats().get(("layernorm", "hip"), 0) == 1          # the statistics pass only
+        assert _rel(y, ref) < 2e-2
