@@ -111,6 +111,8 @@ KERNEL_SIGNATURES = {
     "cgs_upsample_nearest2x_nhwc": [_P, _P, _I, _I, _I, _I, _I, _P],
     # depthwise conv NHWC: x, w[k*k, C], bias, y, N, H, W, C, k, replicate, dtype, stream
     "cgs_dwconv_nhwc": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    # the same + per-pixel LayerNorm (mean, rstd) over C: x, w, bias, y, rs, N, H, W, C, k, replicate, eps, dtype
+    "cgs_dwconv_ln_stats_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _I, _P],
     # conv implicit GEMM NHWC bf16: x[N,H,W,Cin], w[Cout,kh,kw,Cin], bias, residual, out
     "cgs_conv2d_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     # image / utility kernels (csrc/kernels/image.hip)

@@ -469,6 +469,118 @@ CGS_EXPORT int cgs_layernorm(const void* x, void* y, const void* w, const void* 
   return (int)hipGetLastError();
 }
 
+// Depthwise k x k conv (stride 1, 'same' zeros / replicate padding) on NHWC with the LayerNorm statistics
+// of every output pixel over C in the same pass (Stable Cascade ResBlock: depthwise -> LayerNorm2d ->
+// ChannelMLP, common.py ResBlock): LPR lanes per pixel, each lane keeps its <= LN_MAXK 8-channel output
+// chunks in registers (rounded to the output dtype, i.e. the values the next GEMM reads), writes them and
+// forms (mean, rstd) by an exact two-pass over the registers -> rs [pixels, 2] (cgs_layernorm_stats layout).
+// The folded-LayerNorm GEMM (MC_EPI_LNFOLD) then needs no separate statistics pass over the tensor.
+template <int DT, int KF, int LPR>
+__global__ __launch_bounds__(256) void dwconv_ln_stats_kernel(const u16* __restrict__ x, const u16* __restrict__ wt,
+                                                              const u16* __restrict__ b, u16* __restrict__ y,
+                                                              float* __restrict__ rs, int N, int H, int W, int C,
+                                                              int kr, int replicate, float eps) {
+  constexpr int RPB = 256 / LPR;
+  const int lane = threadIdx.x % LPR;
+  const unsigned npix = (unsigned)N * H * W;
+  const unsigned pix = blockIdx.x * RPB + threadIdx.x / LPR;
+  const bool live = pix < npix;
+  const unsigned pp = live ? pix : 0u;
+  const int wo = (int)(pp % (unsigned)W);
+  const unsigned t = pp / (unsigned)W;
+  const int ho = (int)(t % (unsigned)H);
+  const int n = (int)(t / (unsigned)H);
+  const int nch = C >> 3;
+  const int k = KF ? KF : kr;
+  const int p = k >> 1;
+  float v[LN_MAXK][8];
+  float s = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < LN_MAXK; ++kk) {
+    const int ch = lane + LPR * kk;
+    if (live && ch < nch) {
+      float acc[8];
+      if (b) {
+        const s16x8 bv = reinterpret_cast<const s16x8*>(b)[ch];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = cvt_in<DT>((u16)bv[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      }
+#pragma unroll
+      for (int di = 0; di < (KF ? KF : 15); ++di) {
+        if (!KF && di >= k) break;
+        int hi = ho + di - p;
+        if (replicate) hi = min(max(hi, 0), H - 1);
+        else if (hi < 0 || hi >= H) continue;
+#pragma unroll
+        for (int dj = 0; dj < (KF ? KF : 15); ++dj) {
+          if (!KF && dj >= k) break;
+          int wi = wo + dj - p;
+          if (replicate) wi = min(max(wi, 0), W - 1);
+          else if (wi < 0 || wi >= W) continue;
+          const s16x8 xv = *reinterpret_cast<const s16x8*>(x + (((size_t)n * H + hi) * W + wi) * C + ch * 8);
+          const s16x8 wv = *reinterpret_cast<const s16x8*>(wt + (size_t)(di * k + dj) * C + ch * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += cvt_in<DT>((u16)xv[j]) * cvt_in<DT>((u16)wv[j]);
+        }
+      }
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (short)cvt_out<DT>(acc[j]);
+        v[kk][j] = cvt_in<DT>((u16)o[j]);
+        s += v[kk][j];
+      }
+      *reinterpret_cast<s16x8*>(y + (size_t)pix * C + ch * 8) = o;
+    }
+  }
+  const float mean = group_sum<LPR>(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < LN_MAXK; ++kk) {
+    const int ch = lane + LPR * kk;
+    if (live && ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[kk][j] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(group_sum<LPR>(q) / C + eps);
+  if (live && lane == 0) reinterpret_cast<float2*>(rs)[pix] = float2{mean, rstd};
+}
+
+CGS_EXPORT int cgs_dwconv_ln_stats_nhwc(const void* x, const void* wt, const void* b, void* y, float* rs, int N, int H,
+                                        int W, int C, int k, int replicate, float eps, int dtype, hipStream_t stream) {
+  if (C % 8 || C / 8 > 32 * LN_MAXK || (k & 1) == 0 || k > 15 || dtype == CGS_F32) return (int)hipErrorInvalidValue;
+  const long long npix = (long long)N * H * W;
+  if (npix <= 0) return 0;
+  if (npix * C >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  const int nch = C / 8;
+  const int L = nch <= 8 * LN_MAXK ? 8 : (nch <= 16 * LN_MAXK ? 16 : 32);
+#define CGS_DWL(DTV, KV, LPRV)                                                                                     \
+  dwconv_ln_stats_kernel<DTV, KV, LPRV><<<(unsigned)((npix + 256 / LPRV - 1) / (256 / LPRV)), 256, 0, stream>>>( \
+      (const u16*)x, (const u16*)wt, (const u16*)b, (u16*)y, rs, N, H, W, C, k, replicate, eps)
+#define CGS_DWL_K(DTV, LPRV)                                          \
+  do {                                                                \
+    if (k == 3) CGS_DWL(DTV, 3, LPRV);                                \
+    else if (k == 7) CGS_DWL(DTV, 7, LPRV);                           \
+    else CGS_DWL(DTV, 0, LPRV);                                       \
+  } while (0)
+#define CGS_DWL_L(DTV)                                                \
+  do {                                                                \
+    if (L == 8) CGS_DWL_K(DTV, 8);                                    \
+    else if (L == 16) CGS_DWL_K(DTV, 16);                             \
+    else CGS_DWL_K(DTV, 32);                                          \
+  } while (0)
+  if (dtype == CGS_BF16) CGS_DWL_L(CGS_BF16);
+  else CGS_DWL_L(CGS_F16);
+#undef CGS_DWL_L
+#undef CGS_DWL_K
+#undef CGS_DWL
+  return (int)hipGetLastError();
+}
+
 // (mean, rstd) per row of x [rows, C] (C % 8 == 0, C <= the register-resident LayerNorm limit)
 CGS_EXPORT int cgs_layernorm_stats(const void* x, float* rs, int rows, int C, float eps, int dtype, hipStream_t stream) {
   if (rows <= 0) return 0;

@@ -109,15 +109,18 @@ class _ChannelMLP(nn.Sequential):
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not layers._hooked(self[0])
                 and self[0].weight.dtype == torch.bfloat16 and ops.lnfold_available(x, x.shape[-1]))
 
-    def forward_ln(self, x, eps=1e-6, residual=None):
+    def forward_ln(self, x, eps=1e-6, residual=None, rs=None):
         """``forward(LN(x))`` with the LayerNorm folded into the first GEMM: only the per-pixel statistics
-        pass reads ``x``; the normalised tensor is never written (K07 as in the SDXL transformer)."""
+        pass reads ``x`` (or none: ``rs`` from the producer, ops.depthwise_conv2d_nhwc_lnstats); the
+        normalised tensor is never written (K07 as in the SDXL transformer)."""
         if not self.lnfold_ok(x):
             return self(_ln(x, eps), residual=residual)
         lin1 = self[0]
         w2, cs, b2 = lin1._derived_get(("lnfold_noaffine", x.device), lambda: ops.lnfold_weights(
             _cast(lin1.weight, x), _cast(lin1.bias, x), None, None))
-        h = ops.linear_lnfold(x, ops.layernorm_stats(x, eps), w2, cs, b2, act="gelu")
+        if rs is None:
+            rs = ops.layernorm_stats(x, eps)
+        h = ops.linear_lnfold(x, rs, w2, cs, b2, act="gelu")
         return self._grn_linear2(h, x, residual)
 
     def _grn_linear2(self, h, x, residual):
@@ -150,6 +153,12 @@ class ResBlock(nn.Module):
         self.channelwise = _ChannelMLP(c + c_skip, c * 4, c, dtype=dtype, device=device)
 
     def forward(self, x, x_skip=None):
+        if x_skip is None and self.channelwise.lnfold_ok(x):
+            # depthwise conv + LayerNorm statistics in one pass, LayerNorm folded into the first GEMM
+            dw = self.depthwise
+            d, rs = ops.depthwise_conv2d_nhwc_lnstats(x, dw.w_kkc(x), _cast(dw.bias, x), dw.kernel_size[0], 1e-6,
+                                                      dw.replicate)
+            return self.channelwise.forward_ln(d, residual=x, rs=rs)
         d = self.depthwise.forward_nhwc(x)
         if x_skip is None:
             return self.channelwise.forward_ln(d, residual=x)

@@ -18,6 +18,7 @@ from .core import (  # noqa: F401
     linear, linear_geglu, attention, attention_lse, attention_kv2, attention_bias, group_norm, layer_norm, conv2d,
     conv_transpose2d, conv_transpose_phase_weights, silu, gelu,
     upsample_nearest2x, timestep_embedding, cfg_combine, euler_step, depthwise_conv2d_nhwc,
+    depthwise_conv2d_nhwc_lnstats,
     interpolate, fused_bias_act, channel_affine_nhwc, upfirdn2d, upfirdn2d_reference, vq_nearest, grn_nhwc,
     grn_fold_weight, softmax_rows,
     attention_with_probs, philox_randn, euler_ancestral_philox, brownian_increment, step_param, sampler_step_dev,

@@ -900,6 +900,29 @@ def depthwise_conv2d_nhwc(x: torch.Tensor, w_kkc: torch.Tensor, bias: torch.Tens
     return y.permute(0, 2, 3, 1).contiguous()
 
 
+def depthwise_conv2d_nhwc_lnstats(x: torch.Tensor, w_kkc: torch.Tensor, bias: torch.Tensor | None, k: int,
+                                  eps: float, replicate: bool = False):
+    """``(y, rs)``: the depthwise conv of ``depthwise_conv2d_nhwc`` plus the per-pixel LayerNorm statistics
+    of y over C (float32 [pixels, 2] (mean, rstd), the ``layernorm_stats`` layout) from the same pass --
+    the Cascade ResBlock's depthwise -> LayerNorm2d feeding a LayerNorm-folded GEMM (no second read of y)."""
+    N, H, W, C = x.shape
+    be = backend_for("dwconv", x, "cgs_dwconv_ln_stats_nhwc")
+    if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0 and C <= 2048 and k % 2 == 1:
+        count("dwconv", "hip")
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        rs = torch.empty((N * H * W, 2), device=x.device, dtype=torch.float32)
+        _check(_lib().cgs_dwconv_ln_stats_nhwc(xc.data_ptr(), w_kkc.contiguous().data_ptr(), _ptr(bias), y.data_ptr(),
+                                               rs.data_ptr(), N, H, W, C, k, int(replicate), float(eps),
+                                               _DT[x.dtype], _stream()), "cgs_dwconv_ln_stats_nhwc")
+        return y, rs
+    y = depthwise_conv2d_nhwc(x, w_kkc, bias, k, replicate)
+    yf = y.float().reshape(-1, C)
+    mean = yf.mean(dim=1)
+    rstd = torch.rsqrt(yf.var(dim=1, unbiased=False) + eps)
+    return y, torch.stack([mean, rstd], dim=1)
+
+
 # ----------------------------------------------------------------------------------------------
 # Elementwise
 # ----------------------------------------------------------------------------------------------

@@ -1093,5 +1093,26 @@ def test_cascade_resblock_lnfold(cuda, N, H, W, c):
             g = blk.to(device=cuda, dtype=torch.bfloat16)
             ops.reset_stats()
             y = g(x.to(cuda, torch.bfloat16)).float().cpu()
-        assert ops.stats().get(("layernorm", "hip"), 0) == 1          # the statistics pass only
+        # ResBlock: the statistics come out of the depthwise kernel; FeedForwardBlock: one statistics pass
+        assert ops.stats().get(("layernorm", "hip"), 0) == (0 if isinstance(blk, SC.ResBlock) else 1)
         assert _rel(y, ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W,C,k,rep", [(2, 24, 24, 2048, 3, False), (1, 17, 9, 320, 3, False),
+                                           (2, 8, 8, 1280, 7, True), (1, 5, 6, 64, 3, False)])
+def test_dwconv_ln_stats(cuda, N, H, W, C, k, rep):
+    """Depthwise conv with the per-pixel LayerNorm statistics of its (rounded) output in the same pass."""
+    torch.manual_seed(8)
+    x = (torch.randn(N, H, W, C, device=cuda) + 0.5).to(torch.bfloat16)
+    w = (torch.randn(k * k, C, device=cuda) / k).to(torch.bfloat16)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16)
+    y, rs = ops.depthwise_conv2d_nhwc_lnstats(x, w, b, k, 1e-6, rep)
+    xn = x.float().permute(0, 3, 1, 2)
+    if rep:
+        xn = F.pad(xn, (k // 2,) * 4, mode="replicate")
+    ref = F.conv2d(xn, w.float().t().reshape(C, 1, k, k), b.float(), 1, 0 if rep else k // 2, 1, C).permute(0, 2, 3, 1)
+    assert ops.stats().get(("dwconv", "hip"), 0) == 1
+    assert _rel(y, ref) < 1e-2
+    yf = y.float().reshape(-1, C)                   # statistics of the stored bf16 values
+    assert torch.allclose(rs[:, 0], yf.mean(1), atol=1e-3, rtol=1e-3)
+    assert torch.allclose(rs[:, 1], torch.rsqrt(yf.var(1, unbiased=False) + 1e-6), rtol=2e-3)
