@@ -38,6 +38,7 @@ from multiprocessing.connection import Client, Listener
 SAMPLER_TYPES = ("KSampler", "KSamplerAdvanced")
 GC_INTERVAL_S = 10.0          # the reference worker's model cleanup + GC cadence (main.py:139-146)
 MAX_RETRIES = 1               # re-runs of a prompt whose rank died under it
+SPMD_REPORT_TIMEOUT_S = 30.0  # rank 0 waits this long for the workers' reports of a finished SPMD prompt
 
 
 def _housekeeping():
@@ -237,7 +238,7 @@ def worker_main(comm, address, authkey: bytes):
             ex_single.execute(m["prompt"], pid, extra, m["outputs"])
             ex = ex_single
         need_gc = True
-        send_msg(conn, {"op": "done", "prompt_id": pid, "rank": comm.rank, "success": ex.success,
+        send_msg(conn, {"op": "done", "prompt_id": pid, "mode": m["mode"], "rank": comm.rank, "success": ex.success,
                         "messages": ex.status_messages, "outputs_ui": ex.outputs_ui,
                         "seconds": time.perf_counter() - t0, "images_sampled": ctx.images_sampled - n0,
                         "comm_bytes": comm.bytes_moved - b0}, lock)
@@ -308,8 +309,12 @@ class Coordinator:
                     pid = m["prompt_id"]
                     if pid in self.spmd_waiting:
                         self.spmd_waiting[pid][r] = m
-                    else:
+                    elif m.get("mode", "single") == "single":
                         self._finish_single(r, m)
+                    else:
+                        # a survivor's report of an SPMD attempt that was already settled (a rank died
+                        # under it): never let it complete the prompt's single re-run on this rank
+                        logging.info("late SPMD report of prompt %s from rank %d ignored", pid, r)
                     self.cv.notify_all()
 
     def _rank_died(self, r):
@@ -474,8 +479,11 @@ class Coordinator:
         with spmd.activate(self.ctx, mode):
             self.ex_spmd.execute(prompt, prompt_id, extra, outputs)
         mine, mine_b = self.ctx.images_sampled - n0, self.comm.bytes_moved - b0
+        # every live worker's report (a survivor of a rank death fails its next agreement within ~1 s);
+        # bounded, so a wedged worker cannot hold the node
+        t_end = time.perf_counter() + SPMD_REPORT_TIMEOUT_S
         self._wait(lambda: all(r in self.spmd_waiting[prompt_id] for r in self.live() if r != 0)
-                   or len(self.live()) < self.world)
+                   or time.perf_counter() > t_end)
         retry = False
         with self.cv:
             done = self.spmd_waiting.pop(prompt_id)
