@@ -27,7 +27,8 @@ _kernels_err = None
 
 
 def kernel_lib_path() -> str:
-    return os.path.join(LIB_DIR, "libcgs_kernels.so")
+    """The in-tree kernel library (``CGS_KERNELS_SO`` names another build of it: kernel A/B runs)."""
+    return os.environ.get("CGS_KERNELS_SO") or os.path.join(LIB_DIR, "libcgs_kernels.so")
 
 
 def load_kernels():
