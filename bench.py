@@ -223,7 +223,7 @@ def _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log):
     from comfy_gen_server_amd.graph.validation import validate_prompt
     from comfy_gen_server_amd.sched import spmd
     from comfy_gen_server_amd.tools import synth
-    from comfy_gen_server_amd.utils import folder_paths
+    from comfy_gen_server_amd.utils import folder_paths, imageio
     registry.init_nodes(custom_nodes=False)
     synth.register_node()
     synth._PIPELINES[(args.family, 1234)] = (gen.patcher, gen.clip, gen.vae)   # the weights built above
@@ -231,6 +231,7 @@ def _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log):
     folder_paths.set_output_directory(out_dir)
     ctx = spmd.SPMD(comm) if comm.world > 1 else None
     ex = PromptExecutor(None, node_hook=ctx)
+    imageio.defer_saves(True)
 
     def step(i):
         wf = synth.text_to_image_workflow(args.family, seed=1000 + i, text=f"{job.prompt}, variation {i}",
@@ -246,18 +247,21 @@ def _bench_executor(args, comm, gen, job, global_batch, t0, t_build, log):
         else:
             ex.execute(wf, f"bench-{i}", {}, outputs)
         assert ex.success, ex.status_messages[-1:]
-        if not args.cpu:
-            torch.cuda.synchronize()
+        # the PNG encodes of this job run on the CPU pool behind the next job (utils/imageio async
+        # saves, as in the server's worker loop); the timed region ends after every file is written
+        imageio.take_pending()
 
     for i in range(args.warmup):
         ts = time.perf_counter()
         step(i)
         log(f"warmup workflow {i}: {time.perf_counter() - ts:.2f}s")
+    imageio.flush()
     comm.barrier()
     ops.reset_stats()
     t1 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    imageio.flush()
     if not args.cpu:
         torch.cuda.synchronize()
     comm.barrier()

@@ -271,6 +271,13 @@ class PromptServer:
                 output_dir = full
             filename = os.path.basename(filename)
             file = os.path.join(output_dir, filename)
+            from ..utils import imageio
+            fut = imageio.pending(file)
+            if fut is not None:          # still being encoded behind the worker (async saves)
+                try:
+                    await asyncio.wait_for(asyncio.wrap_future(fut), timeout=120)
+                except Exception:
+                    pass
             if not os.path.isfile(file):
                 return web.Response(status=404)
             from PIL import Image

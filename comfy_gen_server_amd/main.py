@@ -16,6 +16,7 @@ Run: ``python -m comfy_gen_server_amd.main --listen 0.0.0.0 --port 8188`` (or ``
 from __future__ import annotations
 
 import asyncio
+import functools
 import gc
 import itertools
 import logging
@@ -104,13 +105,33 @@ def hijack_progress(server):
     progress.set_progress_bar_global_hook(hook)
 
 
+def _finish_prompt(q, server, item_id, prompt_id, outputs_ui, success, messages, t0, client_id, save_errors):
+    if save_errors:
+        success = False
+        messages = messages + [("execution_error", {"prompt_id": prompt_id, "node_id": None,
+                                                    "exception_message": "; ".join(save_errors),
+                                                    "exception_type": "ImageSaveError", "traceback": []})]
+    q.task_done(item_id, outputs_ui,
+                status=q.ExecutionStatus(status_str="success" if success else "error",
+                                         completed=success, messages=messages))
+    if client_id is not None:
+        server.send_sync("executing", {"node": None, "prompt_id": prompt_id}, client_id)
+    dt = time.perf_counter() - t0
+    server.metrics["prompts_total"] += 1
+    server.metrics["execution_seconds_total"] += dt
+    if not success:
+        server.metrics["prompts_failed"] += 1
+    logging.info("Prompt executed in %.2f seconds", dt)
+
+
 def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_interval: float = 10.0):
     """Blocking worker loop (reference ``main.py:93-146``)."""
     from .graph.executor import PromptExecutor
     from .runtime import device as dm
-    from .utils import telemetry
+    from .utils import imageio, telemetry
 
     e = PromptExecutor(server)
+    imageio.defer_saves(True)
     last_gc = time.perf_counter()
     need_gc = False
     timeout = 1000.0
@@ -124,17 +145,15 @@ def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_inter
             with telemetry.maybe_profile(prompt_id):
                 e.execute(item[2], prompt_id, item[3], item[4])
             need_gc = True
-            q.task_done(item_id, e.outputs_ui,
-                        status=q.ExecutionStatus(status_str="success" if e.success else "error",
-                                                 completed=e.success, messages=e.status_messages))
-            if server.client_id is not None:
-                server.send_sync("executing", {"node": None, "prompt_id": prompt_id}, server.client_id)
-            dt = time.perf_counter() - t0
-            server.metrics["prompts_total"] += 1
-            server.metrics["execution_seconds_total"] += dt
-            if not e.success:
-                server.metrics["prompts_failed"] += 1
-            logging.info("Prompt executed in %.2f seconds", dt)
+            # the prompt's PNG encodes (utils/imageio async saves) finish behind the next prompt; the
+            # prompt is reported complete once its files are on disk
+            futs = imageio.take_pending()
+            done = functools.partial(_finish_prompt, q, server, item_id, prompt_id, e.outputs_ui, e.success,
+                                     list(e.status_messages), t0, server.client_id)
+            if futs:
+                threading.Thread(target=lambda d=done, f=futs: d(imageio.wait_futures(f)), daemon=True).start()
+            else:
+                done([])
 
         flags = q.get_flags()
         free_memory = flags.get("free_memory", False)

@@ -174,6 +174,7 @@ def worker_main(comm, address, authkey: bytes):
     """Rank >= 1: execute what rank 0 sends until it says stop."""
     from ..graph.executor import PromptExecutor
     from ..runtime import device as dm
+    from ..utils import imageio
     from . import spmd
     conn = None
     for _ in range(600):
@@ -238,8 +239,12 @@ def worker_main(comm, address, authkey: bytes):
             ex_single.execute(m["prompt"], pid, extra, m["outputs"])
             ex = ex_single
         need_gc = True
-        send_msg(conn, {"op": "done", "prompt_id": pid, "mode": m["mode"], "rank": comm.rank, "success": ex.success,
-                        "messages": ex.status_messages, "outputs_ui": ex.outputs_ui,
+        save_errs = imageio.wait_futures(imageio.take_pending())    # this rank's files are on disk first
+        ok = ex.success and not save_errs
+        msgs = ex.status_messages + ([("execution_error", {"prompt_id": pid, "exception_message": "; ".join(save_errs)})]
+                                     if save_errs else [])
+        send_msg(conn, {"op": "done", "prompt_id": pid, "mode": m["mode"], "rank": comm.rank, "success": ok,
+                        "messages": msgs, "outputs_ui": ex.outputs_ui,
                         "seconds": time.perf_counter() - t0, "images_sampled": ctx.images_sampled - n0,
                         "comm_bytes": comm.bytes_moved - b0}, lock)
     try:
@@ -446,13 +451,18 @@ class Coordinator:
                 self._rank_died(r)
 
     def _local_single(self, prompt_id, prompt, extra, outputs):
+        from ..utils import imageio
         self.server.last_prompt_id = prompt_id
         msg = {"success": False, "messages": [("execution_error", {"prompt_id": prompt_id,
                                                                    "exception_message": "executor raised"})],
                "outputs_ui": {}}
         try:
             self.ex_single.execute(prompt, prompt_id, extra, outputs)
-            msg = {"success": self.ex_single.success, "messages": self.ex_single.status_messages,
+            errs = imageio.wait_futures(imageio.take_pending())
+            msg = {"success": self.ex_single.success and not errs,
+                   "messages": self.ex_single.status_messages + (
+                       [("execution_error", {"prompt_id": prompt_id, "exception_message": "; ".join(errs)})]
+                       if errs else []),
                    "outputs_ui": self.ex_single.outputs_ui}
         except Exception as ex:     # the executor handles node errors itself: this is a bug, not a node error
             logging.exception("rank 0 executor raised")
@@ -463,6 +473,7 @@ class Coordinator:
                 self.cv.notify_all()
 
     def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd"):
+        from ..utils import imageio
         from . import spmd
         self._wait(lambda: not self.busy)
         with self.cv:
@@ -478,6 +489,7 @@ class Coordinator:
         n0, b0 = self.ctx.images_sampled, self.comm.bytes_moved
         with spmd.activate(self.ctx, mode):
             self.ex_spmd.execute(prompt, prompt_id, extra, outputs)
+        save_errs = imageio.wait_futures(imageio.take_pending())
         mine, mine_b = self.ctx.images_sampled - n0, self.comm.bytes_moved - b0
         # every live worker's report (a survivor of a rank death fails its next agreement within ~1 s);
         # bounded, so a wedged worker cannot hold the node
@@ -487,8 +499,10 @@ class Coordinator:
         retry = False
         with self.cv:
             done = self.spmd_waiting.pop(prompt_id)
-            ok = self.ex_spmd.success and all(bool(m.get("success")) for m in done.values())
+            ok = self.ex_spmd.success and not save_errs and all(bool(m.get("success")) for m in done.values())
             msgs = list(self.ex_spmd.status_messages)
+            if save_errs:
+                msgs.append(("execution_error", {"prompt_id": prompt_id, "exception_message": "; ".join(save_errs)}))
             for r, m in sorted(done.items()):
                 if not m.get("success"):
                     msgs += [(e, d) for e, d in (m.get("messages") or []) if e == "execution_error"]

@@ -2,14 +2,20 @@
 
 * ``save_png_batch`` — PNG with ``prompt`` / workflow tEXt chunks (``nodes.py:1810-1837``); the
   batch is converted to uint8 on the device in one op and encoded by a thread pool (PNG encode of
-  large batches is CPU-heavy: SURVEY §7.5 item 6).
+  large batches is CPU-heavy: SURVEY §7.5 item 6). In a thread that opted in (``defer_saves``: the
+  worker loop; ``CGS_ASYNC_SAVE=0`` turns it off) the encodes run behind the caller: the worker loop
+  starts the next prompt while they finish and reports the
+  prompt complete once its files are on disk (``take_pending``); ``/view`` waits for a file still
+  being written (``pending``); each file is written to ``<name>.part`` and renamed into place.
 * ``load_image_frames`` — multi-frame images, EXIF transpose, alpha -> inverted MASK
   (``nodes.py:1866-1893``).
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import logging
 import os
+import threading
 
 import numpy as np
 import torch
@@ -67,8 +73,26 @@ def reserve_png_names(folder, filename, counter, count):
     return names
 
 
-def write_png_files(images, paths, metadata=None, compress_level=4):
-    """Encode ``images`` (B, H, W, C float in [0, 1]) to ``paths`` on the thread pool."""
+_PENDING: dict = {}          # absolute path -> future of an encode still in flight
+_plock = threading.Lock()
+_tl = threading.local()      # futures the calling thread started since its last take_pending()
+
+
+def defer_saves(on: bool = True):
+    """Opt the calling thread into deferred saves (the server's worker loop, bench --via-executor): its
+    PNG encodes return at once and are collected with ``take_pending``. Other callers keep the
+    synchronous behaviour (files on disk when the node returns)."""
+    _tl.defer = bool(on)
+
+
+def async_saves() -> bool:
+    return getattr(_tl, "defer", False) and os.environ.get("CGS_ASYNC_SAVE", "1") != "0"
+
+
+def write_png_files(images, paths, metadata=None, compress_level=4, wait=None):
+    """Encode ``images`` (B, H, W, C float in [0, 1]) to ``paths`` on the thread pool. The device ->
+    host copy happens here; the encodes are waited for unless ``CGS_ASYNC_SAVE`` is on (``wait=None``),
+    in which case the caller collects them with ``take_pending``."""
     arrs = to_uint8_cpu(images)
 
     def work(a, p):
@@ -78,10 +102,60 @@ def write_png_files(images, paths, metadata=None, compress_level=4):
             info = PngInfo()
             for k, v in metadata.items():
                 info.add_text(k, v)
-        img.save(p, pnginfo=info, compress_level=compress_level)
+        tmp = p + ".part"
+        img.save(tmp, format="PNG", pnginfo=info, compress_level=compress_level)
+        os.replace(tmp, p)
     jobs = [_pool().submit(work, a, p) for a, p in zip(arrs, paths)]
-    for j in jobs:
-        j.result()
+    if wait is None:
+        wait = not async_saves()
+    if wait:
+        for j in jobs:
+            j.result()
+        return []
+    with _plock:
+        for p, j in zip(paths, jobs):
+            ap = os.path.abspath(p)
+            _PENDING[ap] = j
+            j.add_done_callback(lambda f, ap=ap: _drop_pending(ap, f))
+    _tl.futs = getattr(_tl, "futs", []) + jobs
+    return jobs
+
+
+def _drop_pending(ap, f):
+    with _plock:
+        if _PENDING.get(ap) is f:
+            del _PENDING[ap]
+
+
+def take_pending() -> list:
+    """The encode futures this thread started since the last call (a prompt's saves)."""
+    futs = getattr(_tl, "futs", [])
+    _tl.futs = []
+    return futs
+
+
+def wait_futures(futs) -> list:
+    """Wait for ``futs``; returns the error strings of the ones that failed."""
+    errs = []
+    for f in futs:
+        try:
+            f.result()
+        except Exception as e:   # a write error fails the prompt that saved the file
+            logging.error("image save failed: %s", e)
+            errs.append(f"{type(e).__name__}: {e}")
+    return errs
+
+
+def pending(path):
+    """The in-flight encode of ``path`` (or None)."""
+    with _plock:
+        return _PENDING.get(os.path.abspath(path))
+
+
+def flush():
+    with _plock:
+        futs = list(_PENDING.values())
+    wait_futures(futs)
 
 
 def save_png_batch(images, folder, filename, counter, metadata=None, compress_level=4):
