@@ -286,18 +286,15 @@ __device__ __forceinline__ void af_softmax(f32x16 (&s)[2], bf16x8 (&pf)[4], f32x
   }
   const float nm = -m_run;
   float ps = 0.f;
-  // exponent arguments two at a time (v_pk_fma_f32: half the issue cycles of two v_fma_f32 -- the
-  // softmax VALU stream, not the matrix pipe, bounds this loop at two waves per SIMD)
-  const f32x2_t c2 = {c, c}, nm2 = {nm, nm};
+  // (v_pk_fma_f32 pairs for these exponent arguments measured 2-4 % SLOWER at SDXL levels 1 / 2,
+  // profiles/r04/attn_pkfma_ab.log: scalar v_fma_f32 stays)
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const f32x2_t a = f32x2_t{s[kt][r], s[kt][r + 1]} * c2 + nm2;
-      const float p0 = __builtin_amdgcn_exp2f(a.x), p1 = __builtin_amdgcn_exp2f(a.y);
-      if constexpr (!MSUM) ps += p0 + p1;
-      pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p0;
-      pf[kt * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][r], c, nm));
+      if constexpr (!MSUM) ps += p;
+      pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p;
     }
   if constexpr (!MSUM) l_run += ps;
 }

@@ -1,3 +1,7 @@
+// STATUS (measured, profiles/r04/gemm_hip_vs_hipblaslt.md): 0.5-0.8x of the production v6 / v7 kernels on
+// every SDXL shape and its GEGLU form off by ~0.1 relative error -- an experiment the dispatcher never
+// selects (tools/gemm_ab.py / gemm_probe.py only); GEGLU is refused at the entry point.
+//
 // "w4" GEMM: persistent 256 x 256 x 64 bf16 GEMM with ONE wave per SIMD (4 waves per workgroup, one
 // workgroup per CU), each wave owning a 128 x 128 output tile (8 x 8 v_mfma_f32_16x16x32_bf16 tiles,
 // 256 accumulator registers), ONE barrier per K-tile. Same fused epilogues as the 8-wave kernels (bias,
@@ -509,6 +513,7 @@ CGS_EXPORT int cgs_gemm_bf16_w4(const void* A, const void* W, void* C, const voi
                                 const float* rs, const float* cs, int bn, hipStream_t stream) {
   const bool gg = (epi & MC_EPI_GEGLU) != 0, ln = (epi & MC_EPI_LNFOLD) != 0;
   const int nout = gg ? N / 2 : N;
+  if (gg) return (int)hipErrorInvalidValue;     // GEGLU form numerically wrong (see STATUS above)
   if (K % 64 || K < 128 || lda % 8 || ldw % 8 || ldc % 8 || nout % 8 || (gg && N % 32) ||
       ((epi & MC_EPI_RESIDUAL) && (gg || ln || ldr % 8)) || (epi & MC_EPI_F32OUT) ||
       ((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R) % 16 || ((uintptr_t)bias % 8) ||

@@ -424,6 +424,7 @@ def test_run_graph_with_controlnet_matches_eager(cuda, monkeypatch, sampler):
         pos = encode_prompt(clip, "a house", 64, 64)
         neg = encode_prompt(clip, "blurry", 64, 64)
         res = {}
+        cnet = rcn.ControlNet(cm, load_device=cuda)      # one loaded net, as the cached loader node's output
         for mode in ("0", "1"):
             monkeypatch.setenv("CGS_RUN_GRAPHS", mode)
             before = dict(run_graph.stats)
@@ -431,7 +432,6 @@ def test_run_graph_with_controlnet_matches_eager(cuda, monkeypatch, sampler):
             for j in range(3):
                 g = torch.Generator().manual_seed(j)
                 hint = torch.rand(1, 64, 64, 3, generator=g).to(cuda)
-                cnet = rcn.ControlNet(cm, load_device=cuda)
                 pc, nc = NM["ControlNetApplyAdvanced"]().apply_controlnet(pos, neg, cnet, hint, 0.8, 0.0, 0.6)
                 latent = torch.zeros([2, 4, 8, 8])
                 noise = S.prepare_noise(latent, 5)
