@@ -13,6 +13,7 @@ Parameter names match the released checkpoints.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -28,6 +29,13 @@ from .layers import Conv2d, DerivedMixin, LayerNorm, Linear, module_epoch
 # ------------------------------------------------------------------------------------------------
 def _ln(x, eps=1e-6):
     return ops.layer_norm(x, None, None, eps)
+
+
+def _fuse(name: str) -> bool:
+    """Cascade block fusions (default on; ``CGS_CASCADE_<NAME>=0`` selects the un-fused form for A/B runs):
+    GELU_EPI (GELU in the first ChannelMLP GEMM), LNFOLD (LayerNorm folded into it, statistics from the
+    depthwise kernel), GRNFOLD (GRN folded into per-image second-GEMM weights)."""
+    return os.environ.get(f"CGS_CASCADE_{name}", "1") != "0"
 
 
 def _cast(w, x):
@@ -99,7 +107,7 @@ class _ChannelMLP(nn.Sequential):
 
     def forward(self, x, residual=None):
         grn = self[2]
-        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4) or not _fuse("GELU_EPI"):
             h = ops.grn_nhwc(self[0](x), _cast(grn.gamma, x), _cast(grn.beta, x), pre_gelu=True)
             return self[4](h, residual=residual)
         return self._grn_linear2(self[0](x, act="gelu"), x, residual)
@@ -107,7 +115,8 @@ class _ChannelMLP(nn.Sequential):
     def lnfold_ok(self, x) -> bool:
         """LayerNorm (no affine) of ``x`` can fold into the first GEMM (device bf16, unhooked weights)."""
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not layers._hooked(self[0])
-                and self[0].weight.dtype == torch.bfloat16 and ops.lnfold_available(x, x.shape[-1]))
+                and self[0].weight.dtype == torch.bfloat16 and ops.lnfold_available(x, x.shape[-1])
+                and _fuse("LNFOLD") and _fuse("GELU_EPI"))
 
     def forward_ln(self, x, eps=1e-6, residual=None, rs=None):
         """``forward(LN(x))`` with the LayerNorm folded into the first GEMM: only the per-pixel statistics
@@ -131,7 +140,7 @@ class _ChannelMLP(nn.Sequential):
         grn = self[2]
         N, H, W, _ = x.shape
         lin2 = self[4]
-        if lin2.out_features < H * W and N <= 64 and h.shape[-1] % 8 == 0:
+        if lin2.out_features < H * W and N <= 64 and h.shape[-1] % 8 == 0 and _fuse("GRNFOLD"):
             w2, b2 = lin2.weight_bias_for(h)
             wn = ops.grn_fold_weight(h, w2, _cast(grn.gamma, h))
             bias = ops.linear(_cast(grn.beta, h).reshape(1, -1), w2, b2).reshape(-1)      # b2 + W2 beta

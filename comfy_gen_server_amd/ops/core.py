@@ -1220,9 +1220,7 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
                                                  rs.data_ptr(), cs.data_ptr(), M, N, K, K, K, N, epi, None, 0,
                                                  variant, _stream()), "cgs_gemm_bf16_lnfold_v")
             return out
-        cands = [("v8", lambda: run_g(8))]
-        if N % 160 == 0:
-            cands.append(("v6", lambda: run_g(6)))
+        cands = [("v8", lambda: run_g(8)), ("v6", lambda: run_g(6))]
         if _underfilled(M, N):
             cands += [(f"v{v}", (lambda v=v: run_g(v))) for v in _SMALL_TILE]
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v6" if N % 160 == 0 else "v8")

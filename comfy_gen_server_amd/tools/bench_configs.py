@@ -120,7 +120,7 @@ def bench_sdxl_cn_lora(reps, pipe=None):
               controlnet="sdxl-size cldm (random init)")
 
 
-def bench_cascade(reps):
+def bench_cascade(reps, ab=None):
     from ..graph import registry
     from ..models.cascade import StageA
     from ..models.layers import init_random_fast_
@@ -162,6 +162,8 @@ def bench_cascade(reps):
     n_c = sum(p.numel() for p in pc.model.diffusion_model.parameters()) / 1e9
     n_b = sum(p.numel() for p in pb.model.diffusion_model.parameters()) / 1e9
 
+    if ab:
+        return _cascade_ab(ab, reps, pc, pb, vae, pos, neg, NM)
     for batch in (1, 4):
         def run():
             with torch.inference_mode():
@@ -179,10 +181,58 @@ def bench_cascade(reps):
               params_c_b=round(n_c, 3), params_b_b=round(n_b, 3))
 
 
+def _cascade_ab(cfgs, rounds, pc, pb, vae, pos, neg, NM):
+    """Batch-1 Cascade jobs alternating between env configurations (``name:ENV=V,...``) in one process:
+    captured graph plans are dropped on every switch and re-captured in an untimed job."""
+    import statistics
+
+    def drop(p):
+        m = p.model
+        for k in ("_step_graph_plans", "_run_graph_plans"):
+            m.__dict__.pop(k, None)
+        r = m.__dict__.get("_graph_runner")
+        if r is not None:
+            r.reset()
+
+    def run():
+        with torch.inference_mode():
+            lat_c, lat_b = NM["StableCascade_EmptyLatentImage"]().generate(1024, 1024, 42, 1)
+            out_c = NM["KSampler"]().sample(pc, 5, 20, 4.0, "euler_ancestral", "simple", pos, neg, lat_c, 1.0)[0]
+            cond_b = NM["StableCascade_StageB_Conditioning"]().set_prior(pos, out_c)[0]
+            neg_b = NM["StableCascade_StageB_Conditioning"]().set_prior(neg, out_c)[0]
+            out_b = NM["KSampler"]().sample(pb, 5, 10, 1.1, "euler_ancestral", "simple", cond_b, neg_b, lat_b, 1.0)[0]
+            NM["VAEDecode"]().decode(vae, out_b)
+        torch.cuda.synchronize()
+
+    parsed = []
+    for c in cfgs:
+        name, _, rest = c.partition(":")
+        parsed.append((name, dict(kv.split("=", 1) for kv in rest.split(",") if kv)))
+    keys = {k for _, e in parsed for k in e}
+    times = {n: [] for n, _ in parsed}
+    for r in range(rounds + 1):
+        for name, env in parsed:
+            for k in keys:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            drop(pc)
+            drop(pb)
+            run()                                   # untimed: autotune keys, graph capture
+            if r:
+                t = time.perf_counter()
+                run()
+                times[name].append(time.perf_counter() - t)
+                print(f"[cascade-ab] round {r} {name}: {times[name][-1]:.3f}s", file=sys.stderr, flush=True)
+    print(json.dumps({n: {"median_s": round(statistics.median(v), 4), "runs": [round(x, 4) for x in v]}
+                      for n, v in times.items()}), flush=True)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="all")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--ab", action="append", default=None,
+                    help="cascade only: name:ENV=V,... configurations alternated per batch-1 job (--reps rounds)")
     a = ap.parse_args(argv)
     if not torch.cuda.is_available():
         print("needs a GPU", file=sys.stderr)
@@ -195,7 +245,7 @@ def main(argv=None):
     del pipe
     torch.cuda.empty_cache()
     if a.which in ("all", "cascade"):
-        bench_cascade(a.reps)
+        bench_cascade(a.reps, a.ab)
     return 0
 
 

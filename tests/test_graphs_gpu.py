@@ -440,10 +440,14 @@ def test_run_graph_with_controlnet_matches_eager(cuda, monkeypatch, sampler):
         torch.cuda.synchronize()
     assert run_graph.stats["capture"] - before["capture"] == 1, run_graph.stats
     assert run_graph.stats["replay_runs"] - before["replay_runs"] == 2, run_graph.stats
+    # the replay of job 2 tracks ITS hint: eager vs replay of the same job agree far more closely than two
+    # jobs with different hints differ (the random tiny net moves the output only ~1e-3 per hint change)
+    hint_effect = (res["0"][1] - res["0"][2]).norm().item()
+    assert hint_effect > 0
     for a, b in zip(res["0"], res["1"]):
-        err = ((a - b).norm() / a.norm()).item()
-        assert err < 1e-2, err
-    assert ((res["1"][1] - res["1"][2]).norm() / res["1"][1].norm()).item() > 1e-3   # the hint reached the replay
+        diff = (a - b).norm().item()
+        assert diff / a.norm().item() < 1e-2, diff
+        assert diff < 0.25 * hint_effect, (diff, hint_effect)
 
 
 @pytest.mark.gpu
