@@ -31,11 +31,16 @@ def _ln(x, eps=1e-6):
     return ops.layer_norm(x, None, None, eps)
 
 
+_FUSE_DEFAULTS = {"GELU_EPI": "1", "LNFOLD": "1", "GRNFOLD": "1", "DWLN": "0"}
+
+
 def _fuse(name: str) -> bool:
-    """Cascade block fusions (default on; ``CGS_CASCADE_<NAME>=0`` selects the un-fused form for A/B runs):
-    GELU_EPI (GELU in the first ChannelMLP GEMM), LNFOLD (LayerNorm folded into it, statistics from the
-    depthwise kernel), GRNFOLD (GRN folded into per-image second-GEMM weights)."""
-    return os.environ.get(f"CGS_CASCADE_{name}", "1") != "0"
+    """Cascade block fusions (``CGS_CASCADE_<NAME>=0/1`` overrides the default, for A/B runs): GELU_EPI
+    (GELU in the first ChannelMLP GEMM), LNFOLD (LayerNorm folded into it), DWLN (its statistics from the
+    depthwise kernel: off -- at Stage C's 1152-pixel grids the per-pixel reduction leaves the kernel
+    latency-bound, 33 us vs 11 + 9 us for the two passes, profiles/r04/cascade_fusion_profile.md),
+    GRNFOLD (GRN folded into per-image second-GEMM weights)."""
+    return os.environ.get(f"CGS_CASCADE_{name}", _FUSE_DEFAULTS[name]) != "0"
 
 
 def _cast(w, x):
@@ -162,7 +167,7 @@ class ResBlock(nn.Module):
         self.channelwise = _ChannelMLP(c + c_skip, c * 4, c, dtype=dtype, device=device)
 
     def forward(self, x, x_skip=None):
-        if x_skip is None and self.channelwise.lnfold_ok(x):
+        if x_skip is None and self.channelwise.lnfold_ok(x) and _fuse("DWLN"):
             # depthwise conv + LayerNorm statistics in one pass, LayerNorm folded into the first GEMM
             dw = self.depthwise
             d, rs = ops.depthwise_conv2d_nhwc_lnstats(x, dw.w_kkc(x), _cast(dw.bias, x), dw.kernel_size[0], 1e-6,
