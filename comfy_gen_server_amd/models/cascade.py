@@ -31,7 +31,10 @@ def _ln(x, eps=1e-6):
     return ops.layer_norm(x, None, None, eps)
 
 
-_FUSE_DEFAULTS = {"GELU_EPI": "1", "LNFOLD": "1", "GRNFOLD": "1", "DWLN": "0"}
+# all off by default: each measured 0.1-0.8 % SLOWER than the separate passes at batch 1 (in-process A/B,
+# profiles/r04/cascade_fusion_ab_r04k.json) -- the GRN / LayerNorm passes they remove are small at these
+# grids while the extra epilogue work sits on the GEMM's critical path
+_FUSE_DEFAULTS = {"GELU_EPI": "0", "LNFOLD": "0", "GRNFOLD": "0", "DWLN": "0"}
 
 
 def _fuse(name: str) -> bool:

@@ -1049,11 +1049,13 @@ def test_gemm_gelu_epilogue(cuda, M, N, K, variant, res):
 
 
 @pytest.mark.parametrize("N,H,W,c", [(2, 16, 16, 64), (2, 6, 6, 64), (1, 32, 24, 128)])
-def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c):
+def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c, monkeypatch):
     """Cascade ChannelMLP on the device -- GELU epilogue, then the GRN either as a pass over h (H W <= c)
     or folded into per-image second-GEMM weights (H W > c) -- vs the fp32 NCHW reference math."""
     from comfy_gen_server_amd.models import cascade as SC
     from comfy_gen_server_amd.models.layers import init_random_
+    for k in ("GELU_EPI", "GRNFOLD"):
+        monkeypatch.setenv(f"CGS_CASCADE_{k}", "1")
     torch.manual_seed(6)
     m = SC._ChannelMLP(c, 4 * c, c)
     init_random_(m, seed=3)
@@ -1075,11 +1077,13 @@ def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c):
 
 
 @pytest.mark.parametrize("N,H,W,c", [(2, 16, 16, 128), (2, 6, 6, 128), (1, 8, 8, 256)])
-def test_cascade_resblock_lnfold(cuda, N, H, W, c):
+def test_cascade_resblock_lnfold(cuda, N, H, W, c, monkeypatch):
     """Cascade ResBlock / FeedForwardBlock on the device: LayerNorm folded into the first GEMM together with
     the GELU epilogue (ops.linear_lnfold act="gelu"), GRN pass or GRN weight fold, vs the fp32 CPU blocks."""
     from comfy_gen_server_amd.models import cascade as SC
     from comfy_gen_server_amd.models.layers import init_random_
+    for k in ("GELU_EPI", "LNFOLD", "GRNFOLD", "DWLN"):
+        monkeypatch.setenv(f"CGS_CASCADE_{k}", "1")
     torch.manual_seed(7)
     for blk in (SC.ResBlock(c), SC.FeedForwardBlock(c)):
         init_random_(blk, seed=4)
