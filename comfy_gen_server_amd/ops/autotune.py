@@ -21,6 +21,7 @@ Env:
                           entries; the packaged table itself is never written)
   CGS_TUNE_DEFAULT=0      do not load the packaged table
   CGS_TUNE_REPS=n         timed repetitions per candidate (default 3)
+  CGS_TUNE_DUMP=path      at exit, write every choice made in this process with its per-candidate ms
 """
 from __future__ import annotations
 
@@ -79,6 +80,22 @@ def _save():
         os.replace(tmp, path)
     except OSError:
         pass
+
+
+def _dump_at_exit():
+    path = os.environ.get("CGS_TUNE_DUMP")
+    if not path:
+        return
+    try:
+        with open(path, "w") as f:
+            json.dump(table(), f, indent=1, sort_keys=True)
+    except OSError:
+        pass
+
+
+if os.environ.get("CGS_TUNE_DUMP"):
+    import atexit
+    atexit.register(_dump_at_exit)
 
 
 def _capturing() -> bool:
