@@ -183,6 +183,8 @@ KERNEL_SIGNATURES = {
     # "w4" GEMM (gemm_w4.hip, one wave per SIMD): A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, rs, cs
     "cgs_gemm_bf16_w4": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _P, _I, _P],
     "cgs_w4_set_group": [_I],
+    # experiment: 4-slot-ring one-wave-per-SIMD GEMM (bias / residual epilogue only)
+    "cgs_gemm_bf16_w5": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
 }
 
 

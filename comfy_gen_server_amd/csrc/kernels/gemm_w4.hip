@@ -163,6 +163,23 @@ __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, co
       fb[j] = *reinterpret_cast<const bf16x8*>(P + AIMG + (wc * WN + 16 * j + fr) * 128 + cb);
   };
 
+  // F0(t+1) reads from buffer rb interleaved with the DMAs of K-tile kd into buffer db (8 + NJ each)
+  auto read_dma = [&](int rb, uint32_t cb, bf16x8 (&fa)[8], bf16x8 (&fb)[NJ], int db, int kd) {
+    const unsigned char* P = smem + rb * BUF;
+    mc::static_for<0, 8 + NJ>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i < 8)
+        fa[i] = *reinterpret_cast<const bf16x8*>(P + (wr * 128 + 16 * i + fr) * 128 + cb);
+      else
+        fb[i - 8] = *reinterpret_cast<const bf16x8*>(P + AIMG + (wc * WN + 16 * (i - 8) + fr) * 128 + cb);
+      // DMA i: A pieces first, then B (the same 8 + NJ loads as dma_tile)
+      if constexpr (i < 8)
+        dma_a(i, db, kd);
+      else
+        dma_b(i - 8, db, kd);
+    });
+  };
+
   f32x4 acc[8][NJ];
   // MFMAs over row tiles [I0, I1) of fragment set (fa, fb); Z: first K-tile (zero accumulator operand)
   auto mma = [&](auto i0c, auto i1c, auto zc, const bf16x8 (&fa)[8], const bf16x8 (&fb)[NJ]) {
@@ -439,8 +456,10 @@ __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, co
     if (k2 == nk && has_next) setup(nm0, nn0);
     const int kd = k2 < nk ? k2 : (has_next ? k2 - nk : nk - 1);
     fence();
-    read_set(sb ^ 1, c0, fa0, fb0);
-    dma_tile(sb, kd);
+    // reads and DMAs alternate in PROGRAM order (r0 d0 r1 d1 ...): a DMA writes LDS, so the scheduler
+    // keeps it ordered against every ds_read -- issued as all-reads-then-all-DMAs, the pin below could
+    // not be met and the compiler bunched the 16 reads and 16 DMAs ahead of the MFMAs
+    read_dma(sb ^ 1, c0, fa0, fb0, sb, kd);
     mma(I4{}, I8{}, F_{}, fa1, fb1);
     pin(std::integral_constant<int, 4 * NJ>{}, std::integral_constant<int, 8 + NJ>{},
         std::integral_constant<int, 8 + NJ>{});

@@ -67,9 +67,9 @@ def main(argv):
     assert lib is not None, _native.kernels_error()
     dev = torch.device("cuda", 0)
     stream = core._stream()
-    rows = ["| shape | M | N | K | epi | w4 TF/s | w4-160 TF/s | v6 TF/s | v7 TF/s | hipBLASLt TF/s | best w4 / best other "
-            "| w4 max rel err |",
-            "|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|"]
+    rows = ["| shape | M | N | K | epi | w4 TF/s | w4-160 TF/s | w5 TF/s | v6 TF/s | v7 TF/s | hipBLASLt TF/s "
+            "| best w4/w5 / best other | w4/w5 max rel err |",
+            "|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|"]
     torch.manual_seed(0)
     for name, M, N, K, epi in SHAPES:
         if only and name not in only:
@@ -126,6 +126,9 @@ def main(argv):
                 return e
             return f
         cands = {} if geglu else {"w4": w4}      # the w4 GEGLU form is refused (gemm_w4.hip STATUS)
+        if not geglu and not ln and K % 128 == 0 and _native.has_kernel("cgs_gemm_bf16_w5"):
+            cands["w5"] = lambda: lib.cgs_gemm_bf16_w5(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), rp, M, N,
+                                                       K, K, K, nout, ldr, flags, 1.0, stream)
         if not geglu and N % 160 == 0:
             cands["w4_160"] = w4v(160)
         errs = {}
@@ -148,12 +151,13 @@ def main(argv):
                 times[vn].append(_bench(f, iters))
         flops = 2.0 * M * N * K
         tf = {vn: flops / statistics.median(t) / 1e9 for vn, t in times.items()}
-        best_w4 = max([v for k, v in tf.items() if k.startswith("w4")] or [0.0])
-        other = max(v for k, v in tf.items() if not k.startswith("w4"))
+        best_w4 = max([v for k, v in tf.items() if k.startswith(("w4", "w5"))] or [0.0])
+        other = max(v for k, v in tf.items() if not k.startswith(("w4", "w5")))
         cell = lambda k: f"{tf[k]:.0f}" if k in tf else "-"  # noqa: E731
-        line = (f"| {name} | {M} | {N} | {K} | {epi or 'bias'} | {cell('w4')} | {cell('w4_160')} | {cell('v6')} | "
+        line = (f"| {name} | {M} | {N} | {K} | {epi or 'bias'} | {cell('w4')} | {cell('w4_160')} | {cell('w5')} | "
+                f"{cell('v6')} | "
                 f"{cell('v7')} | {cell('lib')} | {best_w4 / other:.3f} | "
-                f"{max([v for k, v in errs.items() if k.startswith('w4')] or [0.0]):.2e} |")
+                f"{max([v for k, v in errs.items() if k.startswith(('w4', 'w5'))] or [0.0]):.2e} |")
         rows.append(line)
         print(line, " errs:", {k: f"{v:.1e}" for k, v in errs.items()}, flush=True)
         del a, w, out, ref
