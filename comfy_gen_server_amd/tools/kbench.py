@@ -82,7 +82,7 @@ def main(quick=False, attn_only=False, gemm_only=False):
         fl = 4.0 * b * h * sq * sk * d
         lib = ops.dispatch._native.load_kernels()
         ent = dict(B=b, H=h, Sq=sq, Sk=sk, D=d)
-        for var, name in ((1, "generic"), (2, "d64"), (4, "d64r2"), (0, "auto")):
+        for var, name in ((1, "generic"), (2, "d64"), (4, "d64r2"), (5, "d64q128"), (0, "auto")):
             lib.cgs_attn_set_variant(var)
             t_hip = _time(lambda: ops.attention(q, k, v, h))
             ent[f"{name}_ms"] = t_hip
