@@ -112,11 +112,13 @@ def write_png_files(images, paths, metadata=None, compress_level=4, wait=None):
         for j in jobs:
             j.result()
         return []
+    aps = [os.path.abspath(p) for p in paths]
     with _plock:
-        for p, j in zip(paths, jobs):
-            ap = os.path.abspath(p)
+        for ap, j in zip(aps, jobs):
             _PENDING[ap] = j
-            j.add_done_callback(lambda f, ap=ap: _drop_pending(ap, f))
+    # outside the lock: a future that already finished runs its callback right here, in this thread
+    for ap, j in zip(aps, jobs):
+        j.add_done_callback(lambda f, ap=ap: _drop_pending(ap, f))
     _tl.futs = getattr(_tl, "futs", []) + jobs
     return jobs
 
