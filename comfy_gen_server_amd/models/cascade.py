@@ -12,7 +12,6 @@ Parameter names match the released checkpoints.
 """
 from __future__ import annotations
 
-import math
 import os
 
 import torch
@@ -51,15 +50,15 @@ def _cast(w, x):
                                    w.to(device=x.device, dtype=x.dtype))
 
 
-def _pw(conv, x, residual=None):
-    """1x1 conv on an NHWC tensor as a GEMM over the channel dim."""
+def _pw(conv, x, residual=None, act=None):
+    """1x1 conv on an NHWC tensor as a GEMM over the channel dim (``act="gelu"``: fused GELU epilogue)."""
     w = _cast(conv.weight, x).reshape(conv.out_channels, conv.in_channels)
     if x.is_cuda and conv.in_channels % 32:
         # narrow K (Stage A's 4-channel latent in): zero-pad K to 32 so the HIP GEMM takes it
         kp = (conv.in_channels + 31) // 32 * 32
         w = F.pad(w, (0, kp - conv.in_channels))
         x = F.pad(x, (0, kp - conv.in_channels))
-    return ops.linear(x, w, _cast(conv.bias, x), residual=residual)
+    return ops.linear(x, w, _cast(conv.bias, x), residual=residual, act=act)
 
 
 def _to_nhwc(x):
@@ -278,12 +277,13 @@ class TimestepBlock(nn.Module):
 
 
 def _r_embedding(r, c_r, max_positions=10000):
-    r = r.float() * max_positions
+    """Stable Cascade's sinusoidal r embedding (common.py ``gen_r_embedding``): [sin | cos] of
+    r * max_positions at frequencies exp(-ln(max_positions) k / (half - 1)) -- the same sinusoid as the
+    UNet timestep embedding with max_period = max_positions ** (half / (half - 1)), so it runs on that
+    kernel (one launch instead of the arange / exp / sin / cos / cat chain per step)."""
     half = c_r // 2
-    emb = math.log(max_positions) / (half - 1)
-    emb = torch.arange(half, device=r.device).float().mul(-emb).exp()
-    emb = r[:, None] * emb[None, :]
-    emb = torch.cat([emb.sin(), emb.cos()], dim=1)
+    emb = ops.timestep_embedding(r.float() * max_positions, 2 * half,
+                                 max_period=float(max_positions) ** (half / (half - 1)), flip_sin_to_cos=False)
     if c_r % 2 == 1:
         emb = F.pad(emb, (0, 1))
     return emb
@@ -572,7 +572,7 @@ class StageB(_UNetStage):
         return x if isinstance(mod, nn.Identity) else mod[1].forward_nhwc(_ln(x))
 
     def _mapper(self, seq, x):
-        return _ln(_pw(seq[2], F.gelu(_pw(seq[0], x))))
+        return _ln(_pw(seq[2], _pw(seq[0], x, act="gelu")))
 
     def gen_c_embeddings(self, clip):
         if clip.dim() == 2:
