@@ -441,6 +441,7 @@ def refresh_static_kv(model: nn.Module, sources) -> int:
     step plan's static context tensors, just refreshed with a new job's conditioning)."""
     n = 0
     for m in model.modules():
-        if isinstance(m, CrossAttention):
-            n += m.refresh_static_kv(sources)
+        fn = getattr(m, "refresh_static_kv", None)     # CrossAttention; Stable Cascade's stages
+        if fn is not None:
+            n += fn(sources)
     return n

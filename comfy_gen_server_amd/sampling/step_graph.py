@@ -152,7 +152,7 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
     # identity, so the UNet sees the plan's static tensors themselves (static K/V keys on them)
     try:
         mdt = model.manual_cast_dtype or model.get_dtype()
-        cond = {k: (v.to(mdt) if torch.is_tensor(v) and v.is_floating_point() and k in ("c_crossattn", "y") else v)
+        cond = {k: (v.to(mdt) if torch.is_tensor(v) and v.is_floating_point() and k in _STATIC_CAST else v)
                 for k, v in cond.items()}
     except Exception:
         pass
@@ -238,6 +238,10 @@ def try_sample(mk, x, sigmas, extra_args, callback, kind: str, eta: float = 1.0,
         if callback is not None:
             callback({"x": x_pre, "i": i, "sigma": s[i], "sigma_hat": s[i], "denoised": plan.den.clone()})
     return plan.x.clone()
+
+
+# conds apply_model casts to the compute dtype anyway (not c_concat: that one follows x's dtype)
+_STATIC_CAST = ("c_crossattn", "y", "clip_text", "clip_text_pooled", "clip_img", "clip", "effnet")
 
 
 def _new_plan(x, cond, hints):

@@ -315,6 +315,61 @@ def test_cascade_stage_c_step_graph_captures(cuda, monkeypatch):
     assert err < 2e-2 * (res["0"].abs().max().item() + 1), err
 
 
+@pytest.mark.parametrize("dev", [pytest.param("cuda", marks=pytest.mark.gpu), "cpu"])
+@pytest.mark.parametrize("stage", ["c", "b"])
+def test_cascade_static_cond_protocol(dev, stage):
+    """Stable Cascade's conditioning-only work (every attention block's clip K/V, Stage B's effnet /
+    pixel maps) under the step graph's static protocol: "fill" equals the inline forward, "use" reads
+    the stored buffers (stale after the cond tensors change in place) and refresh_static_kv brings them
+    to the new job's conditioning."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.attention import refresh_static_kv
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    if dev == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cuda = torch.device(dev)
+    g = torch.Generator().manual_seed(3)
+    bf = dict(device=cuda, dtype=torch.bfloat16 if dev == "cuda" else torch.float32)
+    if stage == "c":
+        m = SC.StageC(c_in=16, c_out=16, c_r=64, c_cond=128, c_hidden=[128, 128], nhead=[2, 2],
+                      blocks=[[1, 1], [1, 1]], block_repeat=[[1, 1], [2, 1]], level_config=["CTA", "CTA"],
+                      c_clip_text=64, c_clip_text_pooled=64, c_clip_img=768, c_clip_seq=2, switch_level=[False],
+                      **bf)
+        x = torch.randn(2, 16, 12, 12, generator=g).to(**bf)
+        conds = [torch.randn(2, 7, 64, generator=g).to(**bf), torch.randn(2, 1, 64, generator=g).to(**bf),
+                 torch.randn(2, 1, 768, generator=g).to(**bf)]
+
+        def run(**kw):
+            return m(x, torch.tensor([0.5, 0.25], device=cuda), *conds, **kw).float()
+    else:
+        m = SC.StageB(c_in=4, c_out=4, c_r=64, patch_size=2, c_cond=128, c_hidden=[64, 128], nhead=[-1, 2],
+                      blocks=[[1, 1], [1, 1]], block_repeat=[[1, 1], [1, 1]], level_config=["CT", "CTA"],
+                      c_clip=64, c_clip_seq=2, **bf)
+        x = torch.randn(2, 4, 32, 32, generator=g).to(**bf)
+        conds = [torch.randn(2, 16, 6, 6, generator=g).to(**bf), torch.randn(2, 1, 64, generator=g).to(**bf)]
+
+        def run(**kw):
+            return m(x, torch.tensor([0.5, 0.25], device=cuda), conds[0], conds[1], **kw).float()
+    init_random_fast_(m, seed=4)
+    ids = frozenset(id(t) for t in conds)
+    with torch.inference_mode():
+        ref = run()
+        fill = run(transformer_options={"kv_static": ("fill", ids)})
+        assert m.__dict__.get("_kv_static"), "static conditioning store not filled"
+        use = run(transformer_options={"kv_static": ("use", ids)})
+        for t in conds:                           # the next job's conditioning lands in the same tensors
+            t.copy_(torch.randn(t.shape, generator=g).to(**bf))
+        ref2 = run()
+        stale = run(transformer_options={"kv_static": ("use", ids)})
+        assert refresh_static_kv(m, ids) == 1
+        use2 = run(transformer_options={"kv_static": ("use", ids)})
+    tol = 2e-2 * (ref.abs().max().item() + 1)
+    assert (fill - ref).abs().max().item() < tol
+    assert (use - ref).abs().max().item() < tol
+    assert (use2 - ref2).abs().max().item() < tol
+    assert (stale - ref2).abs().max().item() > 10 * (use2 - ref2).abs().max().item()
+
+
 def _run_jobs(patcher, clip, vae, sampler, seeds, steps=4, scheduler="normal"):
     from comfy_gen_server_amd.parallel.dp import Job, generate_local
     out = []
