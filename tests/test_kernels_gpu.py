@@ -984,7 +984,7 @@ def test_cascade_self_attention_two_source_path(cuda, monkeypatch):
         fast = m(*args).float()
         n_fast = ops.stats().get(("attention", "hip"), 0)
         monkeypatch.setattr(SC.OptimizedAttention, "forward_self",
-                            lambda self, xs, kv, residual=None: self.forward(
+                            lambda self, xs, kv, residual=None, kvp=None: self.forward(
                                 xs, torch.cat([xs, kv.to(xs.dtype)], 1), torch.cat([xs, kv.to(xs.dtype)], 1),
                                 residual=residual))
         slow = m(*args).float()
