@@ -44,6 +44,7 @@ struct ConvArgs {
   int kw_m16;          // ceil(65536 / kw)
   ppk::Split sp;       // v7 split-K tail (S <= 1: none)
   float* gnp;          // v6 only: GroupNorm partial statistics out (pq::run GNS), or null
+  int img_rsrc;        // ConvGatherKD: per-image buffer descriptors (an input >= 2 GiB; Ho*Wo % 256 == 0)
 };
 
 // Host: the multiply-shift constants of ConvGatherK (exact for k0 < kh*kw*Cin, kh*kw <= 32).
@@ -422,23 +423,103 @@ struct ConvGatherKB {
   }
 };
 
+// v6's gather: buffer_load ... lds like ConvGatherKB, with the per-lane work cut to the minimum -- per slot
+// the lane keeps the byte offsets of its output pixel's top-left tap in each input (its 16-B chunk folded in)
+// and the in-bounds tap mask; per K-tile the (tap, input, channel) decode is uniform (SALU) and the lane does
+// one add, one bit test and one select. No 64-bit address math and no exec-mask branch per DMA (the old
+// ConvGatherK source ran ~20 instructions with a divergent zero-page branch per slot, which made the conv
+// loop 25-35 % slower than the same main loop on a dense A; profiles/r04/conv_table_r04t.md). A padding tap
+// gets an offset past the descriptor's range and the DMA writes zeros. Offsets are 32-bit (they wrap mod
+// 2^32: a negative top-left pixel offset plus an in-bounds tap offset is exact), so each descriptor spans
+// < 2 GiB: the whole input, or -- img_rsrc, for the VAE's multi-GiB activations -- the one image a 256-row
+// output tile lies in (host: Ho*Wo % 256 == 0), rebuilt per tile by tile().
+struct ConvGatherKD {
+  static constexpr bool kOwnDMA = true;
+  const ConvArgs* a;
+  uint32_t pb1[4], pb2[4], vm[4];
+  __amdgpu_buffer_rsrc_t r1, r2;
+  __device__ __forceinline__ void make(long long n_img, unsigned px) {
+    const unsigned c2 = (unsigned)(a->in2 ? a->Cin - a->C1 : a->C1);
+    r1 = __builtin_amdgcn_make_buffer_rsrc((void*)(a->in + n_img * px * a->C1), 0, (int)(px * (unsigned)a->C1 * 2u),
+                                           0x00020000);
+    r2 = __builtin_amdgcn_make_buffer_rsrc((void*)((a->in2 ? a->in2 : a->in) + n_img * px * c2), 0,
+                                           (int)(px * c2 * 2u), 0x00020000);
+  }
+  __device__ __forceinline__ void init() {
+    if (!a->img_rsrc) make(0, (unsigned)(a->N * a->H * a->W));
+  }
+  __device__ __forceinline__ void tile(int m0) {   // m0: the tile's first output row (uniform)
+    if (a->img_rsrc) make(m0 / (a->Ho * a->Wo), (unsigned)(a->H * a->W));
+  }
+  __device__ __forceinline__ void setup(int s, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    const bool ok = row < M;
+    row = ok ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    const int n = row / hw;
+    const int rem = row - n * hw;
+    const int oy = rem / a->Wo;
+    const int py = oy * a->stride - a->pad, px = (rem - oy * a->Wo) * a->stride - a->pad;
+    const unsigned pix = (unsigned)(((a->img_rsrc ? 0 : n) * a->H + py) * a->W + px);
+    uint32_t m = 0;
+    if (ok) {
+      for (int ky = 0; ky < a->kh; ++ky) {
+        const bool ry = (unsigned)(py + ky) < (unsigned)a->H;
+        for (int kx = 0; kx < a->kw; ++kx)
+          if (ry && (unsigned)(px + kx) < (unsigned)a->W) m |= 1u << (ky * a->kw + kx);
+      }
+    }
+    vm[s] = m;
+    const unsigned ch = 16u * (unsigned)pp::src_chunk8(s & 1);
+    pb1[s] = pix * (2u * (unsigned)a->C1) + ch;
+    pb2[s] = pix * (2u * (unsigned)(a->Cin - a->C1)) + ch;
+  }
+  __device__ __forceinline__ void dma(int s, int k0, unsigned char* dst) const {
+    // uniform decode, written select-free so the compiler keeps it scalar and branch-free
+    const unsigned kq = (unsigned)k0 >> 6;
+    const unsigned tap = __umulhi(kq, a->cq_magic) + (a->cq_magic ? 0u : kq);
+    const int ci0 = k0 - (int)tap * a->Cin;
+    const int ky = (int)((tap * (unsigned)a->kw_m16) >> 16);
+    const int kx = (int)tap - ky * a->kw;
+    const bool second = ci0 >= a->C1;
+    const unsigned cs2 = 2u * (unsigned)(second ? a->Cin - a->C1 : a->C1);
+    const unsigned so = (unsigned)(ky * a->W + kx) * cs2 + 2u * (unsigned)(second ? ci0 - a->C1 : ci0);
+    // lane: bit `tap` of the mask moved to bit 31 and inverted -> a padding tap's offset has bit 31 set
+    // (past every < 2 GiB descriptor range: the DMA writes zeros)
+    const unsigned off = ((second ? pb2[s] : pb1[s]) + so) | (~(vm[s] << (31u - tap)) & 0x80000000u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? r2 : r1, (lds_void*)dst, 16, off, 0, 0, 0);
+  }
+};
+
 static bool conv_fast_ok(const ConvArgs& a) { return !(a.flags & CONV_UP2X) && a.kh * a.kw <= 32; }
 // an input tensor spans >= 2 GiB (v7's ConvGatherKB descriptors need < 2 GiB)
 static bool conv_wide(const ConvArgs& a) {
   const long long px = (long long)a.N * a.H * a.W;
   return px * a.C1 * 2 >= (1ll << 31) || (a.in2 && px * (a.Cin - a.C1) * 2 >= (1ll << 31));
 }
+// ConvGatherKD applies (sets a.img_rsrc): every input < 2 GiB, or each image < 2 GiB with 256-row output
+// tiles that never straddle two images
+static bool conv_kd(ConvArgs& a) {
+  a.img_rsrc = 0;
+  if (!conv_wide(a)) return true;
+  const long long px = (long long)a.H * a.W;
+  const bool img_ok = ((long long)a.Ho * a.Wo) % 256 == 0 && px * a.C1 * 2 < (1ll << 31) &&
+                      (!a.in2 || px * (a.Cin - a.C1) * 2 < (1ll << 31));
+  a.img_rsrc = img_ok ? 1 : 0;
+  return img_ok;
+}
 
+template <bool KD>   // KD: ConvGatherKD (buffer_load ... lds); else ConvGatherK with 64-bit offsets
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v5k_kernel(ConvArgs a) {
-  // (64-bit offsets: v5 keeps VGPR headroom; the VAE's 4-GiB activations take this path)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn;
   grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
-  ConvGatherK<true> al;
+  typename std::conditional<KD, ConvGatherKD, ConvGatherK<true>>::type al;
   al.a = &a;
+  if constexpr (KD) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
 }
@@ -456,6 +537,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
 }
 
+// v5 / v6 loader override for in-process A/B (-1 auto: KD where legal; 1 forces ConvGatherK, 0 ConvGatherA8)
+static int g_conv_v6_ld = -1;
+CGS_EXPORT void cgs_conv_v6_set_loader(int ld) { g_conv_v6_ld = ld; }
+
 static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
@@ -468,23 +553,31 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   if (conv_fast_ok(a)) {
     static bool attr_k = false;
     if (!attr_k) {
-      (void)hipFuncSetAttribute((const void*)conv_nhwc_v5k_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, pp::LDS);
+      (void)hipFuncSetAttribute((const void*)conv_nhwc_v5k_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                pp::LDS);
+      (void)hipFuncSetAttribute((const void*)conv_nhwc_v5k_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                pp::LDS);
       attr_k = true;
     }
     conv_magic(a);
-    conv_nhwc_v5k_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+    if (g_conv_v6_ld != 1 && conv_kd(a)) conv_nhwc_v5k_kernel<true><<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+    else conv_nhwc_v5k_kernel<false><<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
   } else {
     conv_nhwc_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
   }
 }
 
-template <bool FAST, int DS = 0, bool GNS = false>
+// LD: 0 ConvGatherA8 (generic: UP2X, big filters), 1 ConvGatherK (64-bit offsets: an input >= 2 GiB),
+// 2 ConvGatherKD (buffer_load ... lds, the default where it applies)
+template <int LD, int DS = 0, bool GNS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  typename std::conditional<FAST, ConvGatherK<true>, ConvGatherA8>::type al;
+  typename std::conditional<LD == 2, ConvGatherKD,
+                            typename std::conditional<LD == 1, ConvGatherK<true>, ConvGatherA8>::type>::type al;
   al.a = &a;
+  if constexpr (LD == 2) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   e.gnp = a.gnp;
   e.hw = a.Ho * a.Wo;
@@ -504,16 +597,17 @@ static int conv_num_cus() {
 
 int v6_conv_ds();   // gemm.hip: v6 DMA placement for convs (CGS_V6_CONV_DS / cgs_v6_set_mode)
 
-template <bool FAST, int DS, bool GNS = false>
+template <int LD, int DS, bool GNS = false>
 static void conv_v6_launch(ConvArgs& a, int grid, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<FAST, DS, GNS>,
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<LD, DS, GNS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
     attr = true;
   }
-  conv_nhwc_v6_kernel<FAST, DS, GNS><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+  conv_nhwc_v6_kernel<LD, DS, GNS><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
 }
+
 
 static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   const int M = a.N * a.Ho * a.Wo;
@@ -521,32 +615,27 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
   const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
   const int ds = v6_conv_ds();
-  auto go = [&](auto fc) {
-    constexpr bool F = decltype(fc)::value;
+  int ld = conv_fast_ok(a) ? (conv_kd(a) ? 2 : 1) : 0;
+  if (g_conv_v6_ld >= 0 && g_conv_v6_ld < ld) ld = g_conv_v6_ld;
+  if (ld) conv_magic(a);
+  auto go = [&](auto lc) {
+    constexpr int L = decltype(lc)::value;
+    if (a.gnp) {   // GroupNorm statistics epilogue (split-DMA main loop only)
+      conv_v6_launch<L, 51, true>(a, grid, stream);
+      return;
+    }
     switch (ds) {
-      case 0: conv_v6_launch<F, 0>(a, grid, stream); break;
-      case 3: conv_v6_launch<F, 3>(a, grid, stream); break;
-      case 17: conv_v6_launch<F, 17>(a, grid, stream); break;
-      case 19: conv_v6_launch<F, 19>(a, grid, stream); break;
-      case 1: conv_v6_launch<F, 1>(a, grid, stream); break;
-      default: conv_v6_launch<F, 51>(a, grid, stream);
+      case 0: conv_v6_launch<L, 0>(a, grid, stream); break;
+      case 3: conv_v6_launch<L, 3>(a, grid, stream); break;
+      case 17: conv_v6_launch<L, 17>(a, grid, stream); break;
+      case 19: conv_v6_launch<L, 19>(a, grid, stream); break;
+      case 1: conv_v6_launch<L, 1>(a, grid, stream); break;
+      default: conv_v6_launch<L, 51>(a, grid, stream);
     }
   };
-  if (a.gnp) {   // GroupNorm statistics epilogue (split-DMA main loop only)
-    if (conv_fast_ok(a)) {
-      conv_magic(a);
-      conv_v6_launch<true, 51, true>(a, grid, stream);
-    } else {
-      conv_v6_launch<false, 51, true>(a, grid, stream);
-    }
-    return;
-  }
-  if (conv_fast_ok(a)) {
-    conv_magic(a);
-    go(std::true_type{});
-  } else {
-    go(std::false_type{});
-  }
+  if (ld == 2) go(std::integral_constant<int, 2>{});
+  else if (ld == 1) go(std::integral_constant<int, 1>{});
+  else go(std::integral_constant<int, 0>{});
 }
 
 // v7: the persistent 256 x 256 ping-pong with cross-tile prefetch and register epilogue (mfma_ppk.h)

@@ -90,6 +90,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
 
+// A loader that issues its own LDS DMA (``static constexpr bool kOwnDMA``; ``tile(m0)`` at each output tile,
+// ``dma(slot, k0, dst)`` per K-tile -- conv.hip ConvGatherKD's buffer_load ... lds) instead of handing the
+// main loop a global source address (``src(slot, k0)``).
+template <class T, class = void>
+struct own_dma : std::false_type {};
+template <class T>
+struct own_dma<T, std::void_t<decltype(T::kOwnDMA)>> : std::true_type {};
+
 __device__ __forceinline__ void lds_dma16(const void* src, unsigned char* dst) {
   __builtin_amdgcn_global_load_lds(src, (mc_lds_void*)dst, 16, 0, 0);
 }

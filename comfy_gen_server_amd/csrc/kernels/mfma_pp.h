@@ -60,6 +60,7 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   // ---- loader setup: thread t stages part-local rows (t >> 3) and 64 + (t >> 3), chunk t & 7
   const int lrow = tid >> 3;
   const int lch = tid & 7;
+  if constexpr (mc::own_dma<AL>::value) al.tile(m0);
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
@@ -80,12 +81,17 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
     unsigned char* base = smem + (kt & 1) * BUF + part * PART + wave * 1024;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const void* src;
-      if (part == P_A0) src = al.src(0 * 2 + g, k0);
-      else if (part == P_A1) src = al.src(1 * 2 + g, k0);
-      else if (part == P_B0) src = (const void*)(bsrc[0][g] + k0);
-      else src = (const void*)(bsrc[1][g] + k0);
-      mc::lds_dma16(src, base + g * 8192);
+      if constexpr (mc::own_dma<AL>::value) {
+        if (part == P_A0 || part == P_A1) al.dma((part == P_A0 ? 0 : 2) + g, k0, base + g * 8192);
+        else mc::lds_dma16((const void*)(bsrc[part == P_B0 ? 0 : 1][g] + k0), base + g * 8192);
+      } else {
+        const void* src;
+        if (part == P_A0) src = al.src(0 * 2 + g, k0);
+        else if (part == P_A1) src = al.src(1 * 2 + g, k0);
+        else if (part == P_B0) src = (const void*)(bsrc[0][g] + k0);
+        else src = (const void*)(bsrc[1][g] + k0);
+        mc::lds_dma16(src, base + g * 8192);
+      }
     }
   };
 

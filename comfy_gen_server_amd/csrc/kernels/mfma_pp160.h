@@ -99,6 +99,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   const int lch = tid & 7;
   const u16* bsrc[3];
   auto setup = [&](int m0, int n0) {
+    if constexpr (mc::own_dma<AL>::value) al.tile(m0);
 #pragma unroll
     for (int g = 0; g < 4; ++g) al.setup(g, m0 + g * 64 + lrow);
 #pragma unroll
@@ -111,7 +112,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   };
   // A slot g / B row group g of K-tile kt into ring slot `slot`
   auto dma_a = [&](int g, int kt, int slot) {
-    mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * 8192);
+    if constexpr (mc::own_dma<AL>::value) al.dma(g, kt * BK, smem + slot * STAGE + wave * 1024 + g * 8192);
+    else mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * 8192);
   };
   auto dma_b = [&](int g, int kt, int slot) {
     if (g < 2 || grp == 0)   // B rows 128..159: group 0 only

@@ -1,7 +1,10 @@
 """Per-shape conv table on the SDXL bench shapes (UNet batch 16 at 1024^2, VAE decode batch 8):
 every HIP conv variant vs MIOpen (F.conv2d, channels_last) in TF/s.
 
-python -m comfy_gen_server_amd.tools.conv_table [out.md] [--vae]
+python -m comfy_gen_server_amd.tools.conv_table [out.md] [--vae] [--miopen] [--gemm]
+
+``--gemm`` adds the same-sized plain GEMM (M = N*Ho*Wo, N = Cout, K = k*k*Cin; im2col already done) on
+hipBLASLt (torch.mm) and on our GEMM (ops.linear): the rate an implicit-GEMM conv is chasing.
 """
 from __future__ import annotations
 
@@ -40,7 +43,8 @@ VAE = [
     ("vae 256->128 @1024", 8, 1024, 1024, 256, 128, 3, 1),
     ("vae 128 @1024", 8, 1024, 1024, 128, 128, 3, 1),
 ]
-VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v7": 7, "v7s": 8}   # v7s: v7 + split-K tail
+# v7s: v7 + split-K tail; v6k: v6 with the older per-lane-address gather (ConvGatherK) instead of ConvGatherKD
+VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v6k": 16, "v7": 7, "v7s": 8}
 
 
 def _time(fn, iters):
@@ -61,9 +65,11 @@ def main(argv):
     lib = _native.load_kernels()
     dev = torch.device("cuda", 0)
     shapes = UNET + (VAE if "--vae" in argv else [])
-    argv = [a for a in argv if a not in ("--vae", "--miopen")]
-    rows = ["| conv | N | HxW | Cin | Cout | k/s | " + " | ".join(f"{v} TF/s" for v in VARIANTS) + " | MIOpen TF/s |",
-            "|---|---:|---|---:|---:|---|" + "---:|" * (len(VARIANTS) + 1)]
+    gemm = "--gemm" in argv
+    argv = [a for a in argv if a not in ("--vae", "--miopen", "--gemm")]
+    rows = ["| conv | N | HxW | Cin | Cout | k/s | " + " | ".join(f"{v} TF/s" for v in VARIANTS) + " | MIOpen TF/s |"
+            + (" GEMM hipBLASLt | GEMM ours | GEMM v6 |" if gemm else ""),
+            "|---|---:|---|---:|---:|---|" + "---:|" * (len(VARIANTS) + 1 + 3 * gemm)]
     for name, N, H, W, Cin, Cout, k, s in shapes:
         p = k // 2
         x = (torch.rand(N, Cin, H, W, device=dev) * 2 - 1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -80,6 +86,14 @@ def main(argv):
         ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
         for vn, v in VARIANTS.items():
             def run(v=v):
+                if v == 16:
+                    lib.cgs_conv_v6_set_loader(1)
+                    try:
+                        return lib.cgs_conv2d_nhwc_v(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
+                                                     out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0, 6,
+                                                     core._stream())
+                    finally:
+                        lib.cgs_conv_v6_set_loader(-1)
                 if v == 8:
                     return lib.cgs_conv2d_nhwc_v7ws(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
                                                     out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0,
@@ -101,9 +115,27 @@ def main(argv):
             res["miopen"] = flops / ms / 1e9
         else:
             res["miopen"] = float("nan")
+        extra = ""
+        if gemm:
+            del ws
+            ws = None
+            A = torch.empty(N * Ho * Wo, k * k * Cin, device=dev, dtype=torch.bfloat16).uniform_(-1, 1)
+            Wt = w.reshape(Cout, -1).contiguous()
+            t_lib = _time(lambda: torch.mm(A, Wt.t()), it)
+            t_our = _time(lambda: core.linear(A, Wt, b), it)
+            Cg = torch.empty(A.shape[0], Cout, device=dev, dtype=torch.bfloat16)
+            Kg = A.shape[1]
+
+            def v6():   # the conv's v6 main loop on a row-major A (the im2col-free loader's cost is the difference)
+                return lib.cgs_gemm_bf16_v(A.data_ptr(), Wt.data_ptr(), Cg.data_ptr(), b.data_ptr(), None, A.shape[0],
+                                           Cout, Kg, Kg, Kg, Cout, 0, 1, 1.0, 6, core._stream())
+            t_v6 = _time(v6, it) if Cout % 160 == 0 and v6() == 0 else float("nan")
+            extra = f" {flops / t_lib / 1e9:.0f} | {flops / t_our / 1e9:.0f} | {flops / t_v6 / 1e9:.0f} |"
+            del Cg
+            del A
         rows.append(f"| {name} | {N} | {H}x{W} | {Cin} | {Cout} | {k}/{s} | " +
                     " | ".join("bad" if res[v] == -1.0 else f"{res[v]:.0f}" for v in VARIANTS) +
-                    f" | {res['miopen']:.0f} |")
+                    f" | {res['miopen']:.0f} |" + extra)
         print(rows[-1], flush=True)
         del x, w, wn, out, ws
     text = "\n".join(rows)
