@@ -491,6 +491,63 @@ struct ConvGatherKD {
   }
 };
 
+// ConvGatherKD for the nearest-2x-upsampled input (CONV_UP2X, single input): the source pixel of tap (ky, kx)
+// is ((py + ky) >> 1, (px + kx) >> 1) -- not an affine function of the tap, so the lane keeps its top-left
+// (py, px) in upsampled coordinates and its image's base offset, and does two adds, two shifts and two
+// 24-bit multiply-adds per DMA (still no branch; a padding tap sets bit 31 as in ConvGatherKD).
+struct ConvGatherKU {
+  static constexpr bool kOwnDMA = true;
+  const ConvArgs* a;
+  uint32_t pb[4], vm[4];
+  int py[4], px[4];
+  __amdgpu_buffer_rsrc_t r1;
+  __device__ __forceinline__ void make(long long n_img, unsigned pixels) {
+    r1 = __builtin_amdgcn_make_buffer_rsrc((void*)(a->in + n_img * pixels * a->C1), 0,
+                                           (int)(pixels * (unsigned)a->C1 * 2u), 0x00020000);
+  }
+  __device__ __forceinline__ void init() {
+    if (!a->img_rsrc) make(0, (unsigned)(a->N * a->H * a->W));
+  }
+  __device__ __forceinline__ void tile(int m0) {
+    if (a->img_rsrc) make(m0 / (a->Ho * a->Wo), (unsigned)(a->H * a->W));
+  }
+  __device__ __forceinline__ void setup(int s, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    const bool ok = row < M;
+    row = ok ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    const int n = row / hw;
+    const int rem = row - n * hw;
+    const int oy = rem / a->Wo;
+    const int y0 = oy * a->stride - a->pad, x0 = (rem - oy * a->Wo) * a->stride - a->pad;
+    uint32_t m = 0;
+    if (ok) {
+      for (int ky = 0; ky < a->kh; ++ky) {
+        const bool ry = (unsigned)(y0 + ky) < (unsigned)(2 * a->H);
+        for (int kx = 0; kx < a->kw; ++kx)
+          if (ry && (unsigned)(x0 + kx) < (unsigned)(2 * a->W)) m |= 1u << (ky * a->kw + kx);
+      }
+    }
+    vm[s] = m;
+    py[s] = y0;
+    px[s] = x0;
+    pb[s] = (unsigned)(a->img_rsrc ? 0 : n) * (unsigned)(a->H * a->W) * (2u * (unsigned)a->C1) +
+            16u * (unsigned)pp::src_chunk8(s & 1);
+  }
+  __device__ __forceinline__ void dma(int s, int k0, unsigned char* dst) const {
+    const unsigned kq = (unsigned)k0 >> 6;
+    const unsigned tap = __umulhi(kq, a->cq_magic) + (a->cq_magic ? 0u : kq);
+    const int ci0 = k0 - (int)tap * a->Cin;
+    const int ky = (int)((tap * (unsigned)a->kw_m16) >> 16);
+    const int kx = (int)tap - ky * a->kw;
+    const unsigned iy = (unsigned)((py[s] + ky) >> 1) & 0xffffu, ix = (unsigned)((px[s] + kx) >> 1) & 0xffffu;
+    const unsigned pix = __umul24(iy, (unsigned)a->W) + ix;
+    const unsigned off = (pix * (2u * (unsigned)a->C1) + pb[s] + 2u * (unsigned)ci0) |
+                         (~(vm[s] << (31u - tap)) & 0x80000000u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_void*)dst, 16, off, 0, 0, 0);
+  }
+};
+
 static bool conv_fast_ok(const ConvArgs& a) { return !(a.flags & CONV_UP2X) && a.kh * a.kw <= 32; }
 // an input tensor spans >= 2 GiB (v7's ConvGatherKB descriptors need < 2 GiB)
 static bool conv_wide(const ConvArgs& a) {
@@ -501,6 +558,7 @@ static bool conv_wide(const ConvArgs& a) {
 // tiles that never straddle two images
 static bool conv_kd(ConvArgs& a) {
   a.img_rsrc = 0;
+  if ((a.flags & CONV_UP2X) && (a.in2 || a.kh * a.kw > 32 || a.H >= 32768 || a.W >= 32768)) return false;
   if (!conv_wide(a)) return true;
   const long long px = (long long)a.H * a.W;
   const bool img_ok = ((long long)a.Ho * a.Wo) % 256 == 0 && px * a.C1 * 2 < (1ll << 31) &&
@@ -524,6 +582,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
 }
 
+template <bool KU>   // KU: the upsample-aware buffer gather (ConvGatherKU); else the generic ConvGatherA8
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v5_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
@@ -531,8 +590,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn;
   grouped_tile(logical, gridDim.x / a.tiles_n, a.tiles_n, a.group_m, tm, tn);
-  ConvGatherA8 al;
+  typename std::conditional<KU, ConvGatherKU, ConvGatherA8>::type al;
   al.a = &a;
+  if constexpr (KU) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
 }
@@ -544,7 +604,10 @@ CGS_EXPORT void cgs_conv_v6_set_loader(int ld) { g_conv_v6_ld = ld; }
 static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v5_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, pp::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v5_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pp::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v5_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pp::LDS);
     attr = true;
   }
   const int M = a.N * a.Ho * a.Wo;
@@ -562,8 +625,11 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
     conv_magic(a);
     if (g_conv_v6_ld != 1 && conv_kd(a)) conv_nhwc_v5k_kernel<true><<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
     else conv_nhwc_v5k_kernel<false><<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+  } else if ((a.flags & CONV_UP2X) && g_conv_v6_ld != 0 && conv_kd(a)) {
+    conv_magic(a);
+    conv_nhwc_v5_kernel<true><<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
   } else {
-    conv_nhwc_v5_kernel<<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
+    conv_nhwc_v5_kernel<false><<<(unsigned)nwg, pp::THREADS, pp::LDS, stream>>>(a);
   }
 }
 
@@ -574,10 +640,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  typename std::conditional<LD == 2, ConvGatherKD,
-                            typename std::conditional<LD == 1, ConvGatherK<true>, ConvGatherA8>::type>::type al;
+  typename std::conditional<
+      LD == 3, ConvGatherKU,
+      typename std::conditional<LD == 2, ConvGatherKD,
+                                typename std::conditional<LD == 1, ConvGatherK<true>, ConvGatherA8>::type>::type>::type al;
   al.a = &a;
-  if constexpr (LD == 2) al.init();
+  if constexpr (LD >= 2) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   e.gnp = a.gnp;
   e.hw = a.Ho * a.Wo;
@@ -615,8 +683,8 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
   const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
   const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
   const int ds = v6_conv_ds();
-  int ld = conv_fast_ok(a) ? (conv_kd(a) ? 2 : 1) : 0;
-  if (g_conv_v6_ld >= 0 && g_conv_v6_ld < ld) ld = g_conv_v6_ld;
+  int ld = conv_fast_ok(a) ? (conv_kd(a) ? 2 : 1) : ((a.flags & CONV_UP2X) && conv_kd(a) ? 3 : 0);
+  if (g_conv_v6_ld >= 0 && g_conv_v6_ld < ld) ld = ld == 3 ? 0 : g_conv_v6_ld;
   if (ld) conv_magic(a);
   auto go = [&](auto lc) {
     constexpr int L = decltype(lc)::value;
@@ -633,7 +701,8 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
       default: conv_v6_launch<L, 51>(a, grid, stream);
     }
   };
-  if (ld == 2) go(std::integral_constant<int, 2>{});
+  if (ld == 3) go(std::integral_constant<int, 3>{});
+  else if (ld == 2) go(std::integral_constant<int, 2>{});
   else if (ld == 1) go(std::integral_constant<int, 1>{});
   else go(std::integral_constant<int, 0>{});
 }

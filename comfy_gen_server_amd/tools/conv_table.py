@@ -32,6 +32,8 @@ UNET = [  # (name, N, H, W, Cin, Cout, k, stride)
     ("up conv 1280 @64", 16, 64, 64, 1280, 1280, 3, 1),
     ("up conv 640 @128", 16, 128, 128, 640, 640, 3, 1),
     ("skip 1x1 960->320", 16, 128, 128, 960, 320, 1, 1),
+    ("2x-up conv 1280 32->64", 16, 32, 32, 1280, 1280, 3, 1),     # "2x": input read through nearest-2x
+    ("2x-up conv 640 64->128", 16, 64, 64, 640, 640, 3, 1),
 ]
 VAE = [
     ("vae 512 @128", 8, 128, 128, 512, 512, 3, 1),
@@ -42,6 +44,8 @@ VAE = [
     ("vae 256 @1024", 8, 1024, 1024, 256, 256, 3, 1),
     ("vae 256->128 @1024", 8, 1024, 1024, 256, 128, 3, 1),
     ("vae 128 @1024", 8, 1024, 1024, 128, 128, 3, 1),
+    ("vae 2x-up 512 128->256", 8, 128, 128, 512, 512, 3, 1),
+    ("vae 2x-up 256 512->1024", 8, 512, 512, 256, 256, 3, 1),
 ]
 # v7s: v7 + split-K tail; v6k: v6 with the older per-lane-address gather (ConvGatherK) instead of ConvGatherKD
 VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v6k": 16, "v7": 7, "v7s": 8}
@@ -72,15 +76,19 @@ def main(argv):
             "|---|---:|---|---:|---:|---|" + "---:|" * (len(VARIANTS) + 1 + 3 * gemm)]
     for name, N, H, W, Cin, Cout, k, s in shapes:
         p = k // 2
+        up = "2x" in name
+        fl = 16 if up else 0
         x = (torch.rand(N, Cin, H, W, device=dev) * 2 - 1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         w = ((torch.rand(Cout, Cin, k, k, device=dev) * 2 - 1) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
         wn = w.permute(0, 2, 3, 1).contiguous()
         b = torch.zeros(Cout, device=dev, dtype=torch.bfloat16)
-        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        Hl, Wl = (2 * H, 2 * W) if up else (H, W)
+        Ho, Wo = (Hl + 2 * p - k) // s + 1, (Wl + 2 * p - k) // s + 1
         out = torch.empty(N, Cout, Ho, Wo, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
         flops = 2.0 * N * Ho * Wo * Cout * Cin * k * k
         it = max(2, int(3e11 / flops))
-        ref = F.conv2d(x[:1].float(), w.float(), b.float(), s, p)
+        x1 = x[:1].float()
+        ref = F.conv2d(F.interpolate(x1, scale_factor=2, mode="nearest") if up else x1, w.float(), b.float(), s, p)
         res = {}
         nws = lib.cgs_v7_ws_bytes(N * Ho * Wo, Cout, k * k * Cin)
         ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
@@ -90,16 +98,16 @@ def main(argv):
                     lib.cgs_conv_v6_set_loader(1)
                     try:
                         return lib.cgs_conv2d_nhwc_v(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
-                                                     out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0, 6,
+                                                     out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, fl, 6,
                                                      core._stream())
                     finally:
                         lib.cgs_conv_v6_set_loader(-1)
                 if v == 8:
                     return lib.cgs_conv2d_nhwc_v7ws(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
-                                                    out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0,
+                                                    out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, fl,
                                                     ws.data_ptr(), nws, core._stream())
                 return lib.cgs_conv2d_nhwc_v(x.data_ptr(), None, Cin, wn.data_ptr(), b.data_ptr(), None,
-                                             out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, 0, v,
+                                             out.data_ptr(), N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, fl, v,
                                              core._stream())
             try:
                 if run() != 0:
@@ -111,12 +119,13 @@ def main(argv):
             except Exception:
                 res[vn] = float("nan")
         if "--miopen" in sys.argv:
-            ms = _time(lambda: F.conv2d(x, w, b, s, p), it)
+            ms = _time(lambda: F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest") if up else x, w, b, s, p),
+                       it)
             res["miopen"] = flops / ms / 1e9
         else:
             res["miopen"] = float("nan")
         extra = ""
-        if gemm:
+        if gemm and not up:
             del ws
             ws = None
             A = torch.empty(N * Ho * Wo, k * k * Cin, device=dev, dtype=torch.bfloat16).uniform_(-1, 1)
@@ -133,6 +142,8 @@ def main(argv):
             extra = f" {flops / t_lib / 1e9:.0f} | {flops / t_our / 1e9:.0f} | {flops / t_v6 / 1e9:.0f} |"
             del Cg
             del A
+        elif gemm:
+            extra = " | | |"
         rows.append(f"| {name} | {N} | {H}x{W} | {Cin} | {Cout} | {k}/{s} | " +
                     " | ".join("bad" if res[v] == -1.0 else f"{res[v]:.0f}" for v in VARIANTS) +
                     f" | {res['miopen']:.0f} |" + extra)
