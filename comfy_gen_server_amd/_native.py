@@ -185,12 +185,15 @@ KERNEL_SIGNATURES = {
     "cgs_w4_set_group": [_I],
     # experiment: 4-slot-ring one-wave-per-SIMD GEMM (bias / residual epilogue only)
     "cgs_gemm_bf16_w5": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
+    # skinny GEMM (M <= 128) with its split-K workspace
+    "cgs_gemm_skinny_ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
+    "cgs_gemm_skinny_ws_bytes": [_I, _I, _I],
     # v6 conv gather override (-1 auto, 1 ConvGatherK, 0 ConvGatherA8): in-process A/B
     "cgs_conv_v6_set_loader": [_I],
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
             "cgs_attn_set_variant": None, "cgs_w4_set_group": None,
             "cgs_conv_v6_set_loader": None}

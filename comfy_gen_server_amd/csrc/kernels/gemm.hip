@@ -740,12 +740,16 @@ CGS_EXPORT long long cgs_v7_ws_bytes(int M, int N, int K) {
 // through LDS, bias / residual epilogue. Needs K % 32 == 0 and 16-B aligned rows.
 constexpr int SK_WAVES = 8;
 
+// Split-K form (part != null): gridDim.y = S slices of the K-steps; slice s writes its fp32 partial sums to
+// part[s][row][col] and gemm_skinny_reduce_kernel adds the S slices and applies the epilogue. The 16-column
+// grid alone is N / 16 workgroups -- 80 for N = 1280 (CLIP-G fc2 / out-proj at K = 5120 / 1280 ran ~30 % of
+// the CUs for 40-80 us); the slices fill the chip.
 template <int MR>
 __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(const u16* __restrict__ A, const u16* __restrict__ W,
                                                           u16* __restrict__ C, const u16* __restrict__ bias,
                                                           const u16* __restrict__ R, int M, int N, int K, long long lda,
                                                           long long ldw, long long ldc, long long ldr, int epi,
-                                                          float alpha) {
+                                                          float alpha, float* __restrict__ part = nullptr) {
   __shared__ f32x4 red[SK_WAVES][MR][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16;
@@ -758,8 +762,11 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(const u16* _
   f32x4 acc[MR];
 #pragma unroll
   for (int mr = 0; mr < MR; ++mr) acc[mr] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nks = K / 32;
-  int ks = wave;
+  const int nks_all = K / 32;
+  const int per = (nks_all + gridDim.y - 1) / gridDim.y;
+  const int ks0 = blockIdx.y * per;
+  const int nks = min(nks_all, ks0 + per);
+  int ks = ks0 + wave;
   if (ks < nks) {
     bf16x8 a[MR], b;
     b = *reinterpret_cast<const bf16x8*>(wp + ks * 32);
@@ -783,13 +790,21 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(const u16* _
   __syncthreads();
   const int col = n0 + fr;
   float bv = 0.f;
-  if ((epi & EPI_BIAS) && col < N) bv = bf2f(bias[col]);
+  if (!part && (epi & EPI_BIAS) && col < N) bv = bf2f(bias[col]);
 #pragma unroll
   for (int mr = 0; mr < MR; ++mr) {
     if ((mr % SK_WAVES) != wave) continue;
     f32x4 v = red[0][mr][lane];
 #pragma unroll
     for (int w = 1; w < SK_WAVES; ++w) v += red[w][mr][lane];
+    if (part) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mr * 16 + fq * 4 + r;
+        if (row < M && col < N) part[((long long)blockIdx.y * M + row) * N + col] = v[r];
+      }
+      continue;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = mr * 16 + fq * 4 + r;
@@ -803,14 +818,50 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(const u16* _
   }
 }
 
+// S partial slices + epilogue: out[row][col] = epi(sum_s part[s][row][col])
+__global__ __launch_bounds__(256) void gemm_skinny_reduce_kernel(const float* __restrict__ part, u16* __restrict__ C,
+                                                                 const u16* __restrict__ bias, const u16* __restrict__ R,
+                                                                 int M, int N, int S, long long ldc, long long ldr,
+                                                                 int epi, float alpha) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)M * N) return;
+  const int row = (int)(i / N), col = (int)(i - (long long)row * N);
+  float o = 0.f;
+  for (int s = 0; s < S; ++s) o += part[(long long)s * M * N + i];
+  o *= alpha;
+  if (epi & EPI_BIAS) o += bf2f(bias[col]);
+  if (epi & EPI_GELU) o = gelu_sig(o);
+  if (epi & EPI_RESIDUAL) o += bf2f(R[(long long)row * ldr + col]);
+  C[(long long)row * ldc + col] = f2bf(o);
+}
+
+// K-slices for the skinny kernel: fill ~2 waves of workgroups per CU, >= 8 K-steps per slice, <= 8 slices.
+// Only for long K (>= 4096: CLIP-G fc2 29 -> 22 us); below that the second launch costs more than the
+// slices save (profiles/r04/skinny_split_ab.log).
+static int skinny_splits(int M, int N, int K) {
+  if (M > 128 || K % 32 || K < 4096) return 1;
+  const int wgs = (N + 15) / 16, nks = K / 32;
+  int S = (512 + wgs - 1) / wgs;
+  S = S < nks / 8 ? S : nks / 8;
+  return S < 2 ? 1 : (S > 8 ? 8 : S);
+}
+
+CGS_EXPORT long long cgs_gemm_skinny_ws_bytes(int M, int N, int K) {
+  const int S = skinny_splits(M, N, K);
+  return S > 1 ? (long long)S * M * N * 4 : 0;
+}
+
 static int gemm_skinny_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                               int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                              hipStream_t stream) {
-  const unsigned g = (unsigned)((N + 15) / 16);
+                              hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
+  const int S = skinny_splits(M, N, K);
+  const bool split = S > 1 && ws && ws_bytes >= (long long)S * M * N * 4;
+  const dim3 g((unsigned)((N + 15) / 16), split ? (unsigned)S : 1u);
+  float* part = split ? (float*)ws : nullptr;
   const int mr = (M + 15) / 16;
 #define CGS_SKINNY(MRV)                                                                                          \
   gemm_skinny_kernel<MRV><<<g, 64 * SK_WAVES, 0, stream>>>((const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias,         \
-                                                 (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha)
+                                                 (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, part)
   switch (mr) {
     case 0: CGS_SKINNY(1); break;
     case 2: CGS_SKINNY(2); break;
@@ -822,7 +873,23 @@ static int gemm_skinny_launch(const void* A, const void* W, void* C, const void*
     default: CGS_SKINNY(8); break;
   }
 #undef CGS_SKINNY
+  if (split) {
+    const long long n = (long long)M * N;
+    gemm_skinny_reduce_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(
+        part, (u16*)C, (const u16*)bias, (const u16*)R, M, N, S, ldc, ldr, epi, alpha);
+  }
   return (int)hipGetLastError();
+}
+
+// The skinny GEMM with its split-K workspace (ws from the caller's allocator, >= cgs_gemm_skinny_ws_bytes).
+CGS_EXPORT int cgs_gemm_skinny_ws(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                                  int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                                  float alpha, void* ws, long long ws_bytes, hipStream_t stream) {
+  if (M > 128 || K % 32 || lda % 8 || ldw % 8 || (((uintptr_t)A | (uintptr_t)W) % 16) ||
+      (epi & (EPI_GEGLU | EPI_F32OUT | EPI_LNFOLD)))
+    return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0) return 0;
+  return gemm_skinny_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, ws, ws_bytes);
 }
 
 static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 waves), 4 = v3 (8 waves), 5 = v5 ping-pong

@@ -70,6 +70,19 @@ def _v7_ws(M: int, N: int, K: int, device):
     return torch.empty(n, dtype=torch.uint8, device=device) if n else None
 
 
+_SKWS: dict = {}
+
+
+def _skinny_ws(M: int, N: int, K: int, device):
+    """Split-K workspace of the skinny (M <= 128) GEMM, from the caching allocator; None = no split."""
+    n = _SKWS.get((M, N, K))
+    if n is None:
+        n = int(_lib().cgs_gemm_skinny_ws_bytes(M, N, K)) if _native.has_kernel("cgs_gemm_skinny_ws_bytes") \
+            and os.environ.get("CGS_SKINNY_SPLIT", "1") != "0" else 0
+        _SKWS[(M, N, K)] = n
+    return torch.empty(n, dtype=torch.uint8, device=device) if n else None
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, act: str | None = None,
            out: torch.Tensor | None = None) -> torch.Tensor:
@@ -113,6 +126,13 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
 
         def run_hip(variant):
             o = dst if dst is not None else torch.empty((M, N), device=x.device, dtype=x.dtype)
+            if M <= 128 and variant in (-1, -2) and K % 32 == 0 and (a.data_ptr() | w.data_ptr()) % 16 == 0:
+                ws = _skinny_ws(M, N, K, x.device)     # split-K slices when N / 16 workgroups underfill
+                if ws is not None:
+                    _check(_lib().cgs_gemm_skinny_ws(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),
+                                                     M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
+                                                     ws.data_ptr(), ws.numel(), _stream()), "cgs_gemm_skinny_ws")
+                    return o
             ws = _v7_ws(M, N, K, x.device) if variant == 7 else None
             if ws is not None:
                 _check(_lib().cgs_gemm_bf16_v7ws(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),

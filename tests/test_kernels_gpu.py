@@ -764,24 +764,30 @@ def test_transformer_block_lnfold_matches_unfolded(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N,K", [(77, 3840, 1280), (16, 1280, 1280), (1, 320, 1280), (77, 768, 3072), (128, 200, 96),
-                                   (100, 5120, 1280), (33, 8, 64)])
-@pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
+                                   (100, 5120, 1280), (33, 8, 64), (77, 1280, 5120), (77, 1280, 1280)])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_res", "bias_gelu"])
 def test_gemm_skinny(cuda, M, N, K, epi):
     """Skinny-M GEMM (one prompt through CLIP, time-embedding projections): one workgroup per 16
-    columns, K split over 4 waves, vs fp32 torch."""
+    columns, K split over the 8 waves -- and, where N / 16 workgroups underfill the chip, over S K-slices
+    (fp32 partials + a reduce/epilogue kernel: cgs_gemm_skinny_ws) -- vs fp32 torch."""
     torch.manual_seed(2)
     a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
     w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
     b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
     r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
-    y = ops.linear(a, w, b, residual=r)
+    gelu = epi == "bias_gelu"
+    y = ops.linear(a, w, b, residual=r, act="gelu" if gelu else None)
     ref = a.float() @ w.float().t()
     if b is not None:
         ref = ref + b.float()
+    if gelu:
+        ref = torch.nn.functional.gelu(ref)
     if r is not None:
         ref = ref + r.float()
     assert ops.stats().get(("gemm", "hip"), 0) == 1
     assert _rel(y, ref) < 1e-2
+    if (M, N, K) == (77, 1280, 5120):
+        assert core._SKWS.get((M, N, K), 0) > 0     # takes the split-K form
 
 
 def test_attention_underfilled_grid_autotuned(cuda, monkeypatch):
