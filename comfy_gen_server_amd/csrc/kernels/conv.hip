@@ -597,8 +597,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   pp::tile(al, a.w, K, M, a.Cout, K, tm * pp::BM, tn * pp::BN, e, smem);
 }
 
-// v5 / v6 loader override for in-process A/B (-1 auto: KD where legal; 1 forces ConvGatherK, 0 ConvGatherA8)
-static int g_conv_v6_ld = -1;
+// v5 / v6 loader override for A/B (-1 auto: KD / KU where legal; 1 forces ConvGatherK, 0 ConvGatherA8):
+// CGS_CONV_LOADER at load, cgs_conv_v6_set_loader() after
+static int conv_loader_env() {
+  const char* v = getenv("CGS_CONV_LOADER");
+  return v ? atoi(v) : -1;
+}
+static int g_conv_v6_ld = conv_loader_env();
 CGS_EXPORT void cgs_conv_v6_set_loader(int ld) { g_conv_v6_ld = ld; }
 
 static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
