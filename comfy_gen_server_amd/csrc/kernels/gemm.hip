@@ -539,6 +539,31 @@ struct DenseA32 {
   __device__ __forceinline__ void dma(int slot, int k0, unsigned char* dst) const { mc::lds_dma16(src(slot, k0), dst); }
 };
 
+// DenseA8's buffer-descriptor form (v6 DS & 64): per-slot row byte offsets fixed per tile, the K offset in
+// the SGPR soffset -- the DMA needs no address VALU. Host: M * lda * 2 < 2 GiB. Measured against the
+// pointer form (with DS & 128, the same for B): -5..+8 % per shape, no consistent gain on the GEMMs
+// (profiles/r04/v6_buffer_dma_ab_r04ae.log; unlike the conv gathers, whose per-DMA address work was 5x
+// larger) -- kept as CGS_V6_DS modes 65 / 129 / 193, default off.
+struct DenseKB {
+  static constexpr bool kOwnDMA = true;
+  const u16* A;
+  long long lda;
+  int M;
+  uint32_t off[4];
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ void init() {
+    r = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)((long long)M * lda * 2), 0x00020000);
+  }
+  __device__ __forceinline__ void tile(int) {}
+  __device__ __forceinline__ void setup(int slot, int row) {
+    row = row < M ? row : M - 1;
+    off[slot] = (uint32_t)(((long long)row * lda + 8 * pp::src_chunk8(slot & 1)) * 2);
+  }
+  __device__ __forceinline__ void dma(int slot, int k0, unsigned char* dst) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (mc_lds_void*)dst, 16, off[slot], k0 * 2, 0, 0);
+  }
+};
+
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
 template <bool LN = false, int DS = 0, bool GG = false, bool ACT = false>
@@ -549,9 +574,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // 64-bit operand pointers: the 32-bit-offset (saddr) DMA form measured 3-10 % slower on v6
   // (profiles/r03/v6_offsets32.log)
-  DenseA8 al{A, lda, M, {}};
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
-  pq::run<DenseA8, LN, DS, false, GG, ACT>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  if constexpr ((DS & 64) != 0) {
+    DenseKB al;
+    al.A = A;
+    al.lda = lda;
+    al.M = M;
+    al.init();
+    pq::run<DenseKB, LN, DS, false, GG, ACT>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  } else {
+    DenseA8 al{A, lda, M, {}};
+    pq::run<DenseA8, LN, DS, false, GG, ACT>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  }
 }
 static int num_cus() {
   static int n = 0;
@@ -603,7 +637,9 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   const int tiles_m = (M + pq::BM - 1) / pq::BM;
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
-  const int ds = v6_ds();
+  int ds = v6_ds();
+  if ((long long)M * lda * 2 >= (1ll << 31)) ds &= ~64;    // buffer-descriptor forms need < 2 GiB operands
+  if ((long long)N * ldw * 2 >= (1ll << 31)) ds &= ~128;
   if (epi & EPI_GELU) {    // GELU epilogue: plain or LayerNorm-folded form (no GEGLU)
     if (epi & EPI_GEGLU) return (int)hipErrorInvalidValue;
     if (epi & EPI_LNFOLD)
@@ -630,6 +666,9 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
       case 3: gemm_v6_go<L, 3>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
       case 17: gemm_v6_go<L, 17>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
       case 19: gemm_v6_go<L, 19>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      case 65: gemm_v6_go<L, 65>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      case 129: gemm_v6_go<L, 129>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
+      case 193: gemm_v6_go<L, 193>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs); break;
       default: gemm_v6_go<L, 1>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m, tiles_n, stream, rs, cs);
     }
   };

@@ -98,6 +98,14 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   const int lrow = tid >> 3;
   const int lch = tid & 7;
   const u16* bsrc[3];
+  // DS & 128: B DMAs through a buffer descriptor (per-row byte offsets fixed per tile, the K offset in the
+  // SGPR soffset: no per-DMA address VALU). Host: N * ldw * 2 < 2 GiB.
+  uint32_t boff[3];
+  __amdgpu_buffer_rsrc_t wr;
+  if constexpr ((DS & 128) != 0)
+    wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, (int)((long long)N * ldw * 2 < 0x7fffffffll ? N * ldw * 2
+                                                                                               : 0x7fffffff),
+                                           0x00020000);
   auto setup = [&](int m0, int n0) {
     if constexpr (mc::own_dma<AL>::value) al.tile(m0);
 #pragma unroll
@@ -107,7 +115,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       const int r = g * 64 + lrow;
       int n = n0 + (GG ? gg_row160(r < BN ? r : BN - 1) : b_col160(r < BN ? r : BN - 1));
       n = n < N ? n : N - 1;
-      bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
+      if constexpr ((DS & 128) != 0) boff[g] = (uint32_t)(((long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7))) * 2);
+      else bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
     }
   };
   // A slot g / B row group g of K-tile kt into ring slot `slot`
@@ -116,8 +125,13 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     else mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * 8192);
   };
   auto dma_b = [&](int g, int kt, int slot) {
-    if (g < 2 || grp == 0)   // B rows 128..159: group 0 only
-      mc::lds_dma16((const void*)(bsrc[g] + kt * BK), smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192);
+    if (g < 2 || grp == 0) {  // B rows 128..159: group 0 only
+      if constexpr ((DS & 128) != 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (mc_lds_void*)(smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192),
+                                                 16, boff[g], kt * BK * 2, 0, 0);
+      else
+        mc::lds_dma16((const void*)(bsrc[g] + kt * BK), smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192);
+    }
   };
   // the phase-0 (part 0) / phase-1 (part 1) DMAs of K-tile kt: DS & 3 = 0 all in phase 0, 1 A | B,
   // 2 B | A, 3 balanced (A0 A1 B0 | A2 A3 B1 B2)

@@ -1,7 +1,10 @@
 """In-process interleaved A/B of the GEMM kernels on the SDXL shapes (one wave per SIMD "w4" vs the 8-wave
 v6 / v7 kernels vs hipBLASLt through ATen), with an fp32 numerics check of every HIP variant.
 
-python -m comfy_gen_server_amd.tools.gemm_ab [out.md] [--rounds R] [--iters N] [--shapes a,b,...]
+python -m comfy_gen_server_amd.tools.gemm_ab [out.md] [--rounds R] [--iters N] [--shapes a,b,...] [--v6modes 1,65]
+
+``--v6modes``: extra columns "v6m<m>" = v6 under cgs_v6_set_mode(m) (pq::run DS bits; 64 / 128 = A / B DMAs
+through buffer descriptors), interleaved with the others in the same rounds.
 
 Rows are (name, M, N, K, epilogue): epilogue "" plain + bias, "res" + residual, "geglu" (16-row
 interleaved a/g weights, N/2 outputs), "ln" (LayerNorm folded in, W' = W * gamma), "ln:geglu".
@@ -52,6 +55,7 @@ def main(argv):
     from comfy_gen_server_amd import _native
     from comfy_gen_server_amd.ops import core
     rounds, iters, only = 3, 10, None
+    v6modes = []
     out_md = None
     i = 0
     while i < len(argv):
@@ -61,6 +65,8 @@ def main(argv):
             iters = int(argv[i + 1]); i += 2
         elif argv[i] == "--shapes":
             only = set(argv[i + 1].split(",")); i += 2
+        elif argv[i] == "--v6modes":
+            v6modes = [int(v) for v in argv[i + 1].split(",")]; i += 2
         else:
             out_md = argv[i]; i += 1
     lib = _native.load_kernels()
@@ -136,6 +142,15 @@ def main(argv):
             f = var(v)
             if f() == 0:
                 cands[vn] = f
+        for m in v6modes:
+            def fm(m=m, f6=var(6)):
+                lib.cgs_v6_set_mode(m)
+                try:
+                    return f6()
+                finally:
+                    lib.cgs_v6_set_mode(-1)
+            if fm() == 0:
+                cands[f"v6m{m}"] = fm
         cands["lib"] = lambda: F.linear(a, w, b)
         for vn, f in cands.items():
             if vn == "lib":
@@ -159,7 +174,8 @@ def main(argv):
                 f"{cell('v7')} | {cell('lib')} | {best_w4 / other:.3f} | "
                 f"{max([v for k, v in errs.items() if k.startswith(('w4', 'w5'))] or [0.0]):.2e} |")
         rows.append(line)
-        print(line, " errs:", {k: f"{v:.1e}" for k, v in errs.items()}, flush=True)
+        print(line, " errs:", {k: f"{v:.1e}" for k, v in errs.items()}, " TF/s:", {k: round(v) for k, v in tf.items()},
+              flush=True)
         del a, w, out, ref
         torch.cuda.empty_cache()
     txt = "\n".join(rows)
