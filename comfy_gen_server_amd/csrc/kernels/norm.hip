@@ -30,14 +30,18 @@ __device__ __forceinline__ const u16* gn_src(const u16* __restrict__ x, const u1
   return c < C1 ? x + pix * C1 + c : x2 + pix * (size_t)(C - C1) + (c - C1);
 }
 
-template <int DT, int KM>
+template <int DT, int KM, int PK = 1>
 __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, const u16* __restrict__ x2,
                                                                int C1, float* __restrict__ part,
                                                                int HW, int C, int ppb, int nb, int CS) {
   // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget).
   // KM = 16-byte chunk rounds per lane (ceil(CS / 512)); each wave keeps GN_UNROLL rows of loads in
   // flight before accumulating (one row per wave per trip left the HBM pipe half empty).
+  // PK > 1 (narrow rows, CS / 8 <= 64 / PK chunks, KM = 1): the wave's lanes split into PK groups of
+  // 64 / PK, each on its own pixel -- a 128-channel row (16 chunks) used a quarter of the lanes and ran
+  // the VAE's 1024^2 GroupNorms at ~1.6 TB/s; the groups' sums are combined by shuffles at the end.
   constexpr int GN_UNROLL = 4;
+  constexpr int LPG = 64 / PK;   // lanes per pixel group
   const int n = blockIdx.y;
   const int blk = blockIdx.x;
   const int c0 = blockIdx.z * CS;
@@ -45,37 +49,39 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   const int p1 = min(HW, p0 + ppb);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  const int lch = PK > 1 ? lane % LPG : lane;   // chunk lane
+  const int pg = PK > 1 ? lane / LPG : 0;       // pixel group
   const int nchunk = CS >> 3;
   const size_t pix0 = (size_t)n * HW;
   // shift = the block's first pixel (shared by all 4 waves): keeps the shifted sums well conditioned
   float s1[KM][8], s2[KM][8], sh[KM][8];
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
-    int ch = lane + 64 * k;
+    int ch = lch + 64 * k;
     s16x8 v = {};
     if (ch < nchunk && p0 < p1) v = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, pix0 + p0, c0 + ch * 8));
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sh[k][j] = cvt_in<DT>((u16)v[j]); s1[k][j] = 0.f; s2[k][j] = 0.f; }
   }
   int cnt = 0;
-  for (int p = p0 + wave; p < p1; p += 4 * GN_UNROLL) {
+  for (int p = p0 + wave * PK + pg; p < p1; p += 4 * PK * GN_UNROLL) {
     s16x8 buf[GN_UNROLL][KM];
 #pragma unroll
     for (int u = 0; u < GN_UNROLL; ++u) {
-      const int pu = p + 4 * u;
+      const int pu = p + 4 * PK * u;
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
-        int ch = lane + 64 * k;
+        int ch = lch + 64 * k;
         if (pu < p1 && ch < nchunk) buf[u][k] = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, pix0 + pu, c0 + ch * 8));
       }
     }
 #pragma unroll
     for (int u = 0; u < GN_UNROLL; ++u) {
-      if (p + 4 * u < p1) {
+      if (p + 4 * PK * u < p1) {
         cnt++;
 #pragma unroll
         for (int k = 0; k < KM; ++k) {
-          if (lane + 64 * k < nchunk) {
+          if (lch + 64 * k < nchunk) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               float d = cvt_in<DT>((u16)buf[u][k][j]) - sh[k][j];
@@ -87,6 +93,17 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
       }
     }
   }
+  if constexpr (PK > 1) {   // same channels, same shift in every pixel group: plain sums combine
+#pragma unroll
+    for (int off = LPG; off < 64; off <<= 1) {
+      cnt += __shfl_xor(cnt, off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[0][j] += __shfl_xor(s1[0][j], off);
+        s2[0][j] += __shfl_xor(s2[0][j], off);
+      }
+    }
+  }
   // per-wave (mean, M2) per channel -> LDS, then Chan-combine the 4 waves
   extern __shared__ __attribute__((aligned(16))) float gn_smem[];
   float* lmean = gn_smem;             // [4][CS]
@@ -95,8 +112,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __res
   if (lane == 0) lcnt[wave] = cnt;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
-    int ch = lane + 64 * k;
-    if (ch < nchunk) {
+    int ch = lch + 64 * k;
+    if (ch < nchunk && pg == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float m = 0.f, m2 = 0.f;
@@ -216,8 +233,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x
   const int ch = tid % cpr;
   int cur_n = -1;
   float a[8], bb[8];
-  for (int row = tid / cpr; row < rows_total; row += rows_per_iter) {
-    const int n = row / HW;
+  auto coef = [&](int n) {
     if (n != cur_n) {
       cur_n = n;
       const float4* abp = reinterpret_cast<const float4*>(ab + ((size_t)n * C + ch * 8) * 2);
@@ -227,8 +243,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x
         a[2 * j] = t.x; bb[2 * j] = t.y; a[2 * j + 1] = t.z; bb[2 * j + 1] = t.w;
       }
     }
-    const size_t i = (size_t)row * cpr + ch;
-    s16x8 v = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, (size_t)row, ch * 8));
+  };
+  auto apply = [&](int row, const s16x8& v) {
+    coef(row / HW);
     s16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -236,8 +253,18 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x
       if (SILU) f = silu_f(f);
       o[j] = (short)cvt_out<DT>(f);
     }
-    reinterpret_cast<s16x8*>(y)[i] = o;
+    reinterpret_cast<s16x8*>(y)[(size_t)row * cpr + ch] = o;
+  };
+  // two rows per trip, both loads issued before either is used (one 16-B load in flight per lane left
+  // the big VAE GroupNorms at ~2.3 TB/s)
+  int row = tid / cpr;
+  for (; row + rows_per_iter < rows_total; row += 2 * rows_per_iter) {
+    const s16x8 v0 = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, (size_t)row, ch * 8));
+    const s16x8 v1 = *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, (size_t)(row + rows_per_iter), ch * 8));
+    apply(row, v0);
+    apply(row + rows_per_iter, v1);
   }
+  if (row < rows_total) apply(row, *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, (size_t)row, ch * 8)));
 }
 
 CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
@@ -269,8 +296,18 @@ static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const 
     gn_partial_kernel<CGS_BF16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS); \
   else                                                                                                          \
     gn_partial_kernel<CGS_F16, KMV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS);
-  if (km == 1) { CGS_GN_PARTIAL(1) } else if (km == 2) { CGS_GN_PARTIAL(2) } else if (km == 3) { CGS_GN_PARTIAL(3) } else { CGS_GN_PARTIAL(4) }
+#define CGS_GN_PARTIAL_PK(PKV)                                                                                  \
+  if (dtype == CGS_BF16)                                                                                        \
+    gn_partial_kernel<CGS_BF16, 1, PKV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS); \
+  else                                                                                                          \
+    gn_partial_kernel<CGS_F16, 1, PKV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS);
+  const int nch = CS / 8;
+  if (nch <= 8) { CGS_GN_PARTIAL_PK(8) }
+  else if (nch <= 16) { CGS_GN_PARTIAL_PK(4) }
+  else if (nch <= 32) { CGS_GN_PARTIAL_PK(2) }
+  else if (km == 1) { CGS_GN_PARTIAL(1) } else if (km == 2) { CGS_GN_PARTIAL(2) } else if (km == 3) { CGS_GN_PARTIAL(3) } else { CGS_GN_PARTIAL(4) }
 #undef CGS_GN_PARTIAL
+#undef CGS_GN_PARTIAL_PK
   gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
   return gn_apply_launch(x, x2, C1, y, ab, N, HW, C, silu, dtype, stream);
 }
