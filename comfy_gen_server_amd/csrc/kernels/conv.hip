@@ -548,6 +548,57 @@ struct ConvGatherKU {
   }
 };
 
+// ConvGatherKD with 2 registers per slot instead of 3 (v7 runs at the 256-VGPR cap: KD spilled there): the
+// lane keeps its top-left pixel index and tap mask, and multiplies by the input's row pitch per DMA (one
+// 32-bit multiply, exact mod 2^32 like KD's offsets). Whole-input descriptors only (ppk re-points A per
+// half-tile, so no per-image rebuild).
+struct ConvGatherKL {
+  static constexpr bool kOwnDMA = true;
+  const ConvArgs* a;
+  uint32_t pix[4], vm[4];
+  __amdgpu_buffer_rsrc_t r1, r2;
+  __device__ __forceinline__ void init() {
+    const unsigned px = (unsigned)(a->N * a->H * a->W);
+    r1 = __builtin_amdgcn_make_buffer_rsrc((void*)a->in, 0, (int)(px * (unsigned)a->C1 * 2u), 0x00020000);
+    r2 = __builtin_amdgcn_make_buffer_rsrc((void*)(a->in2 ? a->in2 : a->in), 0,
+                                           (int)(px * (unsigned)(a->in2 ? a->Cin - a->C1 : a->C1) * 2u), 0x00020000);
+  }
+  __device__ __forceinline__ void tile(int) {}
+  __device__ __forceinline__ void setup(int s, int row) {
+    const int M = a->N * a->Ho * a->Wo;
+    const bool ok = row < M;
+    row = ok ? row : M - 1;
+    const int hw = a->Ho * a->Wo;
+    const int n = row / hw;
+    const int rem = row - n * hw;
+    const int oy = rem / a->Wo;
+    const int py = oy * a->stride - a->pad, px = (rem - oy * a->Wo) * a->stride - a->pad;
+    pix[s] = (unsigned)((n * a->H + py) * a->W + px);
+    uint32_t m = 0;
+    if (ok) {
+      for (int ky = 0; ky < a->kh; ++ky) {
+        const bool ry = (unsigned)(py + ky) < (unsigned)a->H;
+        for (int kx = 0; kx < a->kw; ++kx)
+          if (ry && (unsigned)(px + kx) < (unsigned)a->W) m |= 1u << (ky * a->kw + kx);
+      }
+    }
+    vm[s] = m;
+  }
+  __device__ __forceinline__ void dma(int s, int k0, unsigned char* dst) const {
+    const unsigned kq = (unsigned)k0 >> 6;
+    const unsigned tap = __umulhi(kq, a->cq_magic) + (a->cq_magic ? 0u : kq);
+    const int ci0 = k0 - (int)tap * a->Cin;
+    const int ky = (int)((tap * (unsigned)a->kw_m16) >> 16);
+    const int kx = (int)tap - ky * a->kw;
+    const bool second = ci0 >= a->C1;
+    const unsigned cs2 = 2u * (unsigned)(second ? a->Cin - a->C1 : a->C1);
+    const unsigned so = (unsigned)(ky * a->W + kx) * cs2 + 2u * (unsigned)(second ? ci0 - a->C1 : ci0) +
+                        16u * (unsigned)pp::src_chunk8(s & 1);
+    const unsigned off = (pix[s] * cs2 + so) | (~(vm[s] << (31u - tap)) & 0x80000000u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? r2 : r1, (lds_void*)dst, 16, off, 0, 0, 0);
+  }
+};
+
 static bool conv_fast_ok(const ConvArgs& a) { return !(a.flags & CONV_UP2X) && a.kh * a.kw <= 32; }
 // an input tensor spans >= 2 GiB (v7's ConvGatherKB descriptors need < 2 GiB)
 static bool conv_wide(const ConvArgs& a) {
@@ -720,9 +771,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
   const int K = a.kh * a.kw * a.Cin;
-  typename std::conditional<LOADER == 1, ConvGatherKB, ConvGatherA8>::type al;
+  typename std::conditional<LOADER == 2, ConvGatherKL,
+                            typename std::conditional<LOADER == 1, ConvGatherKB, ConvGatherA8>::type>::type al;
   al.a = &a;
-  if constexpr (LOADER == 1) al.init();
+  if constexpr (LOADER >= 1) al.init();
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   ppk::run<false>(al, a.w, K, M, a.Cout, K, e, smem, (M + ppk::BM - 1) / ppk::BM, a.tiles_n, a.group_m, a.sp);
 }
@@ -733,6 +785,8 @@ static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long
     (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ppk::LDS);
     (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ppk::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v7_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ppk::LDS);
     attr = true;
   }
@@ -756,7 +810,9 @@ static void conv_v7_go(ConvArgs& a, hipStream_t stream, void* ws = nullptr, long
   const int grid = (int)(U < conv_num_cus() ? U : conv_num_cus());
   if (conv_fast_ok(a) && !conv_wide(a)) {
     conv_magic(a);
-    conv_nhwc_v7_kernel<1><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+    a.img_rsrc = 0;
+    if (g_conv_v6_ld == 1) conv_nhwc_v7_kernel<1><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
+    else conv_nhwc_v7_kernel<2><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
   } else {
     conv_nhwc_v7_kernel<0><<<grid, ppk::THREADS, ppk::LDS, stream>>>(a);
   }

@@ -16,9 +16,13 @@
 #define GN_MAX_CHUNKS_PER_LANE 4   // <= 64*4*8 = 2048 channels of a row per block (wider rows: channel slices)
 
 static inline int gn_pix_per_block(int N, int HW) {
+  // ~2048 statistics blocks over the batch, >= 16 pixels each -- >= 64 at batch <= 4: there 16-pixel blocks
+  // (1024 per image at 128^2) made the finalize pass (one block per (image, group)) walk 10-40 k partials
+  // each (~16 us per GroupNorm at SDXL batch 1; profiles/r04/groupnorm_b1_r04ai.log)
   int target_blocks_per_n = (2048 + N - 1) / N;
   int ppb = (HW + target_blocks_per_n - 1) / target_blocks_per_n;
   if (ppb < 16) ppb = 16;
+  if (N <= 4 && ppb < 64) ppb = 64;
   return ppb;
 }
 
