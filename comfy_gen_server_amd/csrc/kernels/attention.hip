@@ -330,6 +330,10 @@ struct KV2 {
   long long ksb, kss, vsb, vss;
 };
 
+// A persistent form (one WG per CU walking the units, the next unit's K / V / Q streamed in under the last
+// tiles of the current one) was built and measured in round 4: level 2 651 vs 632 TF/s (auto 663), level 1
+// 792 vs 844 (246 VGPRs) -- the per-unit prologue is not where level 2 loses (profiles/r04/
+// attn_persistent_ab_r04ak.log); removed.
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
 // workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
 template <int NW, bool TWO = false, bool PRIO = true>

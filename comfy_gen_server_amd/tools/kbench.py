@@ -82,8 +82,13 @@ def main(quick=False, attn_only=False, gemm_only=False):
         fl = 4.0 * b * h * sq * sk * d
         lib = ops.dispatch._native.load_kernels()
         ent = dict(B=b, H=h, Sq=sq, Sk=sk, D=d)
+        ref = None
         for var, name in ((1, "generic"), (2, "d64"), (4, "d64r2"), (5, "d64q128"), (0, "auto")):
             lib.cgs_attn_set_variant(var)
+            y = ops.attention(q, k, v, h).float()
+            if ref is None:
+                ref = y
+            ent[f"{name}_maxdiff"] = (y - ref).abs().max().item()
             t_hip = _time(lambda: ops.attention(q, k, v, h))
             ent[f"{name}_ms"] = t_hip
             ent[f"{name}_tflops"] = fl / t_hip / 1e9
