@@ -707,7 +707,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_d64r2_kernel(
 // The reference runs this shape through the same optimized_attention as self-attention
 // (comfy/ldm/modules/attention.py:352-383); the general flash kernel would pay a full 64-key
 // pipeline for 77 keys.
-template <int NKT, bool PRIO = true>
+// QI > 1: each wave walks QI 32-query blocks (stride 128 queries) with the next block's Q rows loaded
+// while the current one computes, so K / V are staged once per 128 * QI queries and the Q stream stays
+// in flight: at QI = 1 a workgroup's life was one K/V + Q load latency for ~1 us of math (SDXL
+// cross-attention ran at ~2.5 TB/s of its Q + O traffic).
+template <int NKT, bool PRIO = true, int QI = 1>
 __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
@@ -743,75 +747,87 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
     *reinterpret_cast<s16x8*>(&Vs[key * 64 + 8 * (ch ^ (((key >> 1) & 1) << 2))]) = vv;
   }
 
-  const int q_row = qb * 128 + wave * 32 + l32;
-  const bool q_ok = q_row < Sq;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    s16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (q_ok) t = *reinterpret_cast<const s16x8*>(qbase + (long long)q_row * qss + ks * 16 + 8 * hf);
-    qf[ks] = __builtin_bit_cast(bf16x8, t);
-  }
-  __syncthreads();
-
-  f32x16 s[NKT];
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    s[kt] = f32x16{};
-    const int key = kt * 32 + l32;
+  auto loadq = [&](int q_row, bf16x8 (&qf)[4]) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      s16x8 a = *reinterpret_cast<const s16x8*>(&Ks[key * 64 + 8 * ((2 * ks + hf) ^ ((key >> 1) & 7))]);
-      s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], s[kt], 0, 0, 0);
+      s16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (q_row < Sq) t = *reinterpret_cast<const s16x8*>(qbase + (long long)q_row * qss + ks * 16 + 8 * hf);
+      qf[ks] = __builtin_bit_cast(bf16x8, t);
     }
-  }
-  // exact softmax over the whole key set (lane = one query, its half of the keys)
-  float mx = -INFINITY;
+  };
+  const int row_base = qb * (128 * QI) + wave * 32 + l32;
+  bf16x8 qf[4];
+  loadq(row_base, qf);
+  __syncthreads();
+
+#pragma unroll 1
+  for (int qi = 0; qi < QI; ++qi) {
+    const int q_row = row_base + 128 * qi;
+    bf16x8 qn[4];
+    if (QI > 1 && qi + 1 < QI) loadq(q_row + 128, qn);   // next block's Q rows, in flight under this one
+    f32x16 s[NKT];
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt] = f32x16{};
+      const int key = kt * 32 + l32;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-      s[kt][r] = key < Sk ? s[kt][r] : -INFINITY;
-      mx = fmaxf(mx, s[kt][r]);
-    }
-  mx = af_xmax(mx) * c;
-  const float nm = -mx;
-  float ps = 0.f;
-  bf16x8 pf[2 * NKT];
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][r], c, nm));
-      ps += p;
-      pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p;
-    }
-  f32x16 ot[2] = {f32x16{}, f32x16{}};
-  const int i16 = lane & 15;
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // P.V MFMAs ahead of co-resident waves' softmax VALU
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const int row0 = kt * 32 + 16 * st + 4 * hf + (i16 >> 2);
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
-        const int ch = col >> 3, half = (col >> 2) & 1;
-        const int r1 = row0 + 8;
-        const int o0 = row0 * 64 + 8 * (ch ^ (((row0 >> 1) & 1) << 2)) + 4 * half;
-        const int o1 = r1 * 64 + 8 * (ch ^ (((r1 >> 1) & 1) << 2)) + 4 * half;
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o0));
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o1));
-        bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        ot[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt * 2 + st], ot[dt], 0, 0, 0);
+      for (int ks = 0; ks < 4; ++ks) {
+        s16x8 a = *reinterpret_cast<const s16x8*>(&Ks[key * 64 + 8 * ((2 * ks + hf) ^ ((key >> 1) & 7))]);
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], s[kt], 0, 0, 0);
       }
     }
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-  const float l_tot = ps + __shfl_xor(ps, 32, 64);
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  af_store_row64(obase + (long long)q_row * oss, ot, inv, hf, q_ok);
+    // exact softmax over the whole key set (lane = one query, its half of the keys)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+        s[kt][r] = key < Sk ? s[kt][r] : -INFINITY;
+        mx = fmaxf(mx, s[kt][r]);
+      }
+    mx = af_xmax(mx) * c;
+    const float nm = -mx;
+    float ps = 0.f;
+    bf16x8 pf[2 * NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][r], c, nm));
+        ps += p;
+        pf[kt * 2 + (r >> 3)][r & 7] = (__bf16)p;
+      }
+    f32x16 ot[2] = {f32x16{}, f32x16{}};
+    const int i16 = lane & 15;
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // P.V MFMAs ahead of co-resident waves' softmax VALU
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int row0 = kt * 32 + 16 * st + 4 * hf + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+          const int ch = col >> 3, half = (col >> 2) & 1;
+          const int r1 = row0 + 8;
+          const int o0 = row0 * 64 + 8 * (ch ^ (((row0 >> 1) & 1) << 2)) + 4 * half;
+          const int o1 = r1 * 64 + 8 * (ch ^ (((r1 >> 1) & 1) << 2)) + 4 * half;
+          bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o0));
+          bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Vs + o1));
+          bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          ot[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt * 2 + st], ot[dt], 0, 0, 0);
+        }
+      }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    const float l_tot = ps + __shfl_xor(ps, 32, 64);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    af_store_row64(obase + (long long)q_row * oss, ot, inv, hf, q_row < Sq);
+    if constexpr (QI > 1) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = qn[ks];
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1119,24 +1135,39 @@ static int flash_attn_impl(const void* q, const void* k, const void* v, void* o,
                       reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) & 15) == 0;
   if (D == 64 && !key_mask && !causal && al16 && Sk > 0 && Sk <= 128 && !lse &&
       (g_attn_variant == 0 || g_attn_variant == 3)) {
-    const int nqb3 = (Sq + 127) / 128;
+    // QI 32-query blocks per wave (K / V staged once per 128 * QI queries): measured +4.5 % at SDXL level 1
+    // (Sq = 4096), -2.6 % at level 2 (profiles/r04/shortkv_qi_ab_r04al.log) -> QI = 4 for Sq >= 2048 while
+    // that leaves >= 2 workgroups per CU; CGS_SKV_QI=1|2|4 overrides (A/B)
+    const long long blocks128 = (long long)((Sq + 127) / 128) * B * H;
+    static const int qi_env = getenv("CGS_SKV_QI") ? atoi(getenv("CGS_SKV_QI")) : 0;
+    int qi = 1;
+    if (qi_env == 1 || qi_env == 2 || qi_env == 4) qi = qi_env;
+    else if (Sq >= 2048 && blocks128 / 4 >= 2 * num_cus_attn()) qi = 4;
+    const int nqb3 = (Sq + 128 * qi - 1) / (128 * qi);
     const long long nwg3 = (long long)nqb3 * B * H;
     if (nwg3 > 0x7fffffff) return (int)hipErrorInvalidValue;
-#define SKV_LAUNCH(NKT)                                                                                              \
+#define SKV_GO(NKT, QIV)                                                                                             \
   do {                                                                                                              \
     if (g_attn_prio)                                                                                                \
-      attn_fwd_d64_shortkv_kernel<NKT><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                                   \
+      attn_fwd_d64_shortkv_kernel<NKT, true, QIV><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                        \
           (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss,   \
           vsh, osb, oss, osh, sl2, nqb3);                                                                           \
     else                                                                                                            \
-      attn_fwd_d64_shortkv_kernel<NKT, false><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                            \
+      attn_fwd_d64_shortkv_kernel<NKT, false, QIV><<<dim3((unsigned)nwg3), 256, 0, stream>>>(                       \
           (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, H, Sq, Sk, qsb, qss, qsh, ksb, kss, ksh, vsb, vss,   \
           vsh, osb, oss, osh, sl2, nqb3);                                                                           \
+  } while (0)
+#define SKV_LAUNCH(NKT)                                                                                              \
+  do {                                                                                                              \
+    if (qi == 4) SKV_GO(NKT, 4);                                                                                    \
+    else if (qi == 2) SKV_GO(NKT, 2);                                                                               \
+    else SKV_GO(NKT, 1);                                                                                            \
   } while (0)
     if (Sk <= 32) SKV_LAUNCH(1);
     else if (Sk <= 64) SKV_LAUNCH(2);
     else if (Sk <= 96) SKV_LAUNCH(3);
     else SKV_LAUNCH(4);
+#undef SKV_GO
 #undef SKV_LAUNCH
     return (int)hipGetLastError();
   }
