@@ -566,25 +566,27 @@ struct DenseKB {
 
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
-template <bool LN = false, int DS = 0, bool GG = false, bool ACT = false>
+template <bool LN = false, int DS = 0, bool GG = false, bool ACT = false, bool RSO = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
-    int epi, float alpha, int tiles_m, int tiles_n, int group_m, const float* rs = nullptr, const float* cs = nullptr) {
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m, const float* rs = nullptr, const float* cs = nullptr,
+    float* rso = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // 64-bit operand pointers: the 32-bit-offset (saddr) DMA form measured 3-10 % slower on v6
   // (profiles/r03/v6_offsets32.log)
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
+  e.gnp = rso;    // RSO: per-row LayerNorm statistics partials out
   if constexpr ((DS & 64) != 0) {
     DenseKB al;
     al.A = A;
     al.lda = lda;
     al.M = M;
     al.init();
-    pq::run<DenseKB, LN, DS, false, GG, ACT>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+    pq::run<DenseKB, LN, DS, false, GG, ACT, RSO>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
   } else {
     DenseA8 al{A, lda, M, {}};
-    pq::run<DenseA8, LN, DS, false, GG, ACT>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+    pq::run<DenseA8, LN, DS, false, GG, ACT, RSO>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
   }
 }
 static int num_cus() {
@@ -615,19 +617,20 @@ int v6_conv_ds() {
 }
 CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; g_v6_conv_ds = m; }
 
-template <bool LN, int DS, bool GG = false, bool ACT = false>
+template <bool LN, int DS, bool GG = false, bool ACT = false, bool RSO = false>
 static void gemm_v6_go(int grid, const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                        int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                       int tiles_m, int tiles_n, hipStream_t stream, const float* rs, const float* cs) {
+                       int tiles_m, int tiles_n, hipStream_t stream, const float* rs, const float* cs,
+                       float* rso = nullptr) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT, RSO>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
     attr_set = true;
   }
-  gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT><<<grid, pq::THREADS, pq::LDS, stream>>>(
+  gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT, RSO><<<grid, pq::THREADS, pq::LDS, stream>>>(
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
-      tiles_m, tiles_n, g_tile_group, rs, cs);
+      tiles_m, tiles_n, g_tile_group, rs, cs, rso);
 }
 
 static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
@@ -677,6 +680,26 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   return (int)hipGetLastError();
 }
 
+
+// v6 GEMM (bias / residual epilogue) that also writes per-row LayerNorm statistics partials of its output
+// (pq::run RSO): part = [M][N / 80] (mean, M2) float pairs; cgs_ln_rs_from_partials turns them into the
+// (mean, rstd) rows a LayerNorm-folded GEMM reads. N % 160 == 0, K % 64 == 0, K >= 128.
+CGS_EXPORT int cgs_gemm_bf16_rowstats(const void* A, const void* W, void* C, const void* bias, const void* R, int M,
+                                      int N, int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                                      float alpha, float* part, hipStream_t stream) {
+  if (!part || N % 160 || K % 64 || K < 128 || (epi & ~(EPI_BIAS | EPI_RESIDUAL)) || lda % 8 || ldw % 8 ||
+      ldc % 8 || ((epi & EPI_RESIDUAL) && ldr % 8) || ((uintptr_t)bias % 8) ||
+      ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16) || ((uintptr_t)part % 8))
+    return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const int tiles_n = N / pq::BN;
+  const int tiles_m = (M + pq::BM - 1) / pq::BM;
+  const long long T = (long long)tiles_m * tiles_n;
+  const int grid = (int)(T < num_cus() ? T : num_cus());
+  gemm_v6_go<false, 1, false, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m,
+                                           tiles_n, stream, nullptr, nullptr, part);
+  return (int)hipGetLastError();
+}
 
 // ------------------------------------------------------------------------------------------------
 // v7: persistent 256 x 256 x 64 ping-pong with cross-tile prefetch and a register epilogue (mfma_ppk.h)

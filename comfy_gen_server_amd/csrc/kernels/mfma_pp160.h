@@ -74,7 +74,12 @@ __device__ __forceinline__ int gg_row160(int r) {
 // rows = 5 interleave groups = 80 output columns per tile (whole rounds where the 256-wide tiles leave a
 // partial one, e.g. SDXL batch 1: M = 2048, N = 10240 -> 512 tiles vs 320). Host: N % 160 == 0.
 // ACT: GELU on (acc * alpha + bias) before the residual add (MC_EPI_GELU: Cascade's ChannelMLP Linear -> GELU).
-template <class AL, bool LN = false, int DS = 0, bool GNS = false, bool GG = false, bool ACT = false>
+// RSO: the epilogue also writes per-row LayerNorm statistics partials of the stored (bf16) outputs -- per row
+// and 80-column chunk (one wave's columns), (mean, M2) shifted by the row's first value in the chunk -- into
+// e.gnp as [M][N / 80][2] floats; a LayerNorm over these rows then needs only cgs_ln_rs_from_partials
+// instead of a statistics pass over the tensor. Host: N % 160 == 0.
+template <class AL, bool LN = false, int DS = 0, bool GNS = false, bool GG = false, bool ACT = false,
+          bool RSO = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -352,6 +357,52 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           float4* d4 = reinterpret_cast<float4*>(dst + (size_t)col * 2);
           d4[0] = float4{mu.x, q.x, mu.y, q.y};
           d4[1] = float4{mu.z, q.z, mu.w, q.w};
+        }
+      }
+      return;
+    }
+    if constexpr (RSO) {
+      uint2 pk[4][5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pk[i][j] = val(i, j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m_w + 16 * i + fr;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int col = n_w + 32 * p + 8 * fq;
+          if (row < M && col < N)
+            *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) =
+                uint4{pk[i][2 * p].x, pk[i][2 * p].y, pk[i][2 * p + 1].x, pk[i][2 * p + 1].y};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
+      // row (16 i + fr) of this wave's 80 columns: 20 values in each of the 4 lanes fr + 16 fq
+      const int P = N / 80;
+      const int chunk = n_w / 80;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float sh = __shfl(unpack4_bf16(pk[i][0]).x, fr, 64);   // shift: the chunk's value of lane fr
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const float4 u = unpack4_bf16(pk[i][j]);
+          const float d0 = u.x - sh, d1 = u.y - sh, d2 = u.z - sh, d3 = u.w - sh;
+          s1 += (d0 + d1) + (d2 + d3);
+          s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
+        s1 += __shfl_xor(s1, 16, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        const int row = m_w + 16 * i + fr;
+        if (fq == 0 && row < M) {
+          constexpr float inv = 1.f / 80.f;
+          *reinterpret_cast<float2*>(e.gnp + ((long long)row * P + chunk) * 2) =
+              float2{sh + s1 * inv, fmaxf(s2 - s1 * s1 * inv, 0.f)};
         }
       }
       return;

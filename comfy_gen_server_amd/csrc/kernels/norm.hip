@@ -271,6 +271,30 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const u16* __restrict__ x
   if (row < rows_total) apply(row, *reinterpret_cast<const s16x8*>(gn_src(x, x2, C, C1, (size_t)row, ch * 8)));
 }
 
+// LayerNorm row statistics from GEMM-epilogue partials (pq::run RSO): part [M][P] (mean, M2) of 80 columns
+// each -> rs [M] (mean, rstd) by Chan's combine (no cancellation), one thread per row.
+__global__ __launch_bounds__(256) void ln_rs_from_partials_kernel(const float* __restrict__ part, float* __restrict__ rs,
+                                                                  int M, int P, float eps) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= M) return;
+  const float2* p = reinterpret_cast<const float2*>(part) + (long long)row * P;
+  float n = 80.f, mean = p[0].x, m2 = p[0].y;
+  for (int c = 1; c < P; ++c) {
+    const float2 v = p[c];
+    const float nn = n + 80.f, d = v.x - mean, f = 80.f / nn;
+    mean += d * f;
+    m2 += v.y + d * d * n * f;
+    n = nn;
+  }
+  reinterpret_cast<float2*>(rs)[row] = float2{mean, rsqrtf(m2 / n + eps)};
+}
+
+CGS_EXPORT int cgs_ln_rs_from_partials(const float* part, float* rs, int M, int P, float eps, hipStream_t stream) {
+  if (M <= 0 || P <= 0) return (int)hipErrorInvalidValue;
+  ln_rs_from_partials_kernel<<<(unsigned)((M + 255) / 256), 256, 0, stream>>>(part, rs, M, P, eps);
+  return (int)hipGetLastError();
+}
+
 CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
   int ppb = gn_pix_per_block(N, HW);
   int nb = (HW + ppb - 1) / ppb;

@@ -76,9 +76,10 @@ class CrossAttention(nn.Module, DerivedMixin):
             ctx_cache[cache_key] = (context, k, v)
         return k, v
 
-    def forward_lnfold(self, x, rs, norm, residual=None, sp=None):
+    def forward_lnfold(self, x, rs, norm, residual=None, sp=None, row_stats=False):
         """Self-attention on LN(x) with the LayerNorm folded into the fused QKV GEMM (K07): ``x`` raw
-        rows, ``rs`` their (mean, rstd) from ``ops.layernorm_stats``."""
+        rows, ``rs`` their (mean, rstd) from ``ops.layernorm_stats``; ``row_stats``: the output feeds a
+        LayerNorm (the out-projection's epilogue writes its statistics partials)."""
         inner = self.heads * self.dim_head
         w2, cs, b2 = self._derived_get(("lnfold_qkv", id(norm)), lambda: ops.lnfold_weights(
             self._w_qkv(), None, norm.weight, norm.bias))
@@ -88,9 +89,10 @@ class CrossAttention(nn.Module, DerivedMixin):
             o = sp.attention(q.contiguous(), k.contiguous(), v.contiguous(), self.heads)
         else:
             o = ops.attention(q, k, v, self.heads)
-        return self.to_out[0](o, residual=residual)
+        return self.to_out[0](o, residual=residual, row_stats=row_stats)
 
-    def forward_lnfold_cross(self, x, rs, norm, context, residual=None, ctx_cache=None, cache_key=None, kv=None):
+    def forward_lnfold_cross(self, x, rs, norm, context, residual=None, ctx_cache=None, cache_key=None, kv=None,
+                             row_stats=False):
         """Cross-attention on LN(x) with the LayerNorm folded into the query GEMM."""
         w2, cs, b2 = self._derived_get(("lnfold_q", id(norm)), lambda: ops.lnfold_weights(
             self.to_q.weight, None, norm.weight, norm.bias))
@@ -100,7 +102,7 @@ class CrossAttention(nn.Module, DerivedMixin):
             kvs = self.static_kv(context, kv)
         k, v = kvs if kvs is not None else self.project_kv(context, None, ctx_cache, cache_key)
         o = ops.attention(q, k, v, self.heads)
-        return self.to_out[0](o, residual=residual)
+        return self.to_out[0](o, residual=residual, row_stats=row_stats)
 
     def static_kv(self, context, kv):
         """Cross-attention K/V of a sampling run's constant context, kept in a per-context buffer
@@ -196,12 +198,12 @@ class FeedForward(nn.Module):
     def lnfold_ok(self) -> bool:
         return isinstance(self.net[0], GEGLU)
 
-    def forward_lnfold(self, x, rs, norm, residual=None):
+    def forward_lnfold(self, x, rs, norm, residual=None, row_stats=False):
         """FF on LN(x) with the LayerNorm folded into the GEGLU GEMM (interleaved a/g rows)."""
         g = self.net[0]
         w2, cs, b2 = g._derived_get(("lnfold_geglu", id(norm)), lambda: ops.lnfold_weights(
             ops.core.geglu_interleave(g.proj.weight), ops.core.geglu_interleave(g.proj.bias), norm.weight, norm.bias))
-        return self.net[2](ops.linear_lnfold(x, rs, w2, cs, b2, geglu=True), residual=residual)
+        return self.net[2](ops.linear_lnfold(x, rs, w2, cs, b2, geglu=True), residual=residual, row_stats=row_stats)
 
 
 class BasicTransformerBlock(nn.Module):
@@ -273,16 +275,19 @@ class BasicTransformerBlock(nn.Module):
             if self.disable_self_attn:
                 x = self.attn1(self.norm1(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 1))
             else:
-                x = self.attn1.forward_lnfold(x, ops.layernorm_stats(x, self.norm1.eps), self.norm1, residual=x,
-                                              sp=to.get("sp"))
+                # (the LayerNorm statistics come from the producing GEMM's epilogue where it wrote them:
+                # ops.layernorm_stats_for)
+                x = self.attn1.forward_lnfold(x, ops.layernorm_stats_for(x, self.norm1.eps), self.norm1, residual=x,
+                                              sp=to.get("sp"), row_stats=True)
             if self.attn2.is_cross and self.norm2.weight is not None and self.norm2.weight.dtype == x.dtype:
-                x = self.attn2.forward_lnfold_cross(x, ops.layernorm_stats(x, self.norm2.eps), self.norm2, context,
-                                                    residual=x, ctx_cache=cache, cache_key=(key, 2),
-                                                    kv=to.get("kv_static"))
+                x = self.attn2.forward_lnfold_cross(x, ops.layernorm_stats_for(x, self.norm2.eps), self.norm2,
+                                                    context, residual=x, ctx_cache=cache, cache_key=(key, 2),
+                                                    kv=to.get("kv_static"), row_stats=True)
             else:
                 x = self.attn2(self.norm2(x), context=context, residual=x, ctx_cache=cache, cache_key=(key, 2),
                                kv=to.get("kv_static"))
-            return self.ff.forward_lnfold(x, ops.layernorm_stats(x, self.norm3.eps), self.norm3, residual=x)
+            return self.ff.forward_lnfold(x, ops.layernorm_stats_for(x, self.norm3.eps), self.norm3, residual=x,
+                                          row_stats=True)
         n = self.norm1(x)
         if self.disable_self_attn:
             x = self.attn1(n, context=context, residual=x, ctx_cache=cache, cache_key=(key, 1))
@@ -393,7 +398,7 @@ class SpatialTransformer(nn.Module):
         # NHWC storage makes this a view on the device
         x = x.permute(0, 2, 3, 1).reshape(b, h * w, -1)
         if self.use_linear:
-            x = self.proj_in(x)
+            x = self.proj_in(x, row_stats=True)       # the first block's LayerNorm reads its statistics partials
         for i, blk in enumerate(self.transformer_blocks):
             to["block_index"] = i
             x = blk(x, context=context[i], transformer_options=to)

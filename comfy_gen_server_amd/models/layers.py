@@ -100,11 +100,12 @@ class Linear(nn.Module, DerivedMixin, CastWeightBiasOp):
         else:
             self.register_parameter("bias", None)
 
-    def forward(self, x, residual=None, act=None):
-        """``act="gelu"``: GELU fused into the GEMM epilogue (before the residual)."""
+    def forward(self, x, residual=None, act=None, row_stats=False):
+        """``act="gelu"``: GELU fused into the GEMM epilogue (before the residual). ``row_stats``: the
+        next op is a LayerNorm over the output (``ops.linear`` row-statistics partials)."""
         if _hooked(self):
             w, b = cast_bias_weight(self, x)
-            return ops.linear(x, w, b, residual=residual, act=act)
+            return ops.linear(x, w, b, residual=residual, act=act, row_stats=row_stats)
         w, b = self.weight, self.bias
         if w.dtype == torch.float8_e4m3fn and w.device == x.device and x.dtype == torch.bfloat16 and x.is_cuda:
             # fp8-stored weights go to the fp8-weight GEMM as they are (widened inside the kernel)
@@ -112,7 +113,7 @@ class Linear(nn.Module, DerivedMixin, CastWeightBiasOp):
         if w.dtype != x.dtype or w.device != x.device:  # manual cast (comfy/ops.py:22-32)
             w = w.to(device=x.device, dtype=x.dtype)
             b = None if b is None else b.to(device=x.device, dtype=x.dtype)
-        return ops.linear(x, w, b, residual=residual, act=act)
+        return ops.linear(x, w, b, residual=residual, act=act, row_stats=row_stats)
 
     def weight_bias_for(self, x):
         """(weight, bias) as the forward would use them for ``x`` (hooks applied, cast to x's dtype)."""

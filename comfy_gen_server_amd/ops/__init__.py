@@ -23,6 +23,6 @@ from .core import (  # noqa: F401
     grn_fold_weight, softmax_rows,
     attention_with_probs, philox_randn, euler_ancestral_philox, brownian_increment, step_param, sampler_step_dev,
     step_advance, vae_out_u8, region_accumulate, region_normalize, clip_embed, pooled_gather,
-    layernorm_stats, lnfold_weights, linear_lnfold, lnfold_available, fourier_filter, tome_match,
+    layernorm_stats, layernorm_stats_for, lnfold_weights, linear_lnfold, lnfold_available, fourier_filter, tome_match,
     rng_key_scope,
 )

@@ -85,10 +85,13 @@ def _skinny_ws(M: int, N: int, K: int, device):
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, act: str | None = None,
-           out: torch.Tensor | None = None) -> torch.Tensor:
+           out: torch.Tensor | None = None, row_stats: bool = False) -> torch.Tensor:
     """y = act(x @ weight^T (+ bias)) (+ residual). ``residual`` has y's shape (fused epilogue add);
     ``act="gelu"`` fuses the GELU into the epilogue (Cascade ChannelMLP Linear -> GELU); ``out``: a
     contiguous [rows, N] destination for the device path (e.g. one image's slice of a batch).
+    ``row_stats``: when the shape runs on the v6 kernel, its epilogue also writes per-row LayerNorm
+    statistics partials of y, attached as ``y._cgs_rowpart`` (see ``layernorm_stats_for``) -- the next
+    LayerNorm-folded GEMM then skips the statistics pass over y.
 
     Device path: the HIP GEMM family (v7 persistent ping-pong 256x256x64 with a register epilogue,
     v6 persistent 256x160, v5 ping-pong 256x256, v3 8-wave 32x32 MFMA, v1 128x128), the kernel picked
@@ -124,8 +127,18 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         if dst is not None:
             assert dst.is_contiguous() and dst.numel() == M * N and dst.dtype == x.dtype, "out: contiguous [M, N]"
 
-        def run_hip(variant):
+        rs_part = []
+
+        def run_hip(variant, final=False):
             o = dst if dst is not None else torch.empty((M, N), device=x.device, dtype=x.dtype)
+            if (final and row_stats and variant == 6 and not gelu and N % 160 == 0 and K % 64 == 0 and K >= 128
+                    and _RSO and _native.has_kernel("cgs_gemm_bf16_rowstats")):
+                part = torch.empty((M, N // 80, 2), device=x.device, dtype=torch.float32)
+                _check(_lib().cgs_gemm_bf16_rowstats(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),
+                                                     M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
+                                                     part.data_ptr(), _stream()), "cgs_gemm_bf16_rowstats")
+                rs_part.append(part)
+                return o
             if M <= 128 and variant in (-1, -2) and K % 32 == 0 and (a.data_ptr() | w.data_ptr()) % 16 == 0:
                 ws = _skinny_ws(M, N, K, x.device)     # split-K slices when N / 16 workgroups underfill
                 if ws is not None:
@@ -176,7 +189,12 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
         variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
-        return run_hip(variant).view(*x.shape[:-1], N)
+        y = run_hip(variant, final=True).view(*x.shape[:-1], N)
+        if rs_part:
+            # (no version counter: inference-mode tensors have none; the consumers take the partials only
+            # on the hook-free transformer path, where y is never modified in place)
+            y._cgs_rowpart = (rs_part[0], y.data_ptr())
+        return y
     if be == "torch":
         count("gemm", "torch")
     else:
@@ -1185,6 +1203,25 @@ def lnfold_available(x: torch.Tensor, K: int) -> bool:
     """The LayerNorm-folded GEMM path applies (device bf16 rows, v7-legal K)."""
     return (_LNFOLD and os.environ.get("CGS_LNFOLD", "1") != "0" and x.is_cuda and x.dtype == torch.bfloat16 and K % 64 == 0 and K >= 128 and K <= 2048
             and backend_for("layernorm", x, "cgs_layernorm_stats") == "hip" and _native.has_kernel("cgs_gemm_bf16_lnfold"))
+
+
+_RSO = os.environ.get("CGS_LN_ROWSTATS", "1") != "0"
+
+
+def layernorm_stats_for(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """``layernorm_stats`` of x, from the partials its producing GEMM wrote (``linear(row_stats=True)``)
+    when they are attached to this tensor; else the statistics pass over x."""
+    h = getattr(x, "_cgs_rowpart", None)
+    if h is not None and h[1] == x.data_ptr() and h[0].shape[0] * 80 * h[0].shape[1] == x.numel() \
+            and _native.has_kernel("cgs_ln_rs_from_partials"):
+        part = h[0]
+        M, P = part.shape[0], part.shape[1]
+        rs = torch.empty((M, 2), device=x.device, dtype=torch.float32)
+        count("layernorm", "hip")
+        _check(_lib().cgs_ln_rs_from_partials(part.data_ptr(), rs.data_ptr(), M, P, float(eps), _stream()),
+               "cgs_ln_rs_from_partials")
+        return rs
+    return layernorm_stats(x, eps)
 
 
 def layernorm_stats(x: torch.Tensor, eps: float) -> torch.Tensor:

@@ -1126,3 +1126,55 @@ def test_dwconv_ln_stats(cuda, N, H, W, C, k, rep):
     yf = y.float().reshape(-1, C)                   # statistics of the stored bf16 values
     assert torch.allclose(rs[:, 0], yf.mean(1), atol=1e-3, rtol=1e-3)
     assert torch.allclose(rs[:, 1], torch.rsqrt(yf.var(1, unbiased=False) + 1e-6), rtol=2e-3)
+
+
+@pytest.mark.parametrize("M,N,K,res", [(65536, 640, 640, True), (16384, 1280, 5120, True), (4100, 1280, 1280, False)])
+def test_gemm_rowstats_epilogue(cuda, M, N, K, res):
+    """v6 GEMM whose epilogue also writes per-row LayerNorm statistics partials (pq::run RSO): the output is
+    bitwise the plain v6 output, and the partials (Chan-combined by cgs_ln_rs_from_partials) give the
+    (mean, rstd) of the stored rows that the statistics pass computes."""
+    torch.manual_seed(5)
+    lib = core._lib()
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16)
+    r = (torch.randn(M, N, device=cuda) * 3 + 2).to(torch.bfloat16) if res else None
+    epi = 1 | (2 if res else 0)
+    y0 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    y1 = torch.empty_like(y0)
+    part = torch.empty(M, N // 80, 2, device=cuda, dtype=torch.float32)
+    s = core._stream()
+    assert lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), y0.data_ptr(), b.data_ptr(), core._ptr(r), M, N, K, K, K, N,
+                               N if res else 0, epi, 1.0, 6, s) == 0
+    assert lib.cgs_gemm_bf16_rowstats(a.data_ptr(), w.data_ptr(), y1.data_ptr(), b.data_ptr(), core._ptr(r), M, N, K,
+                                      K, K, N, N if res else 0, epi, 1.0, part.data_ptr(), s) == 0
+    rs = torch.empty(M, 2, device=cuda, dtype=torch.float32)
+    assert lib.cgs_ln_rs_from_partials(part.data_ptr(), rs.data_ptr(), M, N // 80, 1e-5, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    yf = y1.float()
+    mean = yf.mean(1)
+    rstd = torch.rsqrt(yf.var(1, unbiased=False) + 1e-5)
+    assert (rs[:, 0] - mean).abs().max().item() < 1e-3 * (mean.abs().max().item() + 1)
+    assert ((rs[:, 1] - rstd).abs() / rstd).max().item() < 1e-3
+
+
+def test_transformer_block_rowstats_matches(cuda, monkeypatch):
+    """SDXL transformer block with the LayerNorm statistics taken from the producing GEMMs' epilogues vs the
+    statistics pass (CGS_LN_ROWSTATS off): same output; the block output carries its partials."""
+    from comfy_gen_server_amd.models.attention import BasicTransformerBlock
+    from comfy_gen_server_amd.models.layers import init_random_fast_
+    monkeypatch.setenv("CGS_AUTOTUNE", "1")     # the tuned table (v6 on these shapes) decides the kernel
+    torch.manual_seed(6)
+    blk = BasicTransformerBlock(640, 10, 64, context_dim=2048, dtype=torch.bfloat16, device=cuda)
+    init_random_fast_(blk, seed=3)
+    # the SDXL level-1 shapes at UNet batch 16 (the tuned table runs their GEMMs on v6)
+    x = torch.randn(16, 4096, 640, device=cuda).to(torch.bfloat16)
+    ctx = torch.randn(16, 77, 2048, device=cuda).to(torch.bfloat16)
+    with torch.inference_mode():
+        y1 = blk(x, context=ctx, transformer_options={})
+        assert getattr(y1, "_cgs_rowpart", None) is not None
+        monkeypatch.setattr(core, "_RSO", False)
+        y0 = blk(x, context=ctx, transformer_options={})
+        assert getattr(y0, "_cgs_rowpart", None) is None
+    assert _rel(y1, y0) < 5e-3
