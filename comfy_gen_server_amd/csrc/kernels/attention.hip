@@ -333,7 +333,10 @@ struct KV2 {
 // A persistent form (one WG per CU walking the units, the next unit's K / V / Q streamed in under the last
 // tiles of the current one) was built and measured in round 4: level 2 651 vs 632 TF/s (auto 663), level 1
 // 792 vs 844 (246 VGPRs) -- the per-unit prologue is not where level 2 loses (profiles/r04/
-// attn_persistent_ab_r04ak.log); removed.
+// attn_persistent_ab_r04ak.log); a second version that also issued the next unit's first QK^T under the
+// current unit's last softmax (no pipeline drain between units, 255 VGPRs) measured 663 vs 639-685 at
+// level 2 and 843 vs 834-871 at level 1 (within the run-to-run spread of sequential timing,
+// attn_persistent_v2_r04at.log); removed.
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
 // workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
 template <int NW, bool TWO = false, bool PRIO = true>
