@@ -33,16 +33,25 @@ def _ln(x, eps=1e-6):
 # all off by default: each measured 0.1-0.8 % SLOWER than the separate passes at batch 1 (in-process A/B,
 # profiles/r04/cascade_fusion_ab_r04k.json) -- the GRN / LayerNorm passes they remove are small at these
 # grids while the extra epilogue work sits on the GEMM's critical path
-_FUSE_DEFAULTS = {"GELU_EPI": "0", "LNFOLD": "0", "GRNFOLD": "0", "DWLN": "0"}
+_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0"}
 
 
-def _fuse(name: str) -> bool:
+def _fuse(name: str, rows: int = 0) -> bool:
     """Cascade block fusions (``CGS_CASCADE_<NAME>=0/1`` overrides the default, for A/B runs): GELU_EPI
     (GELU in the first ChannelMLP GEMM), LNFOLD (LayerNorm folded into it), DWLN (its statistics from the
     depthwise kernel: off -- at Stage C's 1152-pixel grids the per-pixel reduction leaves the kernel
     latency-bound, 33 us vs 11 + 9 us for the two passes, profiles/r04/cascade_fusion_profile.md),
-    GRNFOLD (GRN folded into per-image second-GEMM weights)."""
-    return os.environ.get(f"CGS_CASCADE_{name}", _FUSE_DEFAULTS[name]) != "0"
+    GRNFOLD (GRN folded into per-image second-GEMM weights). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
+    (default 4096) pixels per call -- GELU_EPI + LNFOLD measured 2.5 % faster at batch 4 and 0.6 % slower
+    at batch 1 (profiles/r04/cascade_fusion_ab_b4_r04av.json, cascade_fusion_ab_r04k.json)."""
+    v = os.environ.get(f"CGS_CASCADE_{name}", _FUSE_DEFAULTS[name])
+    if v == "auto":
+        return rows >= int(os.environ.get("CGS_CASCADE_FUSE_MIN_ROWS", "4096"))
+    return v != "0"
+
+
+def _rows(x) -> int:
+    return x.numel() // max(1, x.shape[-1])
 
 
 def _cast(w, x):
@@ -114,7 +123,7 @@ class _ChannelMLP(nn.Sequential):
 
     def forward(self, x, residual=None):
         grn = self[2]
-        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4) or not _fuse("GELU_EPI"):
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4) or not _fuse("GELU_EPI", _rows(x)):
             h = ops.grn_nhwc(self[0](x), _cast(grn.gamma, x), _cast(grn.beta, x), pre_gelu=True)
             return self[4](h, residual=residual)
         return self._grn_linear2(self[0](x, act="gelu"), x, residual)
@@ -123,7 +132,7 @@ class _ChannelMLP(nn.Sequential):
         """LayerNorm (no affine) of ``x`` can fold into the first GEMM (device bf16, unhooked weights)."""
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not layers._hooked(self[0])
                 and self[0].weight.dtype == torch.bfloat16 and ops.lnfold_available(x, x.shape[-1])
-                and _fuse("LNFOLD") and _fuse("GELU_EPI"))
+                and _fuse("LNFOLD", _rows(x)) and _fuse("GELU_EPI", _rows(x)))
 
     def forward_ln(self, x, eps=1e-6, residual=None, rs=None):
         """``forward(LN(x))`` with the LayerNorm folded into the first GEMM: only the per-pixel statistics

@@ -163,7 +163,7 @@ def bench_cascade(reps, ab=None):
     n_b = sum(p.numel() for p in pb.model.diffusion_model.parameters()) / 1e9
 
     if ab:
-        return _cascade_ab(ab, reps, pc, pb, vae, pos, neg, NM)
+        return _cascade_ab(ab, reps, pc, pb, vae, pos, neg, NM, batch=int(os.environ.get("CGS_AB_BATCH", "1")))
     for batch in (1, 4):
         def run():
             with torch.inference_mode():
@@ -181,9 +181,9 @@ def bench_cascade(reps, ab=None):
               params_c_b=round(n_c, 3), params_b_b=round(n_b, 3))
 
 
-def _cascade_ab(cfgs, rounds, pc, pb, vae, pos, neg, NM):
-    """Batch-1 Cascade jobs alternating between env configurations (``name:ENV=V,...``) in one process:
-    captured graph plans are dropped on every switch and re-captured in an untimed job."""
+def _cascade_ab(cfgs, rounds, pc, pb, vae, pos, neg, NM, batch=1):
+    """Cascade jobs (``batch`` images) alternating between env configurations (``name:ENV=V,...``) in one
+    process: captured graph plans are dropped on every switch and re-captured in an untimed job."""
     import statistics
 
     def drop(p):
@@ -196,7 +196,7 @@ def _cascade_ab(cfgs, rounds, pc, pb, vae, pos, neg, NM):
 
     def run():
         with torch.inference_mode():
-            lat_c, lat_b = NM["StableCascade_EmptyLatentImage"]().generate(1024, 1024, 42, 1)
+            lat_c, lat_b = NM["StableCascade_EmptyLatentImage"]().generate(1024, 1024, 42, batch)
             out_c = NM["KSampler"]().sample(pc, 5, 20, 4.0, "euler_ancestral", "simple", pos, neg, lat_c, 1.0)[0]
             cond_b = NM["StableCascade_StageB_Conditioning"]().set_prior(pos, out_c)[0]
             neg_b = NM["StableCascade_StageB_Conditioning"]().set_prior(neg, out_c)[0]
