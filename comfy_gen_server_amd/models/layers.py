@@ -148,8 +148,9 @@ class Conv2d(nn.Module, DerivedMixin, CastWeightBiasOp):
     def weight_nhwc(self):
         return self._derived_get("w_nhwc", lambda: self.weight.permute(0, 2, 3, 1).contiguous())
 
-    def forward(self, x, residual=None, upsample2x=False, x2=None):
-        """``x2``: convolve cat([x, x2], 1) without materialising the concat (K14)."""
+    def forward(self, x, residual=None, upsample2x=False, x2=None, gn_stats=False):
+        """``x2``: convolve cat([x, x2], 1) without materialising the concat (K14). ``gn_stats``: the next op
+        is a GroupNorm over the output (``ops.conv2d`` statistics partials from the epilogue)."""
         if _hooked(self):    # per-call weight / bias hooks: transformed weights, no cached layouts
             if x2 is not None:
                 x = torch.cat([x, x2], dim=1)
@@ -161,7 +162,7 @@ class Conv2d(nn.Module, DerivedMixin, CastWeightBiasOp):
         if x2 is not None:
             if x.is_cuda and self.groups == 1 and w.dtype == x.dtype and w.device == x.device:
                 return ops.conv2d(x, w, b, self.stride, self.padding, residual=residual,
-                                  weight_nhwc=self.weight_nhwc(), groups=self.groups, x2=x2)
+                                  weight_nhwc=self.weight_nhwc(), groups=self.groups, x2=x2, gn_stats=gn_stats)
             x = torch.cat([x, x2], dim=1)
         if w.dtype != x.dtype or w.device != x.device:
             w = w.to(device=x.device, dtype=x.dtype)
@@ -184,7 +185,7 @@ class Conv2d(nn.Module, DerivedMixin, CastWeightBiasOp):
         elif x.is_cuda and self.groups == 1:
             wn = self.weight_nhwc()
         return ops.conv2d(x, w, b, self.stride, self.padding, residual=residual, weight_nhwc=wn,
-                          groups=self.groups, upsample2x=upsample2x)
+                          groups=self.groups, upsample2x=upsample2x, gn_stats=gn_stats)
 
 
 class Conv3d(nn.Module, DerivedMixin):

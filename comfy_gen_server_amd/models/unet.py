@@ -75,10 +75,10 @@ class ResBlock(nn.Module):
             if isinstance(self.skip_connection, nn.Identity):
                 x = x.materialize()
             else:
-                h = self.in_layers[2](self.in_layers[0](x.a, silu=True, x2=x.b))
+                h = self.in_layers[2](self.in_layers[0](x.a, silu=True, x2=x.b), gn_stats=True)
                 return self._out(h, emb_silu, self.skip_connection(x.a, x2=x.b))
         h = self.in_layers[0](x, silu=True)
-        h = self.in_layers[2](h)
+        h = self.in_layers[2](h, gn_stats=True)      # out_layers' GroupNorm statistics from its epilogue
         skip = x if isinstance(self.skip_connection, nn.Identity) else None
         return self._out(h, emb_silu, skip if skip is not None else self.skip_connection(x))
 

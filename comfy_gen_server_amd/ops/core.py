@@ -696,6 +696,16 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
         pa = None
         if pre_add is not None:
             pa = pre_add.to(x.dtype).contiguous()
+        gp = getattr(x, "_cgs_gnpart", None) if x2 is None else None
+        if gp is not None and gp[1] == x.data_ptr() and xc is x and gp[0].numel() == N * (H * W // 64) * C * 2 \
+                and _native.has_kernel("cgs_groupnorm_nhwc_part"):
+            # statistics from the producing conv's epilogue (conv2d(gn_stats=True)): finalize + apply only
+            ab = torch.empty(N * C * 2, device=x.device, dtype=torch.float32)
+            _check(_lib().cgs_groupnorm_nhwc_part(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
+                                                  _ptr(pa), gp[0].data_ptr(), ab.data_ptr(), N, H * W, C, groups, 64,
+                                                  float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
+                   "cgs_groupnorm_nhwc_part")
+            return y
         wsb = int(_lib().cgs_groupnorm_workspace(N, H * W, C))
         ws = torch.empty((wsb + 3) // 4, device=x.device, dtype=torch.float32)
         if x2 is None:
@@ -755,12 +765,16 @@ def _spatial():
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
            residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
-           groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
+           groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None,
+           gn_stats: bool = False) -> torch.Tensor:
     """2-D convolution; inside a row-sharded UNet call (latency mode, parallel/spatial.py) the halo rows
-    come from the neighbouring ranks and the residual is added to the kept interior."""
+    come from the neighbouring ranks and the residual is added to the kept interior. ``gn_stats``: when the
+    shape runs on the v6 kernel, its epilogue also writes GroupNorm statistics partials of the output
+    (per image, 64-pixel block and channel), attached as ``y._cgs_gnpart`` -- ``group_norm`` over y then
+    skips its statistics pass."""
     sc = _spatial()
     if sc is None:
-        return _conv2d(x, weight, bias, stride, padding, residual, weight_nhwc, groups, upsample2x, x2)
+        return _conv2d(x, weight, bias, stride, padding, residual, weight_nhwc, groups, upsample2x, x2, gn_stats)
     st = stride[0] if isinstance(stride, (tuple, list)) else stride
     pd = padding[0] if isinstance(padding, (tuple, list)) else padding
     y = sc.conv2d(lambda xx, _: _conv2d(xx, weight, bias, st, pd, None, weight_nhwc, groups, upsample2x, None),
@@ -772,7 +786,8 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, str
 
 def _conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
             residual: torch.Tensor | None = None, weight_nhwc: torch.Tensor | None = None,
-            groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
+            groups: int = 1, upsample2x: bool = False, x2: torch.Tensor | None = None,
+            gn_stats: bool = False) -> torch.Tensor:
     """2-D convolution (K09/K10/K12). Device path: implicit-GEMM NHWC kernel on MFMA
     (csrc/kernels/conv.hip) with fused bias + residual epilogue; ``weight_nhwc`` = weight permuted
     to [Cout, kh, kw, Cin]. ``upsample2x`` reads the input through a nearest-2x upsample inside the
@@ -836,6 +851,16 @@ def _conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, st
             choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None))
                                      + ((("dual", C1),) if x2c is not None else ()), cands, default="auto")
             variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7, "v8": 8, "auto": -2}[choice]
+        if (gn_stats and variant == 6 and _GNS and (Ho * Wo) % 256 == 0 and Cin % 64 == 0 and C1 % 64 == 0
+                and Cout % 8 == 0 and kh * kw * Cin >= 128 and (bias is None or bias.data_ptr() % 8 == 0)
+                and _native.has_kernel("cgs_conv2d_nhwc_gns")):
+            out = torch.empty((N, Cout, Ho, Wo), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+            part = torch.empty(N * (Ho * Wo // 64) * Cout * 2, device=x.device, dtype=torch.float32)
+            _check(_lib().cgs_conv2d_nhwc_gns(xc.data_ptr(), _ptr(x2c), C1, weight_nhwc.data_ptr(), _ptr(bias),
+                                              _ptr(r), out.data_ptr(), N, H, W, Cin, Cout, kh, kw, stride, padding,
+                                              Ho, Wo, flags, part.data_ptr(), _stream()), "cgs_conv2d_nhwc_gns")
+            out._cgs_gnpart = (part, out.data_ptr())
+            return out
         return run(variant)
     if upsample2x:
         x = upsample_nearest2x(x)
@@ -1206,6 +1231,7 @@ def lnfold_available(x: torch.Tensor, K: int) -> bool:
 
 
 _RSO = os.environ.get("CGS_LN_ROWSTATS", "1") != "0"
+_GNS = os.environ.get("CGS_GN_CONVSTATS", "1") != "0"
 
 
 def layernorm_stats_for(x: torch.Tensor, eps: float) -> torch.Tensor:

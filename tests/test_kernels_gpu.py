@@ -923,7 +923,7 @@ def test_channel_affine_nhwc(cuda, N, H, W, C):
 @pytest.mark.parametrize("N,H,W,Cin,Cout,pre", [(2, 32, 32, 320, 320, True), (1, 16, 16, 640, 640, False),
                                                  (2, 16, 32, 128, 160, True)])
 def test_conv_gn_stats_epilogue(cuda, N, H, W, Cin, Cout, pre):
-    """K06 second half (measured, not wired: profiles/r03/gn_stats_in_conv_epilogue.log): the v6 conv's
+    """K06 second half (wired for the UNet ResBlock since r04: profiles/r04/gn_convstats_ab_r04ax.log): the v6 conv's
     epilogue writes the GroupNorm partials of its bf16 output; finalize + apply from them == the GroupNorm
     of the stored conv output (pre-add shift included)."""
     torch.manual_seed(3)
@@ -952,6 +952,33 @@ def test_conv_gn_stats_epilogue(cuda, N, H, W, Cin, Cout, pre):
     xf = out.permute(0, 3, 1, 2).float() + (p.float()[:, :, None, None] if pre else 0.0)
     ref = F.silu(F.group_norm(xf, 32, g.float(), be.float(), 1e-5))
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_conv_gn_stats_wired(cuda, monkeypatch):
+    """ops.conv2d(gn_stats=True) -> ops.group_norm (the UNet ResBlock's in_layers conv -> out_layers GroupNorm,
+    models/unet.py): the statistics come from the conv epilogue and the result equals the two-pass GroupNorm.
+    The shape is a packaged-table key whose tuned kernel is v6 (the only one with the statistics epilogue)."""
+    monkeypatch.setenv("CGS_AUTOTUNE", "1")
+    torch.manual_seed(5)
+    N, H, W, Cin, Cout = 2, 128, 128, 320, 320
+    x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 3, 3, device=cuda) / math.sqrt(Cin * 9)).to(torch.bfloat16)
+    b = torch.randn(Cout, device=cuda).to(torch.bfloat16)
+    wn = w.permute(0, 2, 3, 1).contiguous()
+    g = (1 + 0.1 * torch.randn(Cout, device=cuda)).to(torch.bfloat16)
+    be = (0.1 * torch.randn(Cout, device=cuda)).to(torch.bfloat16)
+    pre = torch.randn(N, Cout, device=cuda).to(torch.bfloat16)
+    h = ops.conv2d(x, w, b, 1, 1, weight_nhwc=wn, gn_stats=True)
+    assert getattr(h, "_cgs_gnpart", None) is not None, "tuned v6 conv did not take the statistics epilogue"
+    y = ops.group_norm(h, 32, g, be, 1e-5, silu=True, pre_add=pre)
+    h_plain = ops.conv2d(x, w, b, 1, 1, weight_nhwc=wn)
+    assert getattr(h_plain, "_cgs_gnpart", None) is None
+    y_ref = ops.group_norm(h_plain, 32, g, be, 1e-5, silu=True, pre_add=pre)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_plain)
+    assert (y.float() - y_ref.float()).abs().max().item() < 0.05
+    ref = F.silu(F.group_norm(h.float() + pre.float()[:, :, None, None], 32, g.float(), be.float(), 1e-5))
+    assert _rel(y, ref) < 1e-2
 
 
 @pytest.mark.parametrize("B,H,Sq,S2", [(2, 32, 576, 85), (1, 8, 300, 77), (2, 4, 1024, 8)])
