@@ -185,6 +185,9 @@ KERNEL_SIGNATURES = {
     "cgs_w4_set_group": [_I],
     # experiment: 4-slot-ring one-wave-per-SIMD GEMM (bias / residual epilogue only)
     "cgs_gemm_bf16_w5": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
+    "cgs_gemm_bf16_w5_dbg": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
+    "cgs_gemm_bf16_w6": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _I, _I, _P],
+    "cgs_gemm_w6_ok": [_I, _I, _I, _L, _L, _L, _L, _I],
     # skinny GEMM (M <= 128) with its split-K workspace
     "cgs_gemm_skinny_ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
     "cgs_gemm_skinny_ws_bytes": [_I, _I, _I],

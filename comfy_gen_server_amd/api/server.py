@@ -374,6 +374,11 @@ class PromptServer:
                 "runtime": {"resident_models": len(dm.current_loaded_models), "metrics": dict(self.metrics),
                             "telemetry": _telemetry_snapshot()},
             }
+            if self.cluster is not None:     # node-wide serving (sched/cluster.py)
+                c = self.cluster
+                stats["cluster"] = {"world": c.world, "generation": c.gen, "regroups": c.regroups,
+                                    "dead": sorted(c.dead), "busy": {str(r): p for r, p in dict(c.busy).items()},
+                                    "spmd_sizes": sorted(c.ctxs)}
             return web.json_response(stats)
 
         @routes.get("/prompt")

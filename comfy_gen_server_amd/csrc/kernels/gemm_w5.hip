@@ -35,6 +35,9 @@ __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 
 __device__ __forceinline__ int swz(int r) { return (-(r >> 2)) & 3; }
 
+// DBG (ablation probes, tools/probes/w5_ablate.py): bit 0 = no main-loop DMAs, bit 1 = no main-loop
+// fragment reads (the MFMAs re-use stale fragments), bit 2 = no per-stage wait + barrier.
+template <int DBG>
 __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, const u16* __restrict__ W, long long ldw,
                                     int M, int N, int K, const mc::Epi& e, unsigned char* smem, int tiles_m,
                                     int tiles_n, int group_m) {
@@ -98,16 +101,18 @@ __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, co
     constexpr int SL = decltype(slot_c)::value;
     constexpr int NX = (SL + 1) & 3, DS = (SL + 3) & 3;
     fence();
-    mc::wait_vmcnt<8>();              // stage s+1 landed (this wave); stage s+2 may stay in flight
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of `cur` are done
-    __builtin_amdgcn_s_barrier();     // ... and every wave's: slot DS is dead, stage s+1 is visible
+    if constexpr (!(DBG & 4)) {
+      mc::wait_vmcnt<8>();              // stage s+1 landed (this wave); stage s+2 may stay in flight
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of `cur` are done
+      __builtin_amdgcn_s_barrier();     // ... and every wave's: slot DS is dead, stage s+1 is visible
+    }
     fence();
     const int sd = s + 3 < ns ? s + 3 : ns - 1;   // past the end: harmless reload into the dead slot
     // program order = issue order: r0 r1 d0 r2 r3 d1 ... (16 reads, 8 DMAs)
     mc::static_for<0, 16>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
-      nxt[g] = *frag_addr(NX, g);
-      if constexpr (g & 1) dma(g >> 1, DS, sd);
+      if constexpr (!(DBG & 2)) nxt[g] = *frag_addr(NX, g);
+      if constexpr ((g & 1) && !(DBG & 1)) dma(g >> 1, DS, sd);
     });
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -119,8 +124,8 @@ __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, co
     mc::static_for<0, 16>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // 3 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
-      if constexpr (g & 1) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);   // 1 VMEM (DMA)
+      if constexpr (!(DBG & 2)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+      if constexpr ((g & 1) && !(DBG & 1)) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);   // 1 VMEM (DMA)
     });
     __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
     fence();
@@ -160,21 +165,24 @@ __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, co
 
 }  // namespace w5
 
+template <int DBG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_bf16_nt_w5_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
     int epi, float alpha, int tiles_m, int tiles_n, int group_m) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   mc::Epi e{C, bias, R, ldc, ldr, epi, alpha};
-  w5::run(A, lda, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  w5::run<DBG>(A, lda, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
 }
 
 static int g_w5_group = -1;
 
+
 // epi: 1 bias, 2 residual (no GEGLU / LayerNorm fold / fp32 out).
-CGS_EXPORT int cgs_gemm_bf16_w5(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
-                                int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                                hipStream_t stream) {
+template <int DBG>
+static int launch_w5(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                     long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                     hipStream_t stream) {
   if (K % 128 || K < 128 || N % 4 || lda % 8 || ldw % 8 || ldc % 4 || ((epi & MC_EPI_RESIDUAL) && ldr % 4) ||
       (epi & (MC_EPI_GEGLU | MC_EPI_LNFOLD | MC_EPI_F32OUT | MC_EPI_GELU)) ||
       ((uintptr_t)A | (uintptr_t)W) % 16 || ((uintptr_t)C | (uintptr_t)R | (uintptr_t)bias) % 8 ||
@@ -183,7 +191,7 @@ CGS_EXPORT int cgs_gemm_bf16_w5(const void* A, const void* W, void* C, const voi
   if (M == 0 || N == 0) return 0;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_w5_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_w5_kernel<DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               w5::LDS);
     attr_set = true;
   }
@@ -191,8 +199,29 @@ CGS_EXPORT int cgs_gemm_bf16_w5(const void* A, const void* W, void* C, const voi
   const int tiles_m = (M + w5::BM - 1) / w5::BM, tiles_n = (N + w5::BN - 1) / w5::BN;
   const long long T = (long long)tiles_m * tiles_n;
   if (T > 0x7fffffffLL) return (int)hipErrorInvalidValue;
-  gemm_bf16_nt_w5_kernel<<<(unsigned)T, w5::THREADS, w5::LDS, stream>>>(
+  gemm_bf16_nt_w5_kernel<DBG><<<(unsigned)T, w5::THREADS, w5::LDS, stream>>>(
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
       tiles_m, tiles_n, g_w5_group);
   return (int)hipGetLastError();
+}
+
+CGS_EXPORT int cgs_gemm_bf16_w5(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
+                                int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                                hipStream_t stream) {
+  return launch_w5<0>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+}
+
+// ablation probes (results are wrong by design for dbg != 0)
+CGS_EXPORT int cgs_gemm_bf16_w5_dbg(const void* A, const void* W, void* C, const void* bias, const void* R, int M,
+                                    int N, int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                                    float alpha, int dbg, hipStream_t stream) {
+  switch (dbg) {
+    case 0: return launch_w5<0>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    case 1: return launch_w5<1>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    case 2: return launch_w5<2>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    case 3: return launch_w5<3>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    case 4: return launch_w5<4>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    case 7: return launch_w5<7>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
 }

@@ -16,11 +16,13 @@ Run: ``python -m comfy_gen_server_amd.main --listen 0.0.0.0 --port 8188`` (or ``
 from __future__ import annotations
 
 import asyncio
+import copy
 import functools
 import gc
 import itertools
 import logging
 import os
+import queue as _queue
 import shutil
 import threading
 import time
@@ -124,7 +126,49 @@ def _finish_prompt(q, server, item_id, prompt_id, outputs_ui, success, messages,
     logging.info("Prompt executed in %.2f seconds", dt)
 
 
-def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_interval: float = 10.0):
+class _OrderedFinisher:
+    """One thread completes prompts in submission order: it waits for a prompt's PNG encodes, then
+    reports it (``task_done`` + the end-of-prompt ``executing`` sentinel + metrics). A single consumer
+    keeps completions ordered and the metrics single-writer; ``task_done`` runs even when the encode
+    wait raises, so no prompt stays in ``currently_running``."""
+
+    def __init__(self):
+        self._q: _queue.Queue = _queue.Queue()
+        self._t = threading.Thread(target=self._loop, name="prompt-finisher", daemon=True)
+        self._t.start()
+
+    def submit(self, done, futs):
+        self._q.put((done, futs))
+
+    def drain(self, timeout: float | None = None):
+        """Block until every submitted completion has run (tests, shutdown)."""
+        t0 = time.perf_counter()
+        while self._q.unfinished_tasks:
+            if timeout is not None and time.perf_counter() - t0 > timeout:
+                return False
+            time.sleep(0.005)
+        return True
+
+    def _loop(self):
+        from .utils import imageio
+        while True:
+            done, futs = self._q.get()
+            errs = []
+            try:
+                try:
+                    errs = imageio.wait_futures(futs) if futs else []
+                except Exception as ex:     # noqa: BLE001 - a failed wait is a save error, not a lost prompt
+                    errs = [f"{type(ex).__name__}: {ex}"]
+                finally:
+                    done(errs)
+            except Exception:               # noqa: BLE001
+                logging.exception("prompt completion failed")
+            finally:
+                self._q.task_done()
+
+
+def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_interval: float = 10.0,
+                  finisher: _OrderedFinisher | None = None):
     """Blocking worker loop (reference ``main.py:93-146``)."""
     from .graph.executor import PromptExecutor
     from .runtime import device as dm
@@ -132,6 +176,7 @@ def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_inter
 
     e = PromptExecutor(server)
     imageio.defer_saves(True)
+    fin = finisher if finisher is not None else _OrderedFinisher()
     last_gc = time.perf_counter()
     need_gc = False
     timeout = 1000.0
@@ -146,14 +191,12 @@ def prompt_worker(q, server, stop_event: threading.Event | None = None, gc_inter
                 e.execute(item[2], prompt_id, item[3], item[4])
             need_gc = True
             # the prompt's PNG encodes (utils/imageio async saves) finish behind the next prompt; the
-            # prompt is reported complete once its files are on disk
+            # prompt is reported complete once its files are on disk. The next execute() rewrites
+            # e.outputs_ui in place, so the finisher gets a snapshot of this prompt's outputs.
             futs = imageio.take_pending()
-            done = functools.partial(_finish_prompt, q, server, item_id, prompt_id, e.outputs_ui, e.success,
-                                     list(e.status_messages), t0, server.client_id)
-            if futs:
-                threading.Thread(target=lambda d=done, f=futs: d(imageio.wait_futures(f)), daemon=True).start()
-            else:
-                done([])
+            done = functools.partial(_finish_prompt, q, server, item_id, prompt_id, copy.deepcopy(e.outputs_ui),
+                                     e.success, list(e.status_messages), t0, server.client_id)
+            fin.submit(done, futs)
 
         flags = q.get_flags()
         free_memory = flags.get("free_memory", False)
@@ -205,7 +248,9 @@ def _cluster_start(args, argv):
         import sys as _sys
         listener, procs = cluster.launch(args.gpus, list(argv) if argv is not None else _sys.argv[1:])
     from .parallel.comm import init_from_env
-    comm = init_from_env(backend="gloo" if args.cpu else None)
+    # a replacement rank (sched/cluster.py respawn) joins the process group at the next re-rendezvous
+    join = os.environ.get("CGS_SCHED_RESPAWN") != "1"
+    comm = init_from_env(backend="gloo" if args.cpu else None, join=join)
     return role, comm, listener, procs
 
 
@@ -217,7 +262,7 @@ def _worker_rank_main(args, comm):
                         custom_dirs=list(itertools.chain.from_iterable(args.custom_nodes_directory))
                         if args.custom_nodes_directory else None)
     addr, key = cluster.worker_address()
-    cluster.worker_main(comm, addr, key)
+    cluster.worker_main(comm, addr, key, respawned=os.environ.get("CGS_SCHED_RESPAWN") == "1")
     comm.shutdown()
     return 0
 
@@ -271,7 +316,7 @@ def main(argv=None):
         grpc_srv.stop(grace=1.0)
     if coord is not None:
         coord.shutdown()
-        for p in cluster_state[3] or []:
+        for p in list(cluster_state[3] or []) + list(coord.procs):
             try:
                 p.wait(timeout=30)
             except Exception:

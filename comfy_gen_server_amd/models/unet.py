@@ -312,6 +312,10 @@ class UNetModel(nn.Module):
                  device=None, build_decoder=True, **unused):
         super().__init__()
         self.default_num_video_frames = None
+        # latency mode may cut this network into row bands (parallel/latency.py): every layer is
+        # band-aware (halo convs, group-summed GroupNorm, sequence-parallel attention) unless temporal
+        # layers mix frames through the band-local ops
+        self.row_shardable = not (use_temporal_attention or use_temporal_resblock)
         vks = video_kernel_size if video_kernel_size is not None else [3, 1, 1]
 
         def resblock(ch_in, emb_ch, ch_out, **kw2):

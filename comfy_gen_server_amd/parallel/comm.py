@@ -30,8 +30,12 @@ class Comm:
         self.local_rank = 0
         self.backend = None
         self.device = torch.device("cpu")
+        self.group = None     # data-plane group (None: the default group)
         self.ctrl = None      # Gloo group for host-side control traffic (None: the default group)
         self.bytes_moved = 0  # tensor bytes this rank sent + received in gathers (serving metrics)
+        self.load_bytes = 0   # checkpoint bytes sent / received by ``broadcast_state_dict`` (R3)
+        self.gen = 0          # process-group generation (bumped by every re-rendezvous, ``reinit``)
+        self.subsets = {}     # k -> SubComm over ranks [0, k) (``build_subsets``)
 
     degraded = False   # set by the DP engine after a rank failure: the process group is unusable
 
@@ -42,9 +46,9 @@ class Comm:
     def barrier(self):
         if self.enabled:
             if self.backend == "nccl":
-                dist.barrier(device_ids=[self.local_rank])
+                dist.barrier(group=self.group, device_ids=[self.local_rank])
             else:
-                dist.barrier()
+                dist.barrier(group=self.group)
 
     def broadcast_object(self, obj, src=0):
         """R1 over the Gloo control group: no device sync, no RCCL op on the issuing stream."""
@@ -69,7 +73,7 @@ class Comm:
 
     def broadcast_tensor(self, t, src=0):
         if self.enabled:
-            dist.broadcast(t, src=src)
+            dist.broadcast(t, src=src, group=self.group)
         return t
 
     @torch.no_grad()
@@ -90,7 +94,7 @@ class Comm:
                     continue
                 if bucket:
                     flat = torch.cat([b.reshape(-1) for b in bucket])
-                    dist.broadcast(flat, src=src)
+                    dist.broadcast(flat, src=src, group=self.group)
                     off = 0
                     for b in bucket:
                         n = b.numel()
@@ -99,13 +103,110 @@ class Comm:
                 bucket, size = ([t], t.numel() * t.element_size()) if t is not None else ([], 0)
         return module
 
+    @torch.no_grad()
+    def broadcast_state_dict(self, sd, device, src=0, bucket_bytes=256 << 20):
+        """R3 for a checkpoint's raw state dict: ``src`` (which read the file) sends the key / shape / dtype
+        table over the control group, then the tensors in same-dtype buckets over the data plane (RCCL over
+        xGMI on the GPU); the other ranks allocate and receive them on ``device`` without touching the file.
+        ``sd`` is None on the receivers. An exception object in place of ``sd`` on ``src`` is re-raised on
+        every rank (a failed load fails the node everywhere)."""
+        if not self.enabled:
+            return sd
+        if self.rank == src:
+            if isinstance(sd, BaseException):
+                self.broadcast_object({"error": f"{type(sd).__name__}: {sd}"}, src=src)
+                raise sd
+            table = [(k, tuple(v.shape), str(v.dtype).replace("torch.", "")) for k, v in sd.items()]
+            self.broadcast_object({"table": table}, src=src)
+        else:
+            msg = self.broadcast_object(None, src=src)
+            if "error" in msg:
+                raise RuntimeError(f"checkpoint load failed on rank {src}: {msg['error']}")
+            table = msg["table"]
+            sd = {k: torch.empty(shape, dtype=getattr(torch, dt), device=device) for k, shape, dt in table}
+        xdev = self.device if self.backend == "nccl" else torch.device("cpu")
+        names = list(sd.keys())
+        by_dt = {}
+        for k in names:
+            by_dt.setdefault(sd[k].dtype, []).append(k)
+        for dt, keys in by_dt.items():
+            bucket, size = [], 0
+            for k in keys + [None]:
+                nb = 0 if k is None else sd[k].numel() * sd[k].element_size()
+                if k is not None and (size + nb <= bucket_bytes or not bucket):
+                    bucket.append(k)
+                    size += nb
+                    continue
+                if bucket:
+                    n = sum(sd[b].numel() for b in bucket)
+                    if self.rank == src:
+                        flat = torch.cat([sd[b].reshape(-1).to(xdev) for b in bucket]) if n else \
+                            torch.empty(0, dtype=dt, device=xdev)
+                    else:
+                        flat = torch.empty(n, dtype=dt, device=xdev)
+                    dist.broadcast(flat, src=src, group=self.group)
+                    self.load_bytes += flat.numel() * flat.element_size()
+                    if self.rank != src:
+                        off = 0
+                        for b in bucket:
+                            m = sd[b].numel()
+                            sd[b].copy_(flat[off:off + m].view_as(sd[b]))
+                            off += m
+                bucket, size = ([k], nb) if k is not None else ([], 0)
+        return sd
+
+    def build_subsets(self, sizes=None):
+        """Data/control groups over the rank prefixes [0, k) for every k in ``sizes`` (default 2..world-1;
+        k = world is this communicator itself). Collective over the default group: every rank calls it
+        with the same sizes in the same order (right after ``init_from_env`` / ``reinit``). A prompt whose
+        image batch is smaller than the node then runs SPMD on k ranks while the others serve single
+        prompts; after a rank death the prefixes below it stay usable until the re-rendezvous."""
+        self.subsets = {}
+        if self.world <= 1:
+            return self.subsets
+        sizes = sorted(set(sizes if sizes is not None else range(2, self.world)))
+        for k in sizes:
+            if not 2 <= k < self.world:
+                continue
+            ranks = list(range(k))
+            g = dist.new_group(ranks)
+            c = dist.new_group(ranks, backend="gloo") if self.backend == "nccl" else g
+            if self.rank < k:
+                self.subsets[k] = SubComm(self, k, g, c)
+        self.subsets[self.world] = self
+        return self.subsets
+
+    def reinit(self, port: int, gen: int, addr: str = "127.0.0.1", timeout_s: float = 600.0):
+        """Re-rendezvous after a rank death: leave the broken process group (a member is gone, so its
+        collectives can never complete) and join generation ``gen`` over a fresh TCPStore on ``port``
+        (hosted by rank 0), together with the survivors and the respawned rank. Never re-execs the
+        process (the GPU context stays)."""
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:        # pragma: no cover - a broken group may not tear down cleanly
+                pass
+        self.degraded = False
+        self.gen = gen
+        self.group = None
+        kw = dict(backend=self.backend or ("nccl" if self.device.type == "cuda" else "gloo"),
+                  init_method=f"tcp://{addr}:{port}", rank=self.rank, world_size=self.world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if kw["backend"] == "nccl":
+            kw["device_id"] = self.device
+        dist.init_process_group(**kw)
+        self.backend = kw["backend"]
+        self.ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s)) \
+            if self.backend == "nccl" else None
+        return self
+
     def all_gather(self, t):
         """Concatenate ``t`` (same shape on every rank) along dim 0 across ranks."""
         if not self.enabled:
             return t
         t = t.contiguous()
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t)
+        dist.all_gather_into_tensor(out, t, group=self.group)
         self.bytes_moved += out.numel() * out.element_size()      # own shard out, every other shard in
         return out
 
@@ -119,10 +220,10 @@ class Comm:
         nb = t.numel() * t.element_size()
         if self.rank == dst:
             parts = [torch.empty_like(t) for _ in range(self.world)]
-            dist.gather(t, gather_list=parts, dst=dst)
+            dist.gather(t, gather_list=parts, dst=dst, group=self.group)
             self.bytes_moved += (self.world - 1) * nb
             return torch.cat(parts)
-        dist.gather(t, dst=dst)
+        dist.gather(t, dst=dst, group=self.group)
         self.bytes_moved += nb
         return None
 
@@ -144,7 +245,7 @@ class Comm:
         if not self.enabled:
             return 1
         t = torch.ones(1, dtype=torch.int32, device=self.device)
-        dist.all_reduce(t)
+        dist.all_reduce(t, group=self.group)
         return int(t.item())
 
     # ---- control plane (R6): the c10d TCPStore (hosted by rank 0) outlives a dead peer, unlike a
@@ -199,6 +300,28 @@ class Comm:
             dist.destroy_process_group()
 
 
+class SubComm(Comm):
+    """A view of ``parent`` restricted to ranks [0, k): the same rank numbers (rank 0 stays the
+    coordinator), collectives on the prefix's own data / control groups, the parent's store."""
+
+    def __init__(self, parent: Comm, k: int, group, ctrl):
+        super().__init__()
+        self.parent = parent
+        self.rank, self.world, self.local_rank = parent.rank, k, parent.local_rank
+        self.backend, self.device, self.gen = parent.backend, parent.device, parent.gen
+        self.group, self.ctrl = group, ctrl
+
+    @property
+    def enabled(self):
+        return self.world > 1 and not self.parent.degraded
+
+    def store(self):
+        return self.parent.store()
+
+    def shutdown(self):     # the parent owns the process group
+        pass
+
+
 _COMM = Comm()
 
 
@@ -206,8 +329,9 @@ def get_comm() -> Comm:
     return _COMM
 
 
-def init_from_env(backend=None, timeout_s=600) -> Comm:
-    """Initialise from torchrun env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT)."""
+def init_from_env(backend=None, timeout_s=600, join=True) -> Comm:
+    """Initialise from torchrun env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT).
+    ``join=False``: rank, world and device only (a replacement rank joins later through ``reinit``)."""
     c = _COMM
     world = int(os.environ.get("WORLD_SIZE", "1"))
     c.rank = int(os.environ.get("RANK", "0"))
@@ -217,7 +341,9 @@ def init_from_env(backend=None, timeout_s=600) -> Comm:
     if use_gpu:
         torch.cuda.set_device(c.local_rank)
         c.device = torch.device("cuda", c.local_rank)
-    if world > 1 and not dist.is_initialized():
+    if world > 1 and not join:
+        c.backend = backend or ("nccl" if use_gpu else "gloo")
+    elif world > 1 and not dist.is_initialized():
         c.backend = backend or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=c.backend, timeout=datetime.timedelta(seconds=timeout_s))

@@ -67,10 +67,21 @@ class LatencyParallel:
         self.spatial_calls = 0
         self.calls = 0
 
-    def _spatial_ok(self, x, c):
-        """Row sharding applies: a band per rank at every level (height divisible by Q * 8: up to three
-        2x downsamples, >= 1 row per band), no model patches (their hooks see whole images)."""
+    @staticmethod
+    def _row_shardable(apply_model):
+        """Only networks whose every layer is band-aware: the openaimodel UNet (``UNetModel.row_shardable``).
+        Cascade's depthwise convs / GRN and any other family would treat band edges as image edges."""
+        owner = getattr(apply_model, "__self__", None)
+        net = getattr(owner, "diffusion_model", None)
+        return getattr(net, "row_shardable", False) is True
+
+    def _spatial_ok(self, x, c, apply_model=None):
+        """Row sharding applies: a row-shardable network (see ``_row_shardable``), a band per rank at every
+        level (height divisible by Q * 8: up to three 2x downsamples, >= 1 row per band), no model patches
+        (their hooks see whole images)."""
         if self.spatial is None or os.environ.get("CGS_LATENCY_SPATIAL", "1") == "0":
+            return False
+        if not self._row_shardable(apply_model):
             return False
         to = c.get("transformer_options", {})
         if to.get("patches") or to.get("patches_replace"):
@@ -113,13 +124,13 @@ class LatencyParallel:
             to["sp"] = self.sp
         c["transformer_options"] = to
         if self.G == 1 or B % self.G:
-            if self._spatial_ok(x, c):
+            if self._spatial_ok(x, c, apply_model):
                 return self._apply_spatial(apply_model, x, t, c)
             return apply_model(x, t, **c)
         n = B // self.G
         lo, hi = self.bg * n, (self.bg + 1) * n
         cs = self._slice(c, B, lo, hi)
-        if self._spatial_ok(x, cs):
+        if self._spatial_ok(x, cs, apply_model):
             out = self._apply_spatial(apply_model, x[lo:hi], t[lo:hi], cs)
         else:
             out = apply_model(x[lo:hi], t[lo:hi], **cs)

@@ -98,8 +98,33 @@ def _load_safetensors(path, device="cpu"):
     return safetensors.torch.load_file(path, device=str(device))
 
 
+FILE_READS: list = []     # paths this process read from disk (serving metrics / the R3 broadcast tests)
+
+
+def _trace_read(path):
+    FILE_READS.append(path)
+    tr = os.environ.get("CGS_TRACE_LOADS")
+    if tr:
+        with open(tr, "a") as fh:
+            fh.write(f"{os.environ.get('RANK', '0')} {path}\n")
+
+
 def load_state_dict(path, safe_load=True, device=None, return_metadata=False):
+    """A checkpoint's state dict. Inside an SPMD prompt of several ranks (``sched/spmd.py``) only rank 0
+    reads the file; the other ranks receive the tensors over the data plane (one disk
+    read per node, RCCL over xGMI into each rank's HBM)."""
     device = device or torch.device("cpu")
+    if os.environ.get("CGS_SPMD_BCAST_LOAD", "1") != "0":
+        from ..sched import spmd as _spmd
+        ctx = _spmd.active()
+        if ctx is not None and ctx.world > 1 and ctx.comm.enabled:
+            return ctx.load_state_dict(path, device, return_metadata,
+                                       lambda: _load_local(path, device, return_metadata))
+    return _load_local(path, device, return_metadata)
+
+
+def _load_local(path, device, return_metadata=False):
+    _trace_read(path)
     meta = None
     if path.lower().endswith(".safetensors") or path.lower().endswith(".sft"):
         sd = _load_safetensors(path, device)

@@ -17,9 +17,17 @@ Transport: JSON messages over ``multiprocessing.connection`` (authenticated loca
 requests and interrupts down, WS events and completions up. Rank 0 forwards a worker's events to the
 submitting client (``sid``); binary preview frames of remote ranks are not forwarded.
 
-Ranks keep two executors each: one sees only SPMD prompts (identical caches on every rank, so every
-rank reaches the same collectives), one serves single prompts (its own cross-prompt cache). A worker
-whose connection drops is marked dead: its running prompt is reported failed, SPMD stops being used.
+Ranks keep one executor for single prompts (its own cross-prompt cache) and one per SPMD rank prefix
+[0, k) (k = the powers of two below N, and N): a prefix's executor only sees that prefix's prompts, so
+its caches stay identical on its members and they all reach the same collectives. A batch b < N runs
+SPMD on the largest prefix <= b while the other ranks keep serving single prompts; an SPMD prompt waits
+only for its own ranks.
+
+Elastic: a worker whose connection drops is marked dead -- its single prompt re-runs on a survivor, an
+SPMD prompt it was part of re-runs on the prefix below it (shards re-queued to the surviving GPUs,
+SURVEY §5.3) -- and a replacement process is started. Once it has connected and no rank is busy, every
+rank leaves the broken process group and rendezvouses again (``Comm.reinit``, generation + 1), and the
+node is whole. Nothing re-execs a process that touched the GPU.
 """
 from __future__ import annotations
 
@@ -113,10 +121,12 @@ def prompt_batch(prompt: dict) -> int:
     return best
 
 
-def choose_mode(prompt: dict, extra_data: dict | None, world: int, latency_default: bool = False) -> str:
-    """``spmd`` when the batch covers every live rank and the prompt samples; ``latency`` for a smaller
-    batch when the server runs with ``--latency-mode`` (one image sooner instead of more images per
-    second); else ``single``. ``extra_data["dp"]`` (``"spmd"`` / ``"latency"`` / ``"single"``) overrides."""
+def choose_mode(prompt: dict, extra_data: dict | None, world: int, latency_default: bool = False,
+                subsets: bool = False) -> str:
+    """``spmd`` when the batch covers every live rank (``subsets``: at least two ranks -- the coordinator
+    then runs it on a rank prefix) and the prompt samples; ``latency`` for a smaller batch when the server
+    runs with ``--latency-mode`` (one image sooner instead of more images per second); else ``single``.
+    ``extra_data["dp"]`` (``"spmd"`` / ``"latency"`` / ``"single"``) overrides."""
     want = (extra_data or {}).get("dp", "auto")
     if world <= 1:
         return "single"
@@ -125,9 +135,12 @@ def choose_mode(prompt: dict, extra_data: dict | None, world: int, latency_defau
     has_sampler = any(isinstance(n, dict) and n.get("class_type") in SAMPLER_TYPES for n in prompt.values())
     if not has_sampler:
         return "single"
-    if prompt_batch(prompt) >= world:
+    b = prompt_batch(prompt)
+    if b >= world:
         return "spmd"
-    return "latency" if latency_default else "single"
+    if latency_default:
+        return "latency"
+    return "spmd" if subsets and b >= 2 else "single"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -170,8 +183,21 @@ def _forward_progress(server):
     progress.set_progress_bar_global_hook(hook)
 
 
-def worker_main(comm, address, authkey: bytes):
-    """Rank >= 1: execute what rank 0 sends until it says stop."""
+def _spmd_sizes(world: int):
+    """Rank prefixes that get their own SPMD groups: the powers of two below the node size, and the node.
+    A batch b < world runs on the largest prefix <= b (SPMD over a subset) and leaves the other ranks to
+    single prompts; each prefix keeps its own executor (identical caches on its members), so few sizes
+    keep few cached model copies."""
+    out, k = [], 2
+    while k < world:
+        out.append(k)
+        k *= 2
+    return out + ([world] if world > 1 else [])
+
+
+def worker_main(comm, address, authkey: bytes, respawned: bool = False):
+    """Rank >= 1: execute what rank 0 sends until it says stop. A respawned rank (replacing one that died)
+    connects first and joins the process group at the coordinator's next re-rendezvous (``regroup``)."""
     from ..graph.executor import PromptExecutor
     from ..runtime import device as dm
     from ..utils import imageio
@@ -186,12 +212,21 @@ def worker_main(comm, address, authkey: bytes):
     if conn is None:
         raise RuntimeError(f"rank {comm.rank}: cannot reach the coordinator at {address}")
     lock = threading.Lock()
-    send_msg(conn, {"op": "hello", "rank": comm.rank}, lock)
+    send_msg(conn, {"op": "hello", "rank": comm.rank, "respawned": respawned}, lock)
     server = RemoteServer(conn, lock)
     _forward_progress(server)
-    ctx = spmd.SPMD(comm)
+    ctxs: dict = {}                  # k -> SPMD context of the rank prefix [0, k)
+    ex_spmd: dict = {}               # k -> executor that only sees that prefix's SPMD prompts
+
+    def build():
+        comm.build_subsets(_spmd_sizes(comm.world))
+        ctxs.clear()
+        ex_spmd.clear()
+        for k, c in sorted(comm.subsets.items()):
+            ctxs[k] = spmd.SPMD(c)   # collective for the whole node (latency-mode groups)
+    if not respawned:
+        build()
     ex_single = PromptExecutor(server)
-    ex_spmd = PromptExecutor(None, node_hook=ctx)
     inbox: queue.Queue = queue.Queue()
 
     def reader():
@@ -215,12 +250,23 @@ def worker_main(comm, address, authkey: bytes):
         op = m.get("op")
         if op == "stop":
             break
+        if op == "regroup":           # re-rendezvous after a rank death (generation m["gen"])
+            ok, err = True, ""
+            try:
+                comm.reinit(int(m["port"]), int(m["gen"]), timeout_s=float(m.get("timeout", 120.0)))
+                build()
+            except Exception as ex:    # noqa: BLE001 - reported; the coordinator keeps the node degraded
+                logging.exception("rank %d: regroup failed", comm.rank)
+                ok, err = False, str(ex)
+            send_msg(conn, {"op": "regrouped", "rank": comm.rank, "gen": int(m["gen"]), "ok": ok, "error": err}, lock)
+            continue
         if op == "free":              # POST /free forwarded by rank 0 (same order as the prompts)
             if m.get("unload_models") or m.get("free_memory"):
                 dm.unload_all_models()
             if m.get("free_memory"):
                 ex_single.reset()
-                ex_spmd.reset()
+                for ex in ex_spmd.values():
+                    ex.reset()
             need_gc, last_gc = True, 0.0
         if op != "run":
             if need_gc and time.perf_counter() - last_gc > GC_INTERVAL_S:
@@ -230,11 +276,16 @@ def worker_main(comm, address, authkey: bytes):
         pid, extra = m["prompt_id"], m.get("extra_data") or {}
         server.last_prompt_id = pid
         t0 = time.perf_counter()
-        n0, b0 = ctx.images_sampled, comm.bytes_moved
-        if m["mode"] in ("spmd", "latency"):
+        k = int(m.get("k") or comm.world)
+        ctx = ctxs.get(k)
+        n0, b0, l0 = (ctx.images_sampled, ctx.comm.bytes_moved, ctx.loads_received) if ctx else (0, 0, 0)
+        if m["mode"] in ("spmd", "latency") and ctx is not None:
+            ex = ex_spmd.get(k)
+            if ex is None:
+                ex = ex_spmd[k] = PromptExecutor(None, node_hook=ctx)
             with spmd.activate(ctx, m["mode"]):
-                ex_spmd.execute(m["prompt"], pid, {}, m["outputs"])
-            ex = ex_spmd
+                ex.execute(m["prompt"], pid, {kk: v for kk, v in extra.items() if kk == "extra_pnginfo"},
+                           m["outputs"])
         else:
             ex_single.execute(m["prompt"], pid, extra, m["outputs"])
             ex = ex_single
@@ -245,8 +296,10 @@ def worker_main(comm, address, authkey: bytes):
                                      if save_errs else [])
         send_msg(conn, {"op": "done", "prompt_id": pid, "mode": m["mode"], "rank": comm.rank, "success": ok,
                         "messages": msgs, "outputs_ui": ex.outputs_ui,
-                        "seconds": time.perf_counter() - t0, "images_sampled": ctx.images_sampled - n0,
-                        "comm_bytes": comm.bytes_moved - b0}, lock)
+                        "seconds": time.perf_counter() - t0,
+                        "images_sampled": (ctx.images_sampled - n0) if ctx else 0,
+                        "comm_bytes": (ctx.comm.bytes_moved - b0) if ctx else 0,
+                        "loads_received": (ctx.loads_received - l0) if ctx else 0}, lock)
     try:
         conn.close()
     except OSError:
@@ -256,13 +309,25 @@ def worker_main(comm, address, authkey: bytes):
 # ------------------------------------------------------------------------------------------------
 # rank 0
 # ------------------------------------------------------------------------------------------------
+MAX_RESPAWNS = 3              # per rank: a rank that keeps dying stays dead
+SPMD_WAIT_LOG_S = 30.0        # an SPMD prompt waiting this long for its ranks to go idle is logged
+REGROUP_TIMEOUT_S = 120.0
+
+
 class Coordinator:
-    def __init__(self, q, server, comm, listener, accept_timeout_s: float = 600.0, latency_default=False):
+    """Rank 0's scheduler for the node. Elastic: a worker that dies is respawned as a fresh child process
+    (never a re-exec of a process that touched the GPU) and, once every rank is idle, all ranks leave the
+    broken process group and rendezvous again (``Comm.reinit``, generation + 1); meanwhile SPMD prompts
+    run on the rank prefix below the dead rank and single prompts on any survivor."""
+
+    def __init__(self, q, server, comm, listener, accept_timeout_s: float = 600.0, latency_default=False,
+                 respawn: bool = True):
         from ..graph.executor import PromptExecutor
-        from . import spmd
         self.q, self.server, self.comm = q, server, comm
         self.world = comm.world
         self.latency_default = latency_default
+        self.respawn = respawn and os.environ.get("CGS_RESPAWN", "1") != "0"
+        self.listener = listener
         self.conns: dict = {}
         self.locks: dict = {}
         self.dead: set = set()
@@ -273,42 +338,79 @@ class Coordinator:
         self._inflight: dict = {}     # rank -> (queue item id, prompt id, prompt, extra, outputs): its single prompt
         self._sids: dict = {}         # prompt id -> submitting client (WS)
         self._retries: dict = {}      # prompt id -> re-runs after a rank death
+        self._respawns: dict = {}     # rank -> respawns so far
+        self._spawned: dict = {}      # rank -> replacement process not yet in the process group
+        self._regroup_acks: dict = {}
+        self.procs: list = []         # replacement processes (the launcher owns the first ones)
+        self.gen = 0
+        self.regroups = 0
         self._last_gc, self._need_gc = time.perf_counter(), False
-
-        def accept_all():
-            while len(self.conns) < self.world - 1:
-                conn = listener.accept()
-                hello = recv_msg(conn)
-                r = int(hello["rank"])
-                self.conns[r], self.locks[r] = conn, threading.Lock()
-        t = threading.Thread(target=accept_all, daemon=True)
-        t.start()
-        t.join(accept_timeout_s)
+        self._accepted = threading.Condition()
+        threading.Thread(target=self._accept_loop, daemon=True).start()
+        with self._accepted:
+            deadline = time.time() + accept_timeout_s
+            while len(self.conns) < self.world - 1 and time.time() < deadline:
+                self._accepted.wait(timeout=1.0)
         if len(self.conns) < self.world - 1:
             raise RuntimeError(f"only {len(self.conns)} of {self.world - 1} worker ranks connected")
-        # after the handshakes: building the SPMD context is collective (latency-mode process groups)
-        self.ctx = spmd.SPMD(comm)
         self.ex_single = PromptExecutor(server)
-        self.ex_spmd = PromptExecutor(server, node_hook=self.ctx)
-        for r, conn in self.conns.items():
-            threading.Thread(target=self._reader, args=(r, conn), daemon=True).start()
+        self._build_contexts()        # after the handshakes: collective (subset + latency-mode groups)
         if hasattr(server, "interrupt_hooks"):
             server.interrupt_hooks.append(self.interrupt_all)
 
+    def _build_contexts(self):
+        from ..graph.executor import PromptExecutor
+        from . import spmd
+        self.comm.build_subsets(_spmd_sizes(self.world))
+        self.ctxs = {k: spmd.SPMD(c) for k, c in sorted(self.comm.subsets.items())}
+        self.ex_spmds = {k: PromptExecutor(self.server, node_hook=c) for k, c in self.ctxs.items()}
+        self.ctx = self.ctxs.get(self.world)
+        self.ex_spmd = self.ex_spmds.get(self.world)
+
     # -------------------------------------------------------------- plumbing
+    def _accept_loop(self):
+        """Worker connections, at start-up and whenever a replacement rank comes up."""
+        while True:
+            try:
+                conn = self.listener.accept()
+                hello = recv_msg(conn)
+            except (OSError, EOFError):
+                return
+            except Exception:       # noqa: BLE001 - a bad handshake must not stop the accept loop
+                logging.exception("worker handshake failed")
+                continue
+            r = int(hello["rank"])
+            with self._accepted:
+                self.conns[r], self.locks[r] = conn, threading.Lock()
+                self._accepted.notify_all()
+            threading.Thread(target=self._reader, args=(r, conn), daemon=True).start()
+            if hello.get("respawned"):
+                logging.warning("replacement for rank %d connected", r)
+                with self.cv:
+                    self.cv.notify_all()
+
     def live(self):
         return [r for r in range(self.world) if r not in self.dead]
+
+    def prefix(self):
+        """Ranks [0, L) that are all alive (the usable SPMD prefixes are the subsets of size <= L)."""
+        return min(self.dead) if self.dead else self.world
 
     def _reader(self, r, conn):
         while True:
             try:
                 m = recv_msg(conn)
             except (EOFError, OSError):
-                self._rank_died(r)
+                if self.conns.get(r) is conn:
+                    self._rank_died(r)
                 return
             op = m.get("op")
             if op == "event":
                 self.server.send_sync(m["event"], m["data"], m.get("sid"))
+            elif op == "regrouped":
+                with self.cv:
+                    self._regroup_acks[r] = m
+                    self.cv.notify_all()
             elif op == "done":
                 with self.cv:
                     pid = m["prompt_id"]
@@ -323,12 +425,16 @@ class Coordinator:
                     self.cv.notify_all()
 
     def _rank_died(self, r):
-        """A worker's connection dropped: mark it dead (no SPMD from now on: the process group lost a
-        member), re-run its single prompt on a survivor (once), unblock a waiting SPMD prompt."""
+        """A worker's connection dropped: mark it dead (SPMD prompts use the rank prefix below it until the
+        next re-rendezvous), re-run its single prompt on a survivor (once), unblock a waiting SPMD prompt,
+        and start a replacement process."""
         logging.error("rank %d left the cluster", r)
         retry = None
         with self.cv:
+            if r in self.dead:
+                return
             self.dead.add(r)
+            self.conns.pop(r, None)       # a replacement says hello on a fresh connection
             try:    # SPMD agreements waiting on the dead rank fail within ~1 s (spmd.SPMD._agree)
                 st = self.comm.store()
                 if st is not None:
@@ -347,9 +453,69 @@ class Coordinator:
             for w in self.spmd_waiting.values():
                 w.setdefault(r, {"success": False, "messages": [], "outputs_ui": {}, "dead": True})
             self.cv.notify_all()
+        self._spawn_replacement(r)
         if retry is not None:
             logging.warning("re-running prompt %s (rank %d died under it)", retry[1], r)
             threading.Thread(target=self._run_single, args=retry, daemon=True).start()
+
+    def _spawn_replacement(self, r):
+        if not self.respawn or _LAUNCH.get("argv") is None:
+            return
+        n = self._respawns.get(r, 0)
+        if n >= MAX_RESPAWNS:
+            logging.error("rank %d died %d times: not respawned", r, n)
+            return
+        self._respawns[r] = n + 1
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), CGS_SCHED_ROLE="worker", CGS_SCHED_RESPAWN="1",
+                   PYTHONPATH=_LAUNCH["pypath"])
+        env.pop("CGS_FAULT", None)    # injected faults fire once, not in the replacement
+        try:
+            p = subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main"] + list(_LAUNCH["argv"]), env=env)
+        except OSError:
+            logging.exception("respawning rank %d failed", r)
+            return
+        self.procs.append(p)
+        self._spawned[r] = p
+        logging.warning("respawned rank %d (pid %d)", r, p.pid)
+
+    def _maybe_regroup(self):
+        """Every dead rank has a connected replacement and no rank is busy: all ranks leave the broken
+        process group and rendezvous again as generation gen + 1 (rank 0 hosts the new TCPStore)."""
+        with self.cv:
+            if not self.dead or self.busy:
+                return
+            if any(r not in self._spawned or self._spawned[r].poll() is not None or r not in self.conns
+                   for r in self.dead):
+                return                    # every replacement is up and has said hello
+            gen, port = self.gen + 1, _free_port()
+            self._regroup_acks = {}
+        logging.warning("re-rendezvous of %d ranks (generation %d)", self.world, gen)
+        for r in range(1, self.world):
+            try:
+                send_msg(self.conns[r], {"op": "regroup", "gen": gen, "port": port, "timeout": REGROUP_TIMEOUT_S},
+                         self.locks[r])
+            except OSError:
+                logging.error("regroup: rank %d unreachable", r)
+                return
+        try:
+            self.comm.reinit(port, gen, timeout_s=REGROUP_TIMEOUT_S)
+            self._build_contexts()
+        except Exception:   # noqa: BLE001
+            logging.exception("regroup failed on rank 0; the node stays degraded")
+            return
+        deadline = time.time() + REGROUP_TIMEOUT_S
+        self._wait(lambda: len(self._regroup_acks) >= self.world - 1 or time.time() > deadline)
+        with self.cv:
+            bad = [r for r in range(1, self.world) if not self._regroup_acks.get(r, {}).get("ok")]
+            if bad:
+                logging.error("regroup: ranks %s did not rejoin", bad)
+                return
+            self.gen = gen
+            self.regroups += 1
+            self.dead.clear()
+            self._spawned.clear()
+            self.cv.notify_all()
+        logging.warning("node whole again (generation %d, %d ranks)", gen, self.world)
 
     def interrupt_all(self):
         for r in list(self.busy):
@@ -386,6 +552,19 @@ class Coordinator:
         self._complete(item_id, pid, m.get("outputs_ui") or {}, bool(m.get("success")), m.get("messages") or [])
 
     # -------------------------------------------------------------- scheduling
+    def spmd_size(self, prompt, extra):
+        """(mode, k): the execution mode of a prompt and the rank prefix [0, k) it runs on."""
+        mode = choose_mode(prompt, extra, self.world, self.latency_default, subsets=True)
+        L = self.prefix()
+        if mode == "latency":
+            return ("latency", self.world) if L == self.world else ("single", 1)
+        if mode != "spmd":
+            return "single", 1
+        want = (extra or {}).get("dp", "auto")
+        b = self.world if want == "spmd" else prompt_batch(prompt)
+        ks = [k for k in self.ctxs if k <= min(b, L)]
+        return ("spmd", max(ks)) if ks else ("single", 1)
+
     def run_forever(self, stop_event: threading.Event | None = None):
         while stop_event is None or not stop_event.is_set():
             got = self.q.get(timeout=1.0)
@@ -395,11 +574,12 @@ class Coordinator:
                 sid = extra.get("client_id")
                 if sid is not None:
                     self._sids[prompt_id] = sid
-                mode = choose_mode(prompt, extra, len(self.live()), self.latency_default)
-                if mode in ("spmd", "latency") and len(self.live()) == self.world:
-                    self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode)
+                mode, k = self.spmd_size(prompt, extra)
+                if mode in ("spmd", "latency"):
+                    self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode, k)
                 else:
                     self._run_single(item_id, prompt_id, prompt, extra, outputs)
+            self._maybe_regroup()
             self._housekeeping()
 
     def _housekeeping(self):
@@ -415,7 +595,8 @@ class Coordinator:
             dm.unload_all_models()
             if free_memory:
                 self.ex_single.reset()
-                self.ex_spmd.reset()
+                for ex in self.ex_spmds.values():
+                    ex.reset()
             for r in self.live():
                 if r != 0:
                     try:
@@ -472,35 +653,59 @@ class Coordinator:
                 self._finish_single(0, msg)
                 self.cv.notify_all()
 
-    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd"):
+    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd", k=None):
         from ..utils import imageio
         from . import spmd
-        self._wait(lambda: not self.busy)
+        k = k or self.world
+        members = list(range(k))
+        t_wait = time.perf_counter()
+        logged = [False]
+
+        def members_idle():
+            if not logged[0] and time.perf_counter() - t_wait > SPMD_WAIT_LOG_S:
+                logged[0] = True
+                logging.warning("SPMD prompt %s has waited %.0f s for ranks %s (busy: %s)", prompt_id,
+                                time.perf_counter() - t_wait, members, dict(self.busy))
+            return all(r not in self.busy for r in members) or any(r in self.dead for r in members)
+        self._wait(members_idle)
+        if any(r in self.dead for r in members):     # a member died while we waited: choose again
+            mode, k = self.spmd_size(prompt, extra)
+            if mode == "single":
+                return self._run_single(item_id, prompt_id, prompt, extra, outputs)
+            return self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode, k)
+        ctx, ex_spmd = self.ctxs[k], self.ex_spmds[k]
         with self.cv:
-            for r in self.live():
+            for r in members:
                 self.busy[r] = prompt_id
             self.spmd_waiting[prompt_id] = {}
-            self.ran_on[prompt_id] = "all" if mode == "spmd" else "latency"
-        msg = {"op": "run", "mode": mode, "prompt_id": prompt_id, "prompt": prompt, "outputs": outputs}
-        for r in self.live():
-            if r != 0:
+            self.ran_on[prompt_id] = ("all" if k == self.world else members) if mode == "spmd" else "latency"
+        # the workers' SPMD executors get the PNG metadata (SaveImage's hidden EXTRA_PNGINFO: every rank
+        # writes its own images), not the client id (their WS events are rank 0's to send)
+        xd = {"extra_pnginfo": extra.get("extra_pnginfo")} if extra.get("extra_pnginfo") is not None else {}
+        msg = {"op": "run", "mode": mode, "k": k, "prompt_id": prompt_id, "prompt": prompt, "outputs": outputs,
+               "extra_data": xd}
+        for r in members[1:]:
+            try:
                 send_msg(self.conns[r], msg, self.locks[r])
+            except OSError:
+                self._rank_died(r)
         self.server.last_prompt_id = prompt_id
-        n0, b0 = self.ctx.images_sampled, self.comm.bytes_moved
-        with spmd.activate(self.ctx, mode):
-            self.ex_spmd.execute(prompt, prompt_id, extra, outputs)
+        n0, b0, l0 = ctx.images_sampled, ctx.comm.bytes_moved, ctx.loads_received
+        ctx.reserved = []
+        with spmd.activate(ctx, mode):
+            ex_spmd.execute(prompt, prompt_id, extra, outputs)
         save_errs = imageio.wait_futures(imageio.take_pending())
-        mine, mine_b = self.ctx.images_sampled - n0, self.comm.bytes_moved - b0
-        # every live worker's report (a survivor of a rank death fails its next agreement within ~1 s);
+        mine, mine_b = ctx.images_sampled - n0, ctx.comm.bytes_moved - b0
+        # every member's report (a survivor of a rank death fails its next agreement within ~1 s);
         # bounded, so a wedged worker cannot hold the node
         t_end = time.perf_counter() + SPMD_REPORT_TIMEOUT_S
-        self._wait(lambda: all(r in self.spmd_waiting[prompt_id] for r in self.live() if r != 0)
+        self._wait(lambda: all(r in self.spmd_waiting[prompt_id] for r in members[1:])
                    or time.perf_counter() > t_end)
         retry = False
         with self.cv:
             done = self.spmd_waiting.pop(prompt_id)
-            ok = self.ex_spmd.success and not save_errs and all(bool(m.get("success")) for m in done.values())
-            msgs = list(self.ex_spmd.status_messages)
+            ok = ex_spmd.success and not save_errs and all(bool(m.get("success")) for m in done.values())
+            msgs = list(ex_spmd.status_messages)
             if save_errs:
                 msgs.append(("execution_error", {"prompt_id": prompt_id, "exception_message": "; ".join(save_errs)}))
             for r, m in sorted(done.items()):
@@ -510,25 +715,38 @@ class Coordinator:
                 if self.busy[r] == prompt_id:
                     del self.busy[r]
             self._need_gc = True
-            # a rank died under the prompt: run it again whole on a survivor (noise is keyed by global
-            # image index, so the images are the ones the split run would have produced)
-            lost = any(m.get("dead") for m in done.values()) or len(self.live()) < self.world
+            # a member died under the prompt: run it again on the survivors (SPMD on the rank prefix below
+            # the dead rank, else whole on one rank). Noise is keyed by global image index, so the images are
+            # the ones the first attempt would have produced.
+            lost = any(m.get("dead") for m in done.values()) or any(r in self.dead for r in members)
+            if not ok:
+                # once every member has reported (or is gone) no rank writes this attempt's files any more
+                from ..utils import imageio as _io
+                _io.flush()
+                ctx.cleanup_reserved()
             if not ok and lost and self.live() and self._retries.get(prompt_id, 0) < MAX_RETRIES:
                 self._retries[prompt_id] = self._retries.get(prompt_id, 0) + 1
                 retry = True
             else:
-                self._complete(item_id, prompt_id, self.ex_spmd.outputs_ui, ok, msgs)
+                self._complete(item_id, prompt_id, ex_spmd.outputs_ui, ok, msgs)
             with self.q.mutex:
                 h = self.q.history.get(prompt_id)
-                if h is not None:   # images sampled per rank (the batch split)
+                if h is not None:   # images sampled per rank (the batch split), checkpoints received (R3)
                     h["metrics"]["images_per_rank"] = {0: mine, **{r: m.get("images_sampled", 0)
                                                                    for r, m in done.items()}}
                     h["metrics"]["comm_bytes_per_rank"] = {0: mine_b, **{r: m.get("comm_bytes", 0)
                                                                          for r, m in done.items()}}
+                    h["metrics"]["loads_received_per_rank"] = {0: ctx.loads_received - l0,
+                                                               **{r: m.get("loads_received", 0)
+                                                                  for r, m in done.items()}}
             self.cv.notify_all()
         if retry:
-            logging.warning("re-running prompt %s on a surviving rank", prompt_id)
-            self._run_single(item_id, prompt_id, prompt, extra, outputs)
+            mode2, k2 = self.spmd_size(prompt, extra)
+            logging.warning("re-running prompt %s on surviving ranks (%s, k=%d)", prompt_id, mode2, k2)
+            if mode2 in ("spmd", "latency"):
+                self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode2, k2)
+            else:
+                self._run_single(item_id, prompt_id, prompt, extra, outputs)
 
     def shutdown(self):
         for r, conn in self.conns.items():
@@ -547,6 +765,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
+_LAUNCH: dict = {}     # argv / PYTHONPATH of the worker command line (replacement ranks use it)
+
+
 def launch(n: int, argv):
     """Rank 0 (this process, before it touches the GPU): start ranks 1..n-1 as children running the
     same command line, set up the rendezvous env for all of them, and return (listener, procs)."""
@@ -561,6 +782,7 @@ def launch(n: int, argv):
     procs = []
     pkg_parent = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     pypath = os.pathsep.join(p for p in (pkg_parent, os.environ.get("PYTHONPATH", "")) if p)
+    _LAUNCH.update(argv=list(argv), pypath=pypath)
     for r in range(1, n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), CGS_SCHED_ROLE="worker", PYTHONPATH=pypath)
         procs.append(subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main"] + list(argv), env=env))

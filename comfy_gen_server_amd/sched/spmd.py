@@ -62,9 +62,43 @@ class SPMD:
         # UNet call is split CFG-/token-parallel over the ranks (parallel/latency.py)
         self.mode = "spmd"
         self.latency = None
-        if comm.world > 1 and comm.enabled:
+        self.loads_received = 0       # checkpoints this rank got over the data plane instead of the disk
+        self.reserved: list = []      # rank 0: PNG names reserved by the current prompt's sharded saves
+        from ..parallel.comm import SubComm
+        if comm.world > 1 and comm.enabled and not isinstance(comm, SubComm):
             from ..parallel.latency import LatencyParallel
             self.latency = LatencyParallel(comm)    # collective: every rank builds its SPMD context once
+
+    def load_state_dict(self, path, device, return_metadata, load_local):
+        """R3 inside an SPMD prompt: rank 0 reads the checkpoint, every other rank of the prompt receives
+        it (``Comm.broadcast_state_dict``) -- one disk read per node. A failed read fails every rank."""
+        comm = self.comm
+        if self.rank == 0:
+            try:
+                res = load_local()
+            except Exception as ex:   # noqa: BLE001 - re-raised on every rank by the broadcast
+                comm.broadcast_state_dict(ex, device)
+                raise
+            sd, meta = res if return_metadata else (res, None)
+            comm.broadcast_state_dict(sd, device)
+            if return_metadata:
+                comm.broadcast_object(meta)
+        else:
+            sd = comm.broadcast_state_dict(None, device)
+            meta = comm.broadcast_object(None) if return_metadata else None
+            self.loads_received += 1
+        return (sd, meta) if return_metadata else sd
+
+    def cleanup_reserved(self):
+        """After a failed (or re-run) prompt: remove the reserved placeholder files no rank wrote (still
+        empty; a written PNG is renamed into place whole), so failures leave no zero-byte images."""
+        for path in self.reserved:
+            try:
+                if os.path.getsize(path) == 0:
+                    os.remove(path)
+            except OSError:
+                pass
+        self.reserved = []
 
     def shard(self, total: int):
         """(offset, count) of this rank's images of a batch of ``total`` (even split, remainder first)."""
@@ -118,7 +152,7 @@ class SPMD:
         if st is None or self.world <= 1:
             return code
         self._seq += 1
-        base = f"cgs/agree/{self._seq}"
+        base = f"cgs/agree/g{self.comm.gen}/k{self.world}/{self._seq}"
         st.set(f"{base}/{self.rank}", repr(float(code)))
         keys = [f"{base}/{r}" for r in range(self.world)]
         while True:
@@ -126,13 +160,15 @@ class SPMD:
                 st.wait(keys, datetime.timedelta(seconds=1.0))
                 break
             except Exception:   # timed out: still waiting for a peer -- or the peer is gone
-                if st.check(["cgs/dead"]) and st.get("cgs/dead"):
-                    self._stage = 2
-                    raise PeerNodeError("a rank of the SPMD prompt died (%s)" % st.get("cgs/dead").decode())
+                if st.check(["cgs/dead"]):
+                    dead = [int(x) for x in st.get("cgs/dead").decode().split(",") if x]
+                    if any(r < self.world for r in dead):     # a member of THIS prompt's ranks
+                        self._stage = 2
+                        raise PeerNodeError("a rank of the SPMD prompt died (%s)" % dead)
         v = max(float(st.get(k).decode()) for k in keys)
         if self._seq > 2:       # every rank read seq - 2 before it wrote seq - 1: its key is dead
             try:
-                st.delete_key(f"cgs/agree/{self._seq - 2}/{self.rank}")
+                st.delete_key(f"cgs/agree/g{self.comm.gen}/k{self.world}/{self._seq - 2}/{self.rank}")
             except Exception:   # pragma: no cover - stores without delete
                 pass
         return v
@@ -207,8 +243,11 @@ class SPMD:
             folder, filename, counter, subfolder, _ = folder_paths.get_save_image_path(
                 prefix + getattr(obj, "prefix_append", ""), out_dir, images.shape[2], images.shape[1])
             names = reserve_png_names(folder, filename, counter, total)
+            self.reserved += [os.path.join(folder, nm) for nm in names]
             plan = (folder, subfolder, names, getattr(obj, "type", "output"))
         folder, subfolder, names, typ = self.comm.broadcast_object(plan)
+        from ..utils import telemetry
+        telemetry.maybe_fault("node", "SaveImageWrite")   # fault site: names reserved, this rank's not written
         metadata = None
         if not NH.args_disable_metadata():
             metadata = {}

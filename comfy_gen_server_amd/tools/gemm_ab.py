@@ -65,6 +65,8 @@ def main(argv):
             iters = int(argv[i + 1]); i += 2
         elif argv[i] == "--shapes":
             only = set(argv[i + 1].split(",")); i += 2
+        elif argv[i] == "--with-w45":
+            i += 1
         elif argv[i] == "--v6modes":
             v6modes = [int(v) for v in argv[i + 1].split(",")]; i += 2
         else:
@@ -73,9 +75,10 @@ def main(argv):
     assert lib is not None, _native.kernels_error()
     dev = torch.device("cuda", 0)
     stream = core._stream()
-    rows = ["| shape | M | N | K | epi | w4 TF/s | w4-160 TF/s | w5 TF/s | v6 TF/s | v7 TF/s | hipBLASLt TF/s "
-            "| best w4/w5 / best other | w4/w5 max rel err |",
-            "|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|"]
+    rows = ["| shape | M | N | K | epi | w6 TF/s | w6 non-persistent | v6 TF/s | v7 TF/s | hipBLASLt TF/s "
+            "| w6 / best other | w6 max rel err |",
+            "|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|"]
+    skip = set(a for a in ("w4", "w4_160", "w5") if "--with-w45" not in argv)
     torch.manual_seed(0)
     for name, M, N, K, epi in SHAPES:
         if only and name not in only:
@@ -132,6 +135,14 @@ def main(argv):
                 return e
             return f
         cands = {} if geglu else {"w4": w4}      # the w4 GEGLU form is refused (gemm_w4.hip STATUS)
+        if _native.has_kernel("cgs_gemm_bf16_w6") and lib.cgs_gemm_w6_ok(M, N, K, K, K, nout, ldr,
+                                                                          flags | (EPI_LN if ln else 0)):
+            cands["w6"] = lambda: lib.cgs_gemm_bf16_w6(a.data_ptr(), w_run.data_ptr(), out.data_ptr(), b_run.data_ptr(),
+                                                       rp, rsp, csp, M, N, K, K, K, nout, ldr,
+                                                       flags | (EPI_LN if ln else 0), 1.0, 0, 4, 0, stream)
+            cands["w6np"] = lambda: lib.cgs_gemm_bf16_w6(a.data_ptr(), w_run.data_ptr(), out.data_ptr(),
+                                                         b_run.data_ptr(), rp, rsp, csp, M, N, K, K, K, nout, ldr,
+                                                         flags | (EPI_LN if ln else 0), 1.0, 0, 4, 1 << 30, stream)
         if not geglu and not ln and K % 128 == 0 and _native.has_kernel("cgs_gemm_bf16_w5"):
             cands["w5"] = lambda: lib.cgs_gemm_bf16_w5(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), rp, M, N,
                                                        K, K, K, nout, ldr, flags, 1.0, stream)
@@ -152,6 +163,7 @@ def main(argv):
             if fm() == 0:
                 cands[f"v6m{m}"] = fm
         cands["lib"] = lambda: F.linear(a, w, b)
+        cands = {k: v for k, v in cands.items() if k not in skip}
         for vn, f in cands.items():
             if vn == "lib":
                 continue
@@ -166,13 +178,10 @@ def main(argv):
                 times[vn].append(_bench(f, iters))
         flops = 2.0 * M * N * K
         tf = {vn: flops / statistics.median(t) / 1e9 for vn, t in times.items()}
-        best_w4 = max([v for k, v in tf.items() if k.startswith(("w4", "w5"))] or [0.0])
-        other = max(v for k, v in tf.items() if not k.startswith(("w4", "w5")))
+        other = max(v for k, v in tf.items() if not k.startswith(("w4", "w5", "w6")))
         cell = lambda k: f"{tf[k]:.0f}" if k in tf else "-"  # noqa: E731
-        line = (f"| {name} | {M} | {N} | {K} | {epi or 'bias'} | {cell('w4')} | {cell('w4_160')} | {cell('w5')} | "
-                f"{cell('v6')} | "
-                f"{cell('v7')} | {cell('lib')} | {best_w4 / other:.3f} | "
-                f"{max([v for k, v in errs.items() if k.startswith(('w4', 'w5'))] or [0.0]):.2e} |")
+        line = (f"| {name} | {M} | {N} | {K} | {epi or 'bias'} | {cell('w6')} | {cell('w6np')} | {cell('v6')} | "
+                f"{cell('v7')} | {cell('lib')} | {tf.get('w6', 0.0) / other:.3f} | {errs.get('w6', float('nan')):.2e} |")
         rows.append(line)
         print(line, " errs:", {k: f"{v:.1e}" for k, v in errs.items()}, " TF/s:", {k: round(v) for k, v in tf.items()},
               flush=True)

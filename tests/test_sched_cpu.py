@@ -3,7 +3,9 @@
 
 * a batch-6 workflow runs SPMD (2 images per rank, noise keyed by global image index) and returns
   the same images as the same prompt served whole on one rank;
-* six independent batch-1 prompts are spread over all three ranks.
+* six independent batch-1 prompts are spread over all three ranks;
+* a batch-2 prompt on 3 ranks runs SPMD on the rank prefix [0, 2) while rank 2 stays free;
+* inside an SPMD prompt only rank 0 reads the checkpoint; the others receive it (R3 broadcast).
 """
 import json
 import os
@@ -100,8 +102,13 @@ def _stop(proc):
 
 @pytest.fixture(scope="module")
 def cluster(tmp_path_factory):
-    proc, url, base = _start(tmp_path_factory, 3)
-    yield url, base
+    trace = tmp_path_factory.mktemp("loads") / "reads.txt"
+    os.environ["CGS_TRACE_LOADS"] = str(trace)
+    try:
+        proc, url, base = _start(tmp_path_factory, 3)
+    finally:
+        os.environ.pop("CGS_TRACE_LOADS", None)
+    yield url, base, trace
     _stop(proc)
 
 
@@ -127,7 +134,7 @@ def _images(base, entry):
 
 
 def test_batch_prompt_split_over_ranks_matches_one_rank(cluster):
-    url, base = cluster
+    url, base, trace = cluster
     a = _post(url + "/prompt", {"prompt": _graph(11, 6, "spmd")})["prompt_id"]
     b = _post(url + "/prompt", {"prompt": _graph(11, 6, "one"), "extra_data": {"dp": "single"}})["prompt_id"]
     h = _wait(url, [a, b])
@@ -141,6 +148,11 @@ def test_batch_prompt_split_over_ranks_matches_one_rank(cluster):
     for r, nb in h[a]["metrics"]["comm_bytes_per_rank"].items():
         if r != "0":
             assert nb <= (1 / 3 + 0.05) * img_bytes, (r, nb)
+    # R3: one disk read of the checkpoint for the SPMD prompt (rank 0); ranks 1 and 2 received it over the
+    # data plane. The single-rank prompt read it once more on its own rank.
+    assert h[a]["metrics"]["loads_received_per_rank"] == {"0": 0, "1": 1, "2": 1}, h[a]["metrics"]
+    reads = [ln.split() for ln in open(trace).read().splitlines() if "tiny.safetensors" in ln]
+    assert len(reads) == 2 and reads[0][0] == "0", reads
     ia, ib = _images(base, h[a]), _images(base, h[b])
     assert len(ia) == len(ib) == 6
     for x, y in zip(ia, ib):
@@ -150,7 +162,7 @@ def test_batch_prompt_split_over_ranks_matches_one_rank(cluster):
 
 
 def test_independent_prompts_use_every_rank(cluster):
-    url, base = cluster
+    url, base, _ = cluster
     pids = [_post(url + "/prompt", {"prompt": _graph(100 + i, 1, f"ind{i}")})["prompt_id"] for i in range(6)]
     h = _wait(url, pids)
     assert all(e["status"]["status_str"] == "success" for e in h.values())
@@ -175,3 +187,30 @@ def test_latency_mode_batch_one_matches_one_rank(tmp_path_factory):
     x, y = _images(base, h[a])[0], _images(base, h[b])[0]
     d = np.abs(x - y)
     assert d.max() <= 2 and d.mean() < 0.25, (d.max(), d.mean())
+
+
+def test_small_batch_runs_spmd_on_a_rank_prefix(cluster):
+    """A batch of 2 on 3 ranks samples on ranks 0 and 1 (one image each); the result equals one rank."""
+    url, base, _ = cluster
+    a = _post(url + "/prompt", {"prompt": _graph(12, 2, "pre")})["prompt_id"]
+    b = _post(url + "/prompt", {"prompt": _graph(12, 2, "pre1"), "extra_data": {"dp": "single"}})["prompt_id"]
+    h = _wait(url, [a, b])
+    assert h[a]["status"]["status_str"] == "success", h[a]["status"]
+    assert h[a]["metrics"]["ranks"] == [0, 1], h[a]["metrics"]
+    assert h[a]["metrics"]["images_per_rank"] == {"0": 1, "1": 1}, h[a]["metrics"]
+    for x, y in zip(_images(base, h[a]), _images(base, h[b])):
+        d = np.abs(x - y)
+        assert d.max() <= 2 and d.mean() < 0.25, (d.max(), d.mean())
+
+
+def test_spmd_png_metadata_on_every_rank(cluster):
+    """SaveImage's workflow metadata (extra_pnginfo) is in every rank's PNGs, not only rank 0's."""
+    from PIL import Image
+    url, base, _ = cluster
+    a = _post(url + "/prompt", {"prompt": _graph(13, 6, "meta"),
+                                "extra_data": {"extra_pnginfo": {"workflow": {"nodes": [1, 2, 3]}}}})["prompt_id"]
+    h = _wait(url, [a])[a]
+    assert h["metrics"]["ranks"] == "all"
+    for im in h["outputs"]["9"]["images"]:
+        info = Image.open(os.path.join(base, "output", im["subfolder"], im["filename"])).info
+        assert json.loads(info["workflow"]) == {"nodes": [1, 2, 3]} and "prompt" in info, im
