@@ -32,6 +32,8 @@ from urllib.parse import quote
 import aiohttp
 from aiohttp import web
 
+VIEW_ALL_MAX_PAGE = 500      # /view_all page_size cap
+
 from ..graph import registry
 from ..graph.validation import validate_prompt
 from ..runtime import device as dm
@@ -186,34 +188,45 @@ class PromptServer:
                 return folder_paths.get_output_directory(), dir_type
             return folder_paths.get_input_directory(), "input"
 
+        def _within(root, path):
+            root = os.path.abspath(root)
+            return os.path.commonpath((root, os.path.abspath(path))) == root
+
         def image_upload(post, image_save_function=None):
+            """Contract of ``/upload/image`` (reference ``server.py:254-309``): the file lands in
+            ``{type dir}/{subfolder}/{name}`` -- renamed ``name (i).ext`` unless ``overwrite`` is true --
+            and the response names it. A path outside the type directory is 400. ``image_save_function``
+            (the mask upload) writes the file itself and returns None, or an error response -- then
+            nothing is written and that error is the answer (never a 200 for a file that does not exist)."""
             image = post.get("image")
             overwrite = post.get("overwrite")
             upload_dir, image_upload_type = get_dir_by_type(post.get("type"))
-            if image and image.file:
-                filename = image.filename
-                if not filename:
-                    return web.Response(status=400)
-                subfolder = post.get("subfolder", "")
-                full_output_folder = os.path.join(upload_dir, os.path.normpath(subfolder))
-                filepath = os.path.abspath(os.path.join(full_output_folder, filename))
-                if os.path.commonpath((os.path.abspath(upload_dir), filepath)) != os.path.abspath(upload_dir):
-                    return web.Response(status=400)
-                os.makedirs(full_output_folder, exist_ok=True)
-                split = os.path.splitext(filename)
-                if not (overwrite is not None and overwrite in ("true", "1")):
-                    i = 1
-                    while os.path.exists(filepath):
-                        filename = f"{split[0]} ({i}){split[1]}"
-                        filepath = os.path.join(full_output_folder, filename)
-                        i += 1
-                if image_save_function is not None:
-                    image_save_function(image, post, filepath)
-                else:
-                    with open(filepath, "wb") as f:
-                        f.write(image.file.read())
-                return web.json_response({"name": filename, "subfolder": subfolder, "type": image_upload_type})
-            return web.Response(status=400)
+            if not (image and getattr(image, "file", None)):
+                return web.Response(status=400)
+            filename = image.filename
+            if not filename or filename != os.path.basename(filename) or filename in (".", ".."):
+                return web.Response(status=400)
+            subfolder = post.get("subfolder", "") or ""
+            full_output_folder = os.path.abspath(os.path.join(upload_dir, os.path.normpath(subfolder)))
+            if not _within(upload_dir, full_output_folder):
+                return web.Response(status=400)
+            filepath = os.path.join(full_output_folder, filename)
+            if not (overwrite is not None and overwrite in ("true", "1")):
+                stem, ext = os.path.splitext(filename)
+                i = 1
+                while os.path.exists(filepath):
+                    filename = f"{stem} ({i}){ext}"
+                    filepath = os.path.join(full_output_folder, filename)
+                    i += 1
+            os.makedirs(full_output_folder, exist_ok=True)
+            if image_save_function is not None:
+                err = image_save_function(image, post, filepath)
+                if err is not None:
+                    return err
+            else:
+                with open(filepath, "wb") as f:
+                    f.write(image.file.read())
+            return web.json_response({"name": filename, "subfolder": subfolder, "type": image_upload_type})
 
         @routes.post("/upload/image")
         async def upload_image(request):
@@ -222,34 +235,44 @@ class PromptServer:
 
         @routes.post("/upload/mask")
         async def upload_mask(request):
+            """The uploaded image's alpha channel applied to ``original_ref`` (an existing image; its PNG
+            text chunks kept), saved as a new file. A malformed reference is 400, an escaping subfolder
+            403, a missing original 404 -- and in each case nothing is written."""
             post = await request.post()
 
             def image_save_function(image, post, filepath):
-                from PIL import Image, ImageOps
+                from PIL import Image
                 from PIL.PngImagePlugin import PngInfo
-                original_ref = json.loads(post.get("original_ref"))
-                filename, output_dir = folder_paths.annotated_filepath(original_ref["filename"])
-                if filename[0] == "/" or ".." in filename:
+                try:
+                    original_ref = json.loads(post.get("original_ref") or "")
+                    ref_name = original_ref["filename"]
+                except (ValueError, KeyError, TypeError):
+                    return web.Response(status=400)
+                if not isinstance(ref_name, str) or not ref_name:
+                    return web.Response(status=400)
+                filename, output_dir = folder_paths.annotated_filepath(ref_name)
+                if filename.startswith("/") or ".." in filename or filename != os.path.basename(filename):
                     return web.Response(status=400)
                 if output_dir is None:
                     output_dir = get_dir_by_type(original_ref.get("type", "output"))[0]
-                if "subfolder" in original_ref:
-                    full = os.path.join(output_dir, original_ref["subfolder"])
-                    if os.path.commonpath((os.path.abspath(full), output_dir)) != output_dir:
+                output_dir = os.path.abspath(output_dir)
+                if original_ref.get("subfolder"):
+                    full = os.path.abspath(os.path.join(output_dir, original_ref["subfolder"]))
+                    if not _within(output_dir, full):
                         return web.Response(status=403)
                     output_dir = full
                 file = os.path.join(output_dir, filename)
-                if os.path.isfile(file):
-                    with Image.open(file) as original_pil:
-                        metadata = PngInfo()
-                        if hasattr(original_pil, "text"):
-                            for key in original_pil.text:
-                                metadata.add_text(key, original_pil.text[key])
-                        original_pil = original_pil.convert("RGBA")
-                        mask_pil = Image.open(image.file).convert("RGBA")
-                        new_alpha = mask_pil.getchannel("A")
-                        original_pil.putalpha(new_alpha)
-                        original_pil.save(filepath, compress_level=4, pnginfo=metadata)
+                if not os.path.isfile(file):
+                    return web.Response(status=404)
+                with Image.open(file) as original_pil:
+                    metadata = PngInfo()
+                    for key, val in getattr(original_pil, "text", {}).items():
+                        metadata.add_text(key, val)
+                    original_pil = original_pil.convert("RGBA")
+                    mask_pil = Image.open(image.file).convert("RGBA")
+                    original_pil.putalpha(mask_pil.getchannel("A"))
+                    original_pil.save(filepath, compress_level=4, pnginfo=metadata)
+                return None
             return image_upload(post, image_save_function)
 
         @routes.get("/view")
@@ -317,8 +340,13 @@ class PromptServer:
 
         @routes.get("/view_all")
         async def view_all(request):
-            page = int(request.rel_url.query.get("page", 1))
-            page_size = int(request.rel_url.query.get("page_size", 50))
+            try:
+                page = int(request.rel_url.query.get("page", 1))
+                page_size = int(request.rel_url.query.get("page_size", 50))
+            except ValueError:
+                return web.json_response({"error": "page and page_size must be integers"}, status=400)
+            if page < 1 or not 1 <= page_size <= VIEW_ALL_MAX_PAGE:
+                return web.json_response({"error": f"page >= 1, 1 <= page_size <= {VIEW_ALL_MAX_PAGE}"}, status=400)
             out_dir = folder_paths.get_output_directory()
             files = []
             if os.path.isdir(out_dir):
