@@ -180,14 +180,9 @@ KERNEL_SIGNATURES = {
     "cgs_transpose_bf16": [_P, _P, _I, _I, _L, _L, _P],                # x, y, rows, cols, ldx, ldy
     "cgs_abort_stream_capture": [_P],
     "cgs_channel_affine2": [_P, _P, _P, _L, _P, _I, _I, _I, _F, _I, _P],
-    # "w4" GEMM (gemm_w4.hip, one wave per SIMD): A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, rs, cs
-    "cgs_gemm_bf16_w4": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _P, _I, _P],
-    "cgs_w4_set_group": [_I],
     # experiment: 4-slot-ring one-wave-per-SIMD GEMM (bias / residual epilogue only)
-    "cgs_gemm_bf16_w5": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
-    "cgs_gemm_bf16_w5_dbg": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _P],
-    "cgs_gemm_bf16_w6": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _I, _I, _P],
-    "cgs_gemm_w6_ok": [_I, _I, _I, _L, _L, _L, _L, _I],
+    "cgs_gemm_bf16_w6": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _I, _I, _I, _P],
+    "cgs_gemm_w6_ok": [_I, _I, _I, _L, _L, _L, _L, _I, _I],
     # skinny GEMM (M <= 128) with its split-K workspace
     "cgs_gemm_skinny_ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
     "cgs_gemm_skinny_ws_bytes": [_I, _I, _I],
@@ -201,7 +196,7 @@ KERNEL_SIGNATURES = {
 
 _RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
-            "cgs_attn_set_variant": None, "cgs_w4_set_group": None,
+            "cgs_attn_set_variant": None,
             "cgs_conv_v6_set_loader": None}
 
 

@@ -958,6 +958,16 @@ static int g_gemm_variant = -1;   // -1 auto, 1 = v1 only, 2 = v2, 3 = v3 (4 wav
 
 CGS_EXPORT void cgs_gemm_set_variant(int v) { g_gemm_variant = v; }
 
+// w6 (gemm_w6.hip): one-wave-per-SIMD 256x256x64 persistent kernel with full-line LDS-DMA; variant 16.
+// variant 17: its 256x160 form (128 x 80 wave tiles).
+CGS_EXPORT int cgs_gemm_w6_ok(int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
+                              int bn);
+CGS_EXPORT int cgs_gemm_bf16_w6(const void* A, const void* W, void* C, const void* bias, const void* R, const float* rs,
+                                const float* cs, int M, int N, int K, long long lda, long long ldw, long long ldc,
+                                long long ldr, int epi, float alpha, int dbg, int group_m, int grid_cap, int bn,
+                                hipStream_t stream);
+constexpr int kVariantW6 = 16, kVariantW6n160 = 17;
+
 static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                          int variant, hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
@@ -1001,6 +1011,12 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
         (long long)M * lda * 2 >= (1ll << 32) || (long long)N * ldw * 2 >= (1ll << 32))
       return (int)hipErrorInvalidValue;
     return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
+  }
+  if (variant == kVariantW6 || variant == kVariantW6n160) {
+    const int bn = variant == kVariantW6 ? 256 : 160;
+    if (!cgs_gemm_w6_ok(M, N, K, lda, ldw, ldc, ldr, epi, bn)) return (int)hipErrorInvalidValue;
+    return cgs_gemm_bf16_w6(A, W, C, bias, R, nullptr, nullptr, M, N, K, lda, ldw, ldc, ldr, epi, alpha, 0, 4, 0, bn,
+                            stream);
   }
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && (!(epi & EPI_GEGLU) || (N % 160 == 0 && !(epi & EPI_RESIDUAL))) &&
       ((uintptr_t)bias % 8 == 0))
@@ -1085,6 +1101,12 @@ static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, 
       return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
     return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream,
                           variant < 0 ? 8 : variant, rs, cs);
+  }
+  if (variant == kVariantW6 || variant == kVariantW6n160) {
+    const int bn = variant == kVariantW6 ? 256 : 160;
+    if (!cgs_gemm_w6_ok(M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, bn)) return (int)hipErrorInvalidValue;
+    return cgs_gemm_bf16_w6(A, W, C, bias, nullptr, rs, cs, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, 0, 4, 0,
+                            bn, stream);
   }
   // v6 (256x160) for the N = 640 / 1280 projections (the cross-attention query), v7 otherwise
   if (variant == 8 || (variant >= 10 && variant <= 14))

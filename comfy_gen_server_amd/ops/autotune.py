@@ -22,6 +22,7 @@ Env:
   CGS_TUNE_DEFAULT=0      do not load the packaged table
   CGS_TUNE_REPS=n         timed repetitions per candidate (default 3)
   CGS_TUNE_DUMP=path      at exit, write every choice made in this process with its per-candidate ms
+  CGS_TUNE_OVERRIDE=json  {key: choice} merged over the loaded tables (A/B runs of one kernel choice)
 """
 from __future__ import annotations
 
@@ -105,6 +106,24 @@ def _capturing() -> bool:
         return False
 
 
+_ov = ("", {})
+
+
+def _override(key):
+    """CGS_TUNE_OVERRIDE (re-read when the variable changes: ab_bench flips it between jobs)."""
+    global _ov
+    src = os.environ.get("CGS_TUNE_OVERRIDE", "")
+    if not src:
+        return None
+    if src != _ov[0]:
+        try:
+            txt = open(src[1:]).read() if src.startswith("@") else src     # "@file.json" or inline JSON
+            _ov = (src, {str(k): str(v) for k, v in json.loads(txt).items()})
+        except (OSError, ValueError):
+            _ov = (src, {})
+    return _ov[1].get(key)
+
+
 def choose(key_parts, candidates, default: str | None = None) -> str:
     """Return the name of the fastest candidate for this key.
 
@@ -116,6 +135,9 @@ def choose(key_parts, candidates, default: str | None = None) -> str:
     if not enabled():               # explicit opt-out: the default kernel, table entries included
         return default
     key = _key(key_parts)
+    ov = _override(key)
+    if ov is not None and ov in names:
+        return ov
     with _lock:
         _load()
         hit = _cache.get(key)

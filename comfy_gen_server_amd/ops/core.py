@@ -24,6 +24,7 @@ EPI_BIAS = 1
 EPI_RESIDUAL = 2
 EPI_GEGLU = 4
 EPI_SILU_IN = 8   # reserved
+EPI_LNFOLD = 8    # (C side: MC_EPI_LNFOLD; the LN-folded entry points add it themselves)
 EPI_GELU = 32     # GELU(acc + bias) before the residual (v6 ACT kernel, mc::tile family, skinny)
 
 # hipBLASLt (through ATen) as a GEMM autotune candidate: off unless explicitly requested -- the
@@ -173,6 +174,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
                     cands.append(("v5", lambda: run_hip(5)))
                 if K >= 128 or not gelu:
                     cands.append(("v6", lambda: run_hip(6)))
+            cands += _w6_cands(M, N, K, epi, run_hip)     # one wave per SIMD, full-line DMA, persistent
             if K % 32 == 0 and N % 8 == 0:
                 cands.append(("v4", lambda: run_hip(4)))
                 cands.append(("v8", lambda: run_hip(8)))      # 128 x 128 tiles (short M / N grids)
@@ -188,7 +190,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")     # explicit opt-in (CGS_GEMM_LIB=1)
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
+        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, "w6": W6, "w6n160": W6_160,
+                   **_SMALL_NAMES}.get(choice, -2)
         y = run_hip(variant, final=True).view(*x.shape[:-1], N)
         if rs_part:
             # (no version counter: inference-mode tensors have none; the consumers take the partials only
@@ -282,12 +285,14 @@ def linear_geglu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | Non
                     if N2 % 160 == 0:    # 256x160 tiles with the GEGLU epilogue (pq::run GG)
                         cands.append(("v6", lambda: run_hip(6)))
                 cands.append(("v5", lambda: run_hip(5)))
+            if _w6_ok(M, N2, K, epi):
+                cands.append(("w6", lambda: run_hip(W6)))
             cands.append(("v4", lambda: run_hip(4)))
             if _underfilled(M, N2):
                 cands += [("v8", lambda: run_hip(8))] + [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
             cands.append(("hip", lambda: run_hip(-1)))
             choice = autotune.choose(("gemm_geglu", M, N2, K, epi), cands, default="hip")
-        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, **_SMALL_NAMES}.get(choice, -2)
+        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, "w6": W6, **_SMALL_NAMES}.get(choice, -2)
         return run_hip(variant).view(*x.shape[:-1], N2 // 2)
     count("gemm_geglu", be)
     # reference path expects the *interleaved* weight too, undo it
@@ -1319,23 +1324,48 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
         return out
 
     variant = -1                  # v6 / v7 by shape
+    w6 = _w6_cands(M, N, K, epi | EPI_LNFOLD, run)
     if _underfilled(M, N) and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
         if N % 160 == 0:    # 256x160 tiles (plain or GEGLU): whole rounds where 256x256 leaves a partial one
             cands.append(("v6", lambda: run(6)))
-        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v7")
-        variant = {"v8": 8, "v6": 6, **_SMALL_NAMES}.get(choice, -1)
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands + w6, default="v7")
+        variant = {"v8": 8, "v6": 6, "w6": W6, "w6n160": W6_160, **_SMALL_NAMES}.get(choice, -1)
     elif geglu and N % 160 == 0 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
-        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), [("v7", lambda: run(7)), ("v6", lambda: run(6))],
-                                 default="v7")
-        variant = 6 if choice == "v6" else 7
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi),
+                                 [("v7", lambda: run(7)), ("v6", lambda: run(6))] + w6, default="v7")
+        variant = {"v6": 6, "w6": W6, "w6n160": W6_160}.get(choice, 7)
     elif not geglu and N % 160 == 0 and N > 1280 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         # wide non-GEGLU projections (fused QKV): 256x160 tiles give whole rounds where 256x256 leave
         # a partial last round (N = 1920 / 3840 at M = 65536 / 16384) -- measured per shape
-        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), [("v7", lambda: run(7)), ("v6", lambda: run(6))],
-                                 default="v7")
-        variant = 6 if choice == "v6" else 7
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi),
+                                 [("v7", lambda: run(7)), ("v6", lambda: run(6))] + w6, default="v7")
+        variant = {"v6": 6, "w6": W6, "w6n160": W6_160}.get(choice, 7)
+    elif w6 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
+        choice = autotune.choose(("gemm_lnfold", M, N, K, epi), [("v7", lambda: run(-1))] + w6, default="v7")
+        variant = {"w6": W6, "w6n160": W6_160}.get(choice, -1)
     return run(variant).view(*x.shape[:-1], nout)
+
+
+W6, W6_160 = 16, 17      # gemm_w6.hip (256 / 160-wide tiles) through cgs_gemm_bf16_v / _lnfold_v
+
+
+def _w6_ok(M, N, K, epi, bn=256) -> bool:
+    """The w6 kernel's shape / epilogue domain (``cgs_gemm_w6_ok``; contiguous operands: lda = ldw = K)."""
+    if M * N * K < (1 << 30) or not _native.has_kernel("cgs_gemm_w6_ok"):
+        return False
+    nout = N // 2 if epi & EPI_GEGLU else N
+    return bool(_lib().cgs_gemm_w6_ok(M, N, K, K, K, nout, nout if epi & EPI_RESIDUAL else 0, epi, bn))
+
+
+def _w6_cands(M, N, K, epi, run):
+    """("w6", ...) / ("w6n160", ...) autotune candidates where the shape is in their domain."""
+    out = []
+    if _w6_ok(M, N, K, epi):
+        out.append(("w6", lambda: run(W6)))
+    if N % 160 == 0 and _w6_ok(M, N, K, epi, 160):
+        out.append(("w6n160", lambda: run(W6_160)))
+    return out
 
 
 _CUS: list = []

@@ -1,5 +1,6 @@
-"""In-process interleaved A/B of the GEMM kernels on the SDXL shapes (one wave per SIMD "w4" vs the 8-wave
-v6 / v7 kernels vs hipBLASLt through ATen), with an fp32 numerics check of every HIP variant.
+"""In-process interleaved A/B of the GEMM kernels on the SDXL shapes (the one-wave-per-SIMD w6 -- persistent,
+non-persistent, 256x160 -- vs the 8-wave v6 / v7 kernels vs hipBLASLt through ATen), with an fp32 numerics
+check of every HIP variant.
 
 python -m comfy_gen_server_amd.tools.gemm_ab [out.md] [--rounds R] [--iters N] [--shapes a,b,...] [--v6modes 1,65]
 
@@ -65,8 +66,6 @@ def main(argv):
             iters = int(argv[i + 1]); i += 2
         elif argv[i] == "--shapes":
             only = set(argv[i + 1].split(",")); i += 2
-        elif argv[i] == "--with-w45":
-            i += 1
         elif argv[i] == "--v6modes":
             v6modes = [int(v) for v in argv[i + 1].split(",")]; i += 2
         else:
@@ -75,10 +74,9 @@ def main(argv):
     assert lib is not None, _native.kernels_error()
     dev = torch.device("cuda", 0)
     stream = core._stream()
-    rows = ["| shape | M | N | K | epi | w6 TF/s | w6 non-persistent | v6 TF/s | v7 TF/s | hipBLASLt TF/s "
-            "| w6 / best other | w6 max rel err |",
-            "|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|"]
-    skip = set(a for a in ("w4", "w4_160", "w5") if "--with-w45" not in argv)
+    rows = ["| shape | M | N | K | epi | w6 TF/s | w6 non-persistent | w6 256x160 | v6 TF/s | v7 TF/s | hipBLASLt TF/s "
+            "| best w6 / best other | w6 max rel err |",
+            "|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|"]
     torch.manual_seed(0)
     for name, M, N, K, epi in SHAPES:
         if only and name not in only:
@@ -116,14 +114,6 @@ def main(argv):
         csp = None if cs is None else cs.data_ptr()
         rsp = None if rs is None else rs.data_ptr()
 
-        def w4v(bn):
-            def f():
-                return lib.cgs_gemm_bf16_w4(a.data_ptr(), w_run.data_ptr(), out.data_ptr(), b_run.data_ptr(), rp, M,
-                                            N, K, K, K, nout, ldr, flags | (EPI_LN if ln else 0), 1.0, rsp, csp, bn,
-                                            stream)
-            return f
-        w4 = w4v(256)
-
         def var(v):
             def f():
                 if ln:
@@ -134,20 +124,20 @@ def main(argv):
                                             N, K, K, K, nout, ldr, flags, 1.0, v, stream)
                 return e
             return f
-        cands = {} if geglu else {"w4": w4}      # the w4 GEGLU form is refused (gemm_w4.hip STATUS)
+        cands = {}
         if _native.has_kernel("cgs_gemm_bf16_w6") and lib.cgs_gemm_w6_ok(M, N, K, K, K, nout, ldr,
-                                                                          flags | (EPI_LN if ln else 0)):
+                                                                          flags | (EPI_LN if ln else 0), 256):
             cands["w6"] = lambda: lib.cgs_gemm_bf16_w6(a.data_ptr(), w_run.data_ptr(), out.data_ptr(), b_run.data_ptr(),
                                                        rp, rsp, csp, M, N, K, K, K, nout, ldr,
-                                                       flags | (EPI_LN if ln else 0), 1.0, 0, 4, 0, stream)
+                                                       flags | (EPI_LN if ln else 0), 1.0, 0, 4, 0, 256, stream)
             cands["w6np"] = lambda: lib.cgs_gemm_bf16_w6(a.data_ptr(), w_run.data_ptr(), out.data_ptr(),
                                                          b_run.data_ptr(), rp, rsp, csp, M, N, K, K, K, nout, ldr,
-                                                         flags | (EPI_LN if ln else 0), 1.0, 0, 4, 1 << 30, stream)
-        if not geglu and not ln and K % 128 == 0 and _native.has_kernel("cgs_gemm_bf16_w5"):
-            cands["w5"] = lambda: lib.cgs_gemm_bf16_w5(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), rp, M, N,
-                                                       K, K, K, nout, ldr, flags, 1.0, stream)
-        if not geglu and N % 160 == 0:
-            cands["w4_160"] = w4v(160)
+                                                         flags | (EPI_LN if ln else 0), 1.0, 0, 4, 1 << 30, 256, stream)
+        if (_native.has_kernel("cgs_gemm_bf16_w6") and N % 160 == 0 and
+                lib.cgs_gemm_w6_ok(M, N, K, K, K, nout, ldr, flags | (EPI_LN if ln else 0), 160)):
+            cands["w6n160"] = lambda: lib.cgs_gemm_bf16_w6(a.data_ptr(), w_run.data_ptr(), out.data_ptr(),
+                                                           b_run.data_ptr(), rp, rsp, csp, M, N, K, K, K, nout, ldr,
+                                                           flags | (EPI_LN if ln else 0), 1.0, 0, 4, 0, 160, stream)
         errs = {}
         for vn, v in (("v6", 6), ("v7", 7)):
             f = var(v)
@@ -163,7 +153,6 @@ def main(argv):
             if fm() == 0:
                 cands[f"v6m{m}"] = fm
         cands["lib"] = lambda: F.linear(a, w, b)
-        cands = {k: v for k, v in cands.items() if k not in skip}
         for vn, f in cands.items():
             if vn == "lib":
                 continue
@@ -180,8 +169,10 @@ def main(argv):
         tf = {vn: flops / statistics.median(t) / 1e9 for vn, t in times.items()}
         other = max(v for k, v in tf.items() if not k.startswith(("w4", "w5", "w6")))
         cell = lambda k: f"{tf[k]:.0f}" if k in tf else "-"  # noqa: E731
-        line = (f"| {name} | {M} | {N} | {K} | {epi or 'bias'} | {cell('w6')} | {cell('w6np')} | {cell('v6')} | "
-                f"{cell('v7')} | {cell('lib')} | {tf.get('w6', 0.0) / other:.3f} | {errs.get('w6', float('nan')):.2e} |")
+        bw6 = max(tf.get("w6", 0.0), tf.get("w6n160", 0.0))
+        line = (f"| {name} | {M} | {N} | {K} | {epi or 'bias'} | {cell('w6')} | {cell('w6np')} | {cell('w6n160')} | "
+                f"{cell('v6')} | {cell('v7')} | {cell('lib')} | {bw6 / other:.3f} | "
+                f"{max(errs.get('w6', 0.0), errs.get('w6n160', 0.0)):.2e} |")
         rows.append(line)
         print(line, " errs:", {k: f"{v:.1e}" for k, v in errs.items()}, " TF/s:", {k: round(v) for k, v in tf.items()},
               flush=True)

@@ -17,7 +17,7 @@ def main(argv):
     kind = argv[0]
     if kind == "gemm":
         M, N, K = (int(v) for v in argv[1:4])
-        var = argv[4] if len(argv) > 4 else "-1"   # kernel variant number, "w4", "w5" or "lib" (hipBLASLt)
+        var = argv[4] if len(argv) > 4 else "-1"   # kernel variant number (16 / 17: w6) or "lib" (hipBLASLt)
         grp = int(argv[5]) if len(argv) > 5 else 8
         iters = int(argv[6]) if len(argv) > 6 else 20
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -30,13 +30,7 @@ def main(argv):
             if var == "lib":
                 torch.mm(a, w.t(), out=out)
                 return
-            if var == "w4":
-                err = lib.cgs_gemm_bf16_w4(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K, K, K, N, 0,
-                                           0, 1.0, None, None, 0, core._stream())
-            elif var == "w5":
-                err = lib.cgs_gemm_bf16_w5(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K, K, K, N, 0,
-                                           0, 1.0, core._stream())
-            else:
+            if True:
                 err = lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), None, None, M, N, K, K, K, N, 0,
                                           0, 1.0, int(var), core._stream())
             assert err == 0, err

@@ -1205,3 +1205,53 @@ def test_transformer_block_rowstats_matches(cuda, monkeypatch):
         y0 = blk(x, context=ctx, transformer_options={})
         assert getattr(y0, "_cgs_rowpart", None) is None
     assert _rel(y1, y0) < 5e-3
+
+
+# w6 (gemm_w6.hip, variant 16): one wave per SIMD, 64-deep full-line LDS-DMA K-tiles, persistent with the
+# next unit's first K-tiles prefetched under the current one; partial M / N tiles, several units per
+# workgroup (M x N >> 256 tiles), every epilogue (bias, residual, GEGLU, LayerNorm fold, LN + GEGLU).
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 336, 640), (4096, 1280, 1280), (16384, 3840, 1280),
+                                   (1232, 2560, 2048), (65536, 640, 640), (777, 4096, 256)])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_res", "geglu", "ln", "ln_geglu"])
+@pytest.mark.parametrize("variant", [16, 17], ids=["w6", "w6n160"])
+def test_gemm_w6(cuda, M, N, K, epi, variant):
+    lib = _native.load_kernels()
+    torch.manual_seed(3)
+    geglu, ln = "geglu" in epi, epi.startswith("ln")
+    if geglu and (N % 32 or variant == 17):
+        pytest.skip("GEGLU needs N % 32 == 0 and 256-wide tiles")
+    x = (torch.randn(M, K, device=cuda) * (3 if ln else 1) + (1.5 if ln else 0)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
+    nout = N // 2 if geglu else N
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
+    flags = (core.EPI_BIAS if b is not None else 0) | (core.EPI_RESIDUAL if r is not None else 0) | \
+        (core.EPI_GEGLU if geglu else 0)
+    if ln:
+        gamma = (torch.rand(K, device=cuda) + 0.5).to(torch.bfloat16)
+        beta = (torch.randn(K, device=cuda) * 0.2).to(torch.bfloat16)
+        xf = F.layer_norm(x.float(), (K,), gamma.float(), beta.float(), 1e-5)
+        rs = ops.layernorm_stats(x, 1e-5)
+    else:
+        xf = x.float()
+    h = xf @ w.float().t() + (b.float() if b is not None else 0)
+    if geglu:
+        a_, g_ = h.chunk(2, dim=-1)
+        ref = a_ * F.gelu(g_)
+        wk, bk = core.geglu_interleave(w), core.geglu_interleave(b)
+    else:
+        ref = h + (r.float() if r is not None else 0)
+        wk, bk = w, b
+    y = torch.empty(M, nout, device=cuda, dtype=torch.bfloat16)
+    if ln:
+        w2, cs, b2 = ops.lnfold_weights(wk, bk, gamma, beta)
+        assert lib.cgs_gemm_bf16_lnfold_v(x.data_ptr(), w2.data_ptr(), y.data_ptr(), b2.data_ptr(), rs.data_ptr(),
+                                          cs.data_ptr(), M, N, K, K, K, nout, flags | core.EPI_BIAS, None, 0, variant,
+                                          core._stream()) == 0
+    else:
+        assert lib.cgs_gemm_bf16_v(x.data_ptr(), wk.data_ptr(), y.data_ptr(), 0 if bk is None else bk.data_ptr(),
+                                   0 if r is None else r.data_ptr(), M, N, K, K, K, nout, N if r is not None else 0,
+                                   flags, 1.0, variant, core._stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    assert _rel(y, ref) < (1.5e-2 if ln else 1e-2), _rel(y, ref)

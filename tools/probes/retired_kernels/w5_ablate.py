@@ -66,7 +66,7 @@ def main(argv):
             for gc, tag in ((0, "p"), (1 << 30, "np")):
                 cands[f"w6d{d}{tag}"] = (lambda d=d, gc=gc: lib.cgs_gemm_bf16_w6(
                     a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), None, None, None, M, N, K, K, K, N, 0, 1,
-                    1.0, d, 4, gc, stream))
+                    1.0, d, 4, gc, 256, stream))
         cands["v7"] = lambda: lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), None, M, N,
                                                   K, K, K, N, 0, 1, 1.0, 7, stream)
         cands["v6"] = lambda: lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), None, M, N,
