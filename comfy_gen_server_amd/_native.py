@@ -163,6 +163,9 @@ KERNEL_SIGNATURES = {
     "cgs_attn_set_prio": [_I],
     "cgs_flash_attn_fwd_kv2": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _F, _P],
     "cgs_conv2d_nhwc_gns": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P],
+    # row-sharded GroupNorm (parallel/spatial.py): band statistics, then apply with combined (mean, rstd)
+    "cgs_groupnorm_band_stats": [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "cgs_groupnorm_apply_stats": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "cgs_groupnorm_nhwc_part": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
     "cgs_conv2d_nhwc_v7ws": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P],

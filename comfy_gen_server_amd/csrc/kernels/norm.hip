@@ -160,10 +160,13 @@ __device__ __forceinline__ void chan_merge(float& na, float& ma, float& qa, floa
   na = nn;
 }
 
+template <bool STATS_ONLY = false>
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ part, const void* __restrict__ gamma,
                                                          const void* __restrict__ beta, const void* __restrict__ pre_add,
                                                          float* __restrict__ ab, int HW, int C, int G, int ppb, int nb,
                                                          float eps, int wdt) {
+  // STATS_ONLY (row-sharded GroupNorm, parallel/spatial.py): ab[(n G + g) * 2] = (mean, M2) of this rank's
+  // band; the ranks' triples are Chan-combined on the host side and applied by gn_ab_from_stats_kernel.
   // one 256-thread block per (n, g): ONE pass over the per-(block, channel) (mean, M2) partials, each
   // thread Chan-combining its items (all loads of a round issued before any combine), then a Chan tree
   // over the wave (shuffles) and the 4 waves (LDS). (The two-pass form re-read every partial: at batch 1
@@ -210,6 +213,13 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
   cnt = red[0][0]; mean = red[1][0]; m2 = red[2][0];
 #pragma unroll
   for (int w = 1; w < 4; ++w) chan_merge(cnt, mean, m2, red[0][w], red[1][w], red[2][w]);
+  if constexpr (STATS_ONLY) {
+    if (tid == 0) {
+      ab[((size_t)n * G + g) * 2] = mean;
+      ab[((size_t)n * G + g) * 2 + 1] = m2;
+    }
+    return;
+  }
   const float var = m2 / fmaxf(cnt, 1.f);
   const float rstd = rsqrtf(fmaxf(var, 0.f) + eps);
   for (int cc = tid; cc < Cg; cc += 256) {
@@ -338,6 +348,73 @@ static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const 
 #undef CGS_GN_PARTIAL_PK
   gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
   return gn_apply_launch(x, x2, C1, y, ab, N, HW, C, silu, dtype, stream);
+}
+
+// The statistics half of groupnorm_impl: per-(n, g) (mean, M2) of the given rows into stats [N][G][2].
+static int groupnorm_stats_impl(const void* x, const void* x2, int C1, const void* pre_add, void* ws, float* stats,
+                                int N, int HW, int C, int G, int dtype, hipStream_t stream) {
+  const int ns = (C + 2047) / 2048;
+  if (C % 8 || C % G || C % (8 * ns) || C > 8192 || C1 % 8 || C1 > C) return (int)hipErrorInvalidValue;
+  const int CS = C / ns;
+  int ppb = gn_pix_per_block(N, HW);
+  int nb = (HW + ppb - 1) / ppb;
+  float* part = (float*)ws;
+  dim3 g1(nb, N, ns);
+  const int km = (CS / 8 + 63) / 64;
+  const int nch = CS / 8;
+#define CGS_GN_PARTIAL(KMV, PKV)                                                                                \
+  if (dtype == CGS_BF16)                                                                                        \
+    gn_partial_kernel<CGS_BF16, KMV, PKV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS); \
+  else                                                                                                          \
+    gn_partial_kernel<CGS_F16, KMV, PKV><<<g1, GN_THREADS, 8 * CS * sizeof(float), stream>>>((const u16*)x, (const u16*)x2, C1, part, HW, C, ppb, nb, CS);
+  if (nch <= 8) { CGS_GN_PARTIAL(1, 8) }
+  else if (nch <= 16) { CGS_GN_PARTIAL(1, 4) }
+  else if (nch <= 32) { CGS_GN_PARTIAL(1, 2) }
+  else if (km == 1) { CGS_GN_PARTIAL(1, 1) } else if (km == 2) { CGS_GN_PARTIAL(2, 1) }
+  else if (km == 3) { CGS_GN_PARTIAL(3, 1) } else { CGS_GN_PARTIAL(4, 1) }
+#undef CGS_GN_PARTIAL
+  gn_finalize_kernel<true><<<dim3(G, N), 256, 0, stream>>>(part, nullptr, nullptr, pre_add, stats, HW, C, G, ppb, nb,
+                                                          0.f, dtype);
+  return (int)hipGetLastError();
+}
+
+// (mean, rstd) per (n, g) -> the per-(n, c) affine of gn_apply (gamma / beta / pre-add folded as in finalize).
+__global__ __launch_bounds__(256) void gn_ab_from_stats_kernel(const float* __restrict__ mr, const void* __restrict__ gamma,
+                                                               const void* __restrict__ beta,
+                                                               const void* __restrict__ pre_add, float* __restrict__ ab,
+                                                               int N, int C, int G, int wdt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C, g = c / (C / G);
+  auto ld = [&](const void* p, int idx) -> float {
+    return (wdt == CGS_BF16) ? bf2f(((const u16*)p)[idx]) : (wdt == CGS_F16 ? h2f(((const u16*)p)[idx]) : ((const float*)p)[idx]);
+  };
+  const float mean = mr[((size_t)n * G + g) * 2], rstd = mr[((size_t)n * G + g) * 2 + 1];
+  const float gm = gamma ? ld(gamma, c) : 1.f, bt = beta ? ld(beta, c) : 0.f;
+  const float sh = pre_add ? ld(pre_add, n * C + c) : 0.f;
+  const float a = rstd * gm;
+  ab[(size_t)i * 2] = a;
+  ab[(size_t)i * 2 + 1] = (sh - mean) * a + bt;
+}
+
+// Row-sharded GroupNorm (latency mode, parallel/spatial.py), step 1: this rank's band statistics.
+// x ([N, HW, C1]) / x2 ([N, HW, C - C1], or null: C1 = C) NHWC; pre_add [N, C] or null; ws of
+// cgs_groupnorm_workspace(N, HW, C) bytes; stats out: [N][G] (mean, M2) over the band (count = HW * C / G).
+CGS_EXPORT int cgs_groupnorm_band_stats(const void* x, const void* x2, int C1, const void* pre_add, void* ws,
+                                        float* stats, int N, int HW, int C, int G, int dtype, hipStream_t stream) {
+  if (!stats || !ws || HW <= 0) return (int)hipErrorInvalidValue;
+  return groupnorm_stats_impl(x, x2 ? x2 : nullptr, x2 ? C1 : C, pre_add, ws, stats, N, HW, C, G, dtype, stream);
+}
+
+// Step 2 (after the ranks' (mean, M2) were combined): y = GN(x) with the given per-(n, g) (mean, rstd).
+// ab: N * C * 2 floats of workspace.
+CGS_EXPORT int cgs_groupnorm_apply_stats(const void* x, const void* x2, int C1, void* y, const void* gamma,
+                                         const void* beta, const void* pre_add, const float* mean_rstd, float* ab,
+                                         int N, int HW, int C, int G, int silu, int dtype, hipStream_t stream) {
+  if (C % 8 || C % G || !mean_rstd || !ab || (x2 && (C1 % 8 || C1 > C))) return (int)hipErrorInvalidValue;
+  gn_ab_from_stats_kernel<<<(unsigned)((N * C + 255) / 256), 256, 0, stream>>>(mean_rstd, gamma, beta, pre_add, ab, N,
+                                                                              C, G, dtype);
+  return gn_apply_launch(x, x2, x2 ? C1 : C, y, ab, N, HW, C, silu, dtype, stream);
 }
 
 static int gn_apply_launch(const void* x, const void* x2, int C1, void* y, const float* ab, int N, int HW, int C,

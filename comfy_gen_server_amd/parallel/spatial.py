@@ -11,7 +11,11 @@ rows ``[r * H / P, (r + 1) * H / P)`` of every feature map at every level and
   two rows from above for the stride-2 downsample; one row each way BEFORE the fused nearest-2x
   upsample), convolve the extended band and keep the interior -- the first / last rank's halo is
   zeros, which is the convolution's zero padding;
-* GroupNorm statistics are summed over the group (one all-reduce of [N, groups, 2] fp64 per norm);
+* GroupNorm statistics: each rank computes its band's per-(image, group) (mean, M2) with the native
+  statistics kernel (``cgs_groupnorm_band_stats``), the [P, N, groups, 2] fp32 partials are all-gathered
+  (a few KB) and Chan-combined (no cancellation, no fp64), and the native apply kernel normalises the band
+  (``cgs_groupnorm_apply_stats``, SiLU / timestep pre-add / dual-source skip concat fused as in the
+  single-GPU GroupNorm); on the CPU the same two steps run in fp32 torch;
 * the SpatialTransformers take their local rows as their token shard: self-attention runs over the
   whole image through ``SeqParallel.attention`` (Ulysses all-to-all or K/V all-gather), everything
   else is token-local;
@@ -55,30 +59,51 @@ class SpatialShard:
 
     def halo(self, x, top: int, bottom: int):
         """[N, C, top + R + bottom, W]: ``top`` rows from the rank above and ``bottom`` rows from the rank
-        below around the local band (zeros at the image edge)."""
+        below around the local band (zeros at the image edge). The extended band is allocated once and the
+        neighbours' rows are received straight into it (NHWC: for one image a row range is one contiguous
+        block), so the only copy is the band itself."""
         self.stats["halo"] += 1
         N, C, R, W = x.shape
         above, below = self.rank - 1, self.rank + 1
-        ops = []
-        recv_top = recv_bot = None
+        cl = x.is_cuda
+        ext = torch.empty((N, C, top + R + bottom, W), dtype=x.dtype, device=x.device,
+                          memory_format=torch.channels_last if cl else torch.contiguous_format)
+        ext[:, :, top:top + R] = x
+        ops, fix = [], []
+
+        fmt = torch.channels_last if cl else torch.contiguous_format
+
+        def slot(lo, n):
+            v = ext[:, :, lo:lo + n]
+            if v.is_contiguous(memory_format=fmt):
+                return v, None            # receive in place
+            return torch.empty((N, C, n, W), dtype=x.dtype, device=x.device, memory_format=fmt), v
         if top:
-            recv_top = torch.zeros((N, C, top, W), dtype=x.dtype, device=x.device)
             if above >= 0:
-                ops.append(dist.P2POp(dist.irecv, recv_top, self.ranks[above], self.group))
+                buf, dst = slot(0, top)
+                ops.append(dist.P2POp(dist.irecv, buf, self.ranks[above], self.group))
+                if dst is not None:
+                    fix.append((dst, buf))
+            else:
+                ext[:, :, :top].zero_()
             if below < self.P:    # my last `top` rows are the lower neighbour's top halo
                 ops.append(dist.P2POp(dist.isend, x[:, :, R - top:].contiguous(), self.ranks[below], self.group))
         if bottom:
-            recv_bot = torch.zeros((N, C, bottom, W), dtype=x.dtype, device=x.device)
             if below < self.P:
-                ops.append(dist.P2POp(dist.irecv, recv_bot, self.ranks[below], self.group))
+                buf, dst = slot(top + R, bottom)
+                ops.append(dist.P2POp(dist.irecv, buf, self.ranks[below], self.group))
+                if dst is not None:
+                    fix.append((dst, buf))
+            else:
+                ext[:, :, top + R:].zero_()
             if above >= 0:        # my first `bottom` rows are the upper neighbour's bottom halo
                 ops.append(dist.P2POp(dist.isend, x[:, :, :bottom].contiguous(), self.ranks[above], self.group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        parts = [p for p in (recv_top, x, recv_bot) if p is not None]
-        out = torch.cat(parts, dim=2)
-        return out.contiguous(memory_format=torch.channels_last) if x.is_cuda else out
+        for dst, buf in fix:
+            dst.copy_(buf)
+        return ext
 
     # ---- layers ----------------------------------------------------------------------------------
     def conv2d(self, conv_fn, x, kh, stride, padding, upsample2x, x2):
@@ -101,25 +126,62 @@ class SpatialShard:
         self.stats["gather_fallback"] += 1
         return self.shard_rows(conv_fn(self.gather_rows(x), None))
 
+    def _gather_stats(self, st):
+        """[N, G, 2] (mean, M2) of every rank of the group -> [P, N, G, 2]."""
+        if self.P == 1:
+            return st[None]
+        parts = [torch.empty_like(st) for _ in range(self.P)]
+        dist.all_gather(parts, st.contiguous(), group=self.group)
+        return torch.stack(parts)
+
     def group_norm(self, x, groups, weight, bias, eps, silu=False, pre_add=None, x2=None):
-        """GroupNorm over the whole image from band-local sums (fp64 all-reduce of [N, G, 2])."""
+        """GroupNorm over the whole image from the bands' (mean, M2) (Chan combine of the all-gathered
+        [P, N, G, 2] fp32 partials; equal band sizes)."""
+        from ..ops import core
         self.stats["gn"] += 1
-        if x2 is not None:
-            x = torch.cat([x, x2.to(x.dtype)], dim=1)
-        xf = x.float()
-        if pre_add is not None:
-            xf = xf + pre_add.float()[:, :, None, None]
-        N, C, R, W = xf.shape
-        g = xf.reshape(N, groups, C // groups, R, W)
-        s = torch.stack([g.sum(dim=(2, 3, 4), dtype=torch.float64),
-                         (g.double() ** 2).sum(dim=(2, 3, 4))], dim=-1)
-        dist.all_reduce(s, group=self.group)
-        cnt = float((C // groups) * R * W * self.P)
-        mean = s[..., 0] / cnt
-        var = (s[..., 1] / cnt - mean * mean).clamp_min(0.0)
-        rstd = torch.rsqrt(var + eps)
-        y = (g - mean.float()[:, :, None, None, None]) * rstd.float()[:, :, None, None, None]
-        y = y.reshape(N, C, R, W)
+        N, C1, R, W = x.shape
+        C = C1 + (0 if x2 is None else x2.shape[1])
+        native = (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and weight is not None and C % 8 == 0
+                  and C1 % 8 == 0 and C % groups == 0 and C <= 8192 and C % (8 * ((C + 2047) // 2048)) == 0
+                  and (x2 is None or (x2.dtype == x.dtype and x2.is_cuda))
+                  and core._native.has_kernel("cgs_groupnorm_band_stats"))
+        cnt = float((C // groups) * R * W)
+        if native:
+            lib, dt = core._lib(), core._DT[x.dtype]
+            xc = x.contiguous(memory_format=torch.channels_last)
+            x2c = None if x2 is None else x2.contiguous(memory_format=torch.channels_last)
+            pa = None if pre_add is None else pre_add.to(x.dtype).contiguous()
+            ws = torch.empty((int(lib.cgs_groupnorm_workspace(N, R * W, C)) + 3) // 4, device=x.device,
+                             dtype=torch.float32)
+            st = torch.empty((N, groups, 2), device=x.device, dtype=torch.float32)
+            core._check(lib.cgs_groupnorm_band_stats(xc.data_ptr(), core._ptr(x2c), C1, core._ptr(pa), ws.data_ptr(),
+                                                     st.data_ptr(), N, R * W, C, groups, dt, core._stream()),
+                        "cgs_groupnorm_band_stats")
+        else:
+            xf = x.float() if x2 is None else torch.cat([x.float(), x2.float()], dim=1)
+            if pre_add is not None:
+                xf = xf + pre_add.float()[:, :, None, None]
+            g = xf.reshape(N, groups, -1)
+            mean = g.mean(-1)
+            st = torch.stack([mean, ((g - mean[..., None]) ** 2).sum(-1)], dim=-1)
+        allst = self._gather_stats(st)
+        mean = allst[..., 0].mean(0)
+        m2 = allst[..., 1].sum(0) + cnt * ((allst[..., 0] - mean) ** 2).sum(0)
+        rstd = torch.rsqrt((m2 / (cnt * self.P)).clamp_min(0.0) + eps)
+        if native:
+            core.count("groupnorm", "hip")
+            self.stats["gn_native"] = self.stats.get("gn_native", 0) + 1
+            w = weight.to(device=x.device, dtype=x.dtype).contiguous()
+            b = None if bias is None else bias.to(device=x.device, dtype=x.dtype).contiguous()
+            mr = torch.stack([mean, rstd], dim=-1).contiguous()
+            ab = torch.empty(N * C * 2, device=x.device, dtype=torch.float32)
+            y = torch.empty((N, C, R, W), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+            core._check(lib.cgs_groupnorm_apply_stats(xc.data_ptr(), core._ptr(x2c), C1, y.data_ptr(), w.data_ptr(),
+                                                      core._ptr(b), core._ptr(pa), mr.data_ptr(), ab.data_ptr(), N,
+                                                      R * W, C, groups, 1 if silu else 0, dt, core._stream()),
+                        "cgs_groupnorm_apply_stats")
+            return y
+        y = ((g - mean[..., None]) * rstd[..., None]).reshape(N, C, R, W)
         if weight is not None:
             y = y * weight.float()[None, :, None, None]
         if bias is not None:

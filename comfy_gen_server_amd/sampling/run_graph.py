@@ -188,7 +188,12 @@ def try_run(ksampler, guider, mk, x, sigmas, extra_args, callback):
     from ..sched import spmd
     ctx = spmd.active()
     if ctx is not None and ctx.mode == "latency":
-        return _ineligible("latency mode (collectives inside the UNet call)")
+        # The UNet call's collectives (CFG all-gather, halo send / recv, GroupNorm statistics) are RCCL ops
+        # on the capturing stream, which RCCL records into the graph. Opt-in: every rank of the group must
+        # make the same capture / replay decision, and a capture failure on one rank would leave the others
+        # inside a captured collective -- CGS_LATENCY_GRAPHS=1 once a node has been validated with it.
+        if os.environ.get("CGS_LATENCY_GRAPHS") != "1" or getattr(ctx.comm, "backend", None) != "nccl":
+            return _ineligible("latency mode (collectives inside the UNet call; CGS_LATENCY_GRAPHS=1 captures them)")
     fn = ksampler.sampler_function
     if getattr(fn, "__name__", "") in ("sample_dpm_fast", "sample_dpm_adaptive", "fn"):
         return _ineligible("adaptive step size (host-side error control)")

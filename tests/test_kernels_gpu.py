@@ -1255,3 +1255,54 @@ def test_gemm_w6(cuda, M, N, K, epi, variant):
     torch.cuda.synchronize()
     assert torch.isfinite(y).all()
     assert _rel(y, ref) < (1.5e-2 if ln else 1e-2), _rel(y, ref)
+
+
+@pytest.mark.parametrize("C,C2,G,silu,pre", [(640, 0, 32, True, True), (1280, 0, 32, False, False),
+                                              (640, 320, 32, True, False), (320, 0, 32, True, True)])
+def test_row_sharded_groupnorm_native(cuda, C, C2, G, silu, pre):
+    """Latency mode's row-sharded GroupNorm (parallel/spatial.py) on the native kernels: each band's
+    (mean, M2) from cgs_groupnorm_band_stats, Chan-combined, applied by cgs_groupnorm_apply_stats -- two
+    bands of one image reproduce the fp32 GroupNorm of the whole image; no ATen GroupNorm runs."""
+    from comfy_gen_server_amd.parallel.spatial import SpatialShard
+    torch.manual_seed(5)
+    H, W = 32, 24
+    x = (torch.randn(1, C, H, W, device=cuda) * 2 + 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    x2 = (torch.randn(1, C2, H, W, device=cuda)).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last) if C2 else None
+    Ct = C + C2
+    w = (torch.rand(Ct, device=cuda) + 0.5).to(torch.bfloat16)
+    b = (torch.randn(Ct, device=cuda) * 0.1).to(torch.bfloat16)
+    pa = torch.randn(1, Ct, device=cuda).to(torch.bfloat16) if pre else None
+    xf = x.float() if x2 is None else torch.cat([x.float(), x2.float()], 1)
+    if pa is not None:
+        xf = xf + pa.float()[:, :, None, None]
+    ref = F.group_norm(xf, G, w.float(), b.float(), 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    bands = []
+    for r in range(2):
+        sc = SpatialShard(None, 2, r, [0, 1])
+        other = SpatialShard(None, 1, 0, [0])
+
+        def gather(st, sc=sc, r=r):
+            lo, hi = sc.band(H)
+            olo, ohi = (hi, H) if r == 0 else (0, lo)
+            xo = x[:, :, olo:ohi]
+            x2o = None if x2 is None else x2[:, :, olo:ohi]
+            # the other band's statistics through the same native kernel (a 1-rank shard of its rows)
+            cap = {}
+            other._gather_stats = lambda s2: cap.setdefault("s", s2)[None]
+            other.group_norm(xo, G, w, b, 1e-5, silu=silu, pre_add=pa, x2=x2o)
+            parts = [st, cap["s"]] if r == 0 else [cap["s"], st]
+            return torch.stack(parts)
+        sc._gather_stats = gather
+        ops.reset_stats()
+        lo, hi = sc.band(H)
+        yb = sc.group_norm(x[:, :, lo:hi], G, w, b, 1e-5, silu=silu, pre_add=pa,
+                           x2=None if x2 is None else x2[:, :, lo:hi])
+        assert sc.stats.get("gn_native", 0) == 1
+        assert ops.stats().get(("groupnorm", "hip"), 0) >= 1 and not any(k[1] == "lib" for k in ops.stats())
+        bands.append(yb)
+    y = torch.cat(bands, dim=2)
+    assert _rel(y, ref) < 1e-2, _rel(y, ref)
