@@ -30,7 +30,7 @@ def conditioning_set_values(conditioning, values=None):
 
 def prepare_callback(model, steps, x0_output_dict=None):
     """Per-step progress (+ optional async latent preview, every ``preview_every`` steps)."""
-    from ..utils.preview import Latent2RGBPreviewer, get_previewer
+    from ..utils.preview import get_previewer
     previewer = get_previewer(model.load_device, model.model.latent_format, _FLAGS["preview_method"])
     pbar = ProgressBar(steps)
     every = max(1, int(_FLAGS["preview_every"]))
@@ -40,9 +40,6 @@ def prepare_callback(model, steps, x0_output_dict=None):
             x0_output_dict["x0"] = x0
         preview = None
         if previewer is not None and (step % every == 0 or step + 1 == total_steps):
-            if isinstance(previewer, Latent2RGBPreviewer):
-                preview = previewer.decode_latent_to_preview_image("JPEG", x0, block=step + 1 == total_steps)
-            else:
-                preview = previewer.decode_latent_to_preview_image("JPEG", x0)
+            preview = previewer.decode_latent_to_preview_image("JPEG", x0, block=step + 1 == total_steps)
         pbar.update_absolute(step + 1, total_steps, preview)
     return callback

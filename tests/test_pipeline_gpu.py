@@ -44,3 +44,26 @@ def test_family_pipeline_captures_and_stays_native(cuda, family):
     assert step_graph.stats.get("capture_failed", 0) == before.get("capture_failed", 0)
     assert step_graph.stats["replay"] > before["replay"]
     assert img.shape[0] == 2 and torch.isfinite(img.float()).all()
+
+
+def test_taesd_preview_is_async_on_gpu(cuda):
+    """TAESD previews decode on a side stream: a step's call returns at once (an earlier preview or
+    None), never more than `depth` decodes are queued, and the blocking last call returns the newest
+    step's image, equal to a direct decode."""
+    import numpy as np
+    from comfy_gen_server_amd.models.layers import init_random_
+    from comfy_gen_server_amd.models.taesd import TAESD
+    from comfy_gen_server_amd.utils.preview import TAESDPreviewerImpl
+    t = TAESD(None, None, latent_channels=4)
+    init_random_(t, seed=3)
+    t = t.to(cuda)
+    prev = TAESDPreviewerImpl(t)
+    xs = [torch.randn(1, 4, 64, 64, device=cuda) for _ in range(6)]
+    with torch.inference_mode():
+        outs = [prev.decode_latent_to_preview_image("JPEG", x, block=(i == 5)) for i, x in enumerate(xs)]
+        ref = t.decode(xs[-1])[0].movedim(0, 2).clamp(0, 1).float().cpu()
+    assert prev.submitted + prev.skipped == 6 and len(prev._pending) == 0
+    last = outs[-1][1]
+    got = torch.from_numpy(np.asarray(last).astype(np.float32)) / 255.0
+    assert last.size == (512, 512)
+    assert (got - ref).abs().max() <= 2.0 / 255, (got - ref).abs().max()
