@@ -128,6 +128,12 @@ KERNEL_SIGNATURES = {
     "cgs_grn_scale_weight": [_P, _P, _P, _I, _I, _I, _I, _P, _P],
     # host (mmap) -> device upload through pinned double buffers (csrc/kernels/io.hip)
     "cgs_h2d_upload": [_P, _P, _L, _L, _I, _P],                        # src, dst, nbytes, chunk, threads
+    # f32.hip: fp32-I/O GEMM / conv / GroupNorm / LayerNorm (--force-fp32, --fp32-vae)
+    "cgs_gemm_f32": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _I, _L, _L, _L, _P],
+    "cgs_conv_f32": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "cgs_groupnorm_f32_ws": [_I, _I, _I],
+    "cgs_groupnorm_f32": [_P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
+    "cgs_layernorm_f32": [_P, _P, _P, _P, _L, _I, _F, _P],
     "cgs_softmax_rows": [_P, _P, _L, _I, _F, _I, _P],                  # x, y(f32), rows, cols, scale, dtype
     # bf16 activations x fp8-e4m3fn weights (K21), same epilogues as cgs_gemm_bf16
     "cgs_gemm_bf16_w8": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P],
@@ -197,7 +203,7 @@ KERNEL_SIGNATURES = {
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_groupnorm_f32_ws": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
             "cgs_attn_set_variant": None,
             "cgs_conv_v6_set_loader": None}

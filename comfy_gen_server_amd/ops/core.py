@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from .. import _native
 from . import autotune
+from . import f32 as _f32
 from .dispatch import backend_for, count, vendor_fallback
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -103,6 +104,11 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             return linear(x, weight.to(x.dtype), None if bias is None else bias.to(x.dtype), residual, act, out)
         return _linear_w8(x, weight, bias, residual)
     be = backend_for("gemm", x, "cgs_gemm_bf16")
+    if be == "hip" and x.dtype == torch.float32 and weight.dtype == torch.float32 and _f32.available():
+        y = _f32.linear(x, weight, bias, residual, act, out)     # --force-fp32 / --fp32-vae (f32.hip)
+        if y is not None:
+            count("gemm", "hip")
+            return y
     # K % 8: the kernels' 16-byte row loads (a K=2 coordinate MLP is not GEMM-shaped work anyway)
     if be == "hip" and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
         K = x.shape[-1]
@@ -353,6 +359,11 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
     Sk = k.shape[1]
     D = HD // heads
     be = backend_for("attention", q, "cgs_flash_attn_fwd")
+    if be == "hip" and q.dtype == torch.float32 and _f32.available():
+        o = _f32.attention(q, k, v, heads, mask=mask, causal=causal, key_padding=key_padding)
+        if o is not None:
+            count("attention", "hip")
+            return o
     wide_ok = D == 512 and not causal and key_padding is None
     if (be == "hip" and mask is None and (D in _FLASH_HEAD_DIMS or wide_ok) and q.dtype == torch.bfloat16
             and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1):
@@ -684,6 +695,11 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
         return sc.group_norm(x, groups, weight, bias, eps, silu=silu, pre_add=pre_add, x2=x2)
     be = backend_for("groupnorm", x, "cgs_groupnorm_nhwc_ws")
     Ct = x.shape[1] + (0 if x2 is None else x2.shape[1])
+    if be == "hip" and x.dim() == 4 and x.dtype == torch.float32 and _f32.available("cgs_groupnorm_f32"):
+        y = _f32.group_norm(x, groups, weight, bias, eps, silu, x2, pre_add)     # f32.hip
+        if y is not None:
+            count("groupnorm", "hip")
+            return y
     if be == "hip" and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16) and \
             weight is not None and Ct % 8 == 0 and Ct % groups == 0 and Ct <= 8192 and \
             Ct % (8 * ((Ct + 2047) // 2048)) == 0 and x.shape[1] % 8 == 0 and \
@@ -744,6 +760,11 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor 
                eps: float = 1e-5) -> torch.Tensor:
     be = backend_for("layernorm", x, "cgs_layernorm")
     C = x.shape[-1]
+    if be == "hip" and x.dtype == torch.float32 and _f32.available("cgs_layernorm_f32"):
+        y = _f32.layer_norm(x, weight, bias, eps)
+        if y is not None:
+            count("layernorm", "hip")
+            return y
     if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0:
         count("layernorm", "hip")
         xc = x.contiguous()
@@ -806,6 +827,12 @@ def _conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, st
     be = backend_for("conv", x, "cgs_conv2d_nhwc")
     Cout, Cin_g, kh, kw = weight.shape
     cin_total = x.shape[1] + (0 if x2 is None else x2.shape[1])
+    if (be == "hip" and groups == 1 and x.dtype == torch.float32 and weight.dtype == torch.float32
+            and _f32.available("cgs_conv_f32")):
+        y = _f32.conv2d(x, weight, bias, stride, padding, residual, weight_nhwc, upsample2x, x2)
+        if y is not None:
+            count("conv", "hip")
+            return y
     hip_ok = (be == "hip" and groups == 1 and x.dtype == torch.bfloat16 and weight_nhwc is not None
               and x.dim() == 4 and cin_total % 32 == 0 and (Cout % 8 == 0 or Cout <= 16 or cin_total % 64 == 0))
     dual_ok = x2 is None or (hip_ok and x.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0 and x2.dtype == x.dtype

@@ -83,7 +83,7 @@ def main(quick=False, attn_only=False, gemm_only=False):
         lib = ops.dispatch._native.load_kernels()
         ent = dict(B=b, H=h, Sq=sq, Sk=sk, D=d)
         ref = None
-        for var, name in ((1, "generic"), (2, "d64"), (4, "d64r2"), (5, "d64q128"), (0, "auto")):
+        for var, name in ((1, "generic"), (2, "d64"), (5, "d64q128"), (0, "auto")):
             lib.cgs_attn_set_variant(var)
             y = ops.attention(q, k, v, h).float()
             if ref is None:
