@@ -124,6 +124,11 @@ KERNEL_SIGNATURES = {
     "cgs_grn_nhwc": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P],          # x, gamma, beta, y, ws, N, HW, C
     # GRN statistics only (gx / block sums in the v2 ws layout): x, ws, N, HW, C, pre_gelu, dtype
     "cgs_grn_stats": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "cgs_splitk_ws_bytes": [_I, _I, _I],
+    "cgs_gemm_bf16_splitk": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _I, _I, _P, _L, _P],
+    "cgs_grn_stats_gns": [_P, _P, _I, _I, _I, _P],                      # part, ws, N, HW, C
+    "cgs_grn_apply_gns": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],      # h, part, gamma, beta, y, ws, N, HW, C
+    "cgs_gemm_bf16_gelu_gns": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _I, _P, _I, _P],
     # per-image GRN-scaled weights of the next Linear: W, gamma, ws(stats), N, HW, O, K, Wn
     "cgs_grn_scale_weight": [_P, _P, _P, _I, _I, _I, _I, _P, _P],
     # host (mmap) -> device upload through pinned double buffers (csrc/kernels/io.hip)
@@ -203,7 +208,7 @@ KERNEL_SIGNATURES = {
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_groupnorm_f32_ws": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_splitk_ws_bytes": ctypes.c_longlong, "cgs_groupnorm_f32_ws": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
             "cgs_attn_set_variant": None,
             "cgs_conv_v6_set_loader": None}

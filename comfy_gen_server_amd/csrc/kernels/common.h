@@ -24,13 +24,11 @@ __device__ __forceinline__ float bf2f(u16 v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
 
+// fp32 -> bf16, round-to-nearest-even, NaN kept NaN: the gfx950 conversion instruction (v_cvt_pk_bf16_f32),
+// one VALU op and no branch (the integer RNE sequence with its inf / NaN branch was ~8 ops + an exec-mask
+// branch per element: most of the VALU of the elementwise kernels)
 __device__ __forceinline__ u16 f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) {  // inf / nan: keep class
-    return (u16)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  }
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (u16)(u >> 16);
+  return __builtin_bit_cast(u16, (__bf16)f);
 }
 
 __device__ __forceinline__ float h2f(u16 v) {
@@ -70,7 +68,9 @@ __device__ __forceinline__ float4 unpack4_bf16(uint2 w) {
                 __uint_as_float(w.y & 0xffff0000u)};
 }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division (~10 VALU ops:
+// div_scale x2, rcp, fma chain, div_fmas, div_fixup): far below the bf16 / fp16 output ulp
+__device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 __device__ __forceinline__ float gelu_f(float x) {  // exact erf GELU (torch default)
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));

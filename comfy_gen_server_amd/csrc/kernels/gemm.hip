@@ -449,6 +449,130 @@ static int gemm_v8_launch(const void* A, const void* W, void* C, const void* bia
   return gemm_small_tile_launch<128, 128>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs);
 }
 
+// Split-K form of the v8 family (K13, batch-1 grids): blockIdx.y = K slice z, the tile computes
+// A[:, z Ks : (z + 1) Ks] . W[:, same]^T into the fp32 partial ws[z] (MC_EPI_F32RAW); splitk_reduce_kernel
+// then sums the slices and applies the whole epilogue (alpha, LayerNorm fold, bias, GELU, residual) once.
+// For the under-filled shapes of SDXL batch 1 (M = 2048: FF-out K = 5120, out-proj K = 1280) a 160-tile
+// grid becomes 320-640 workgroups.
+template <int BN, int BMV, int NS = mc::STAGES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v8sk_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, float* __restrict__ ws, int M, int N, int Ks,
+    long long lda, long long ldw, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  grouped_tile(logical, gridDim.x / tiles_n, tiles_n, group_m, tm, tn);
+  const long long kb = (long long)blockIdx.y * Ks;
+  DenseA al{A + kb, lda, M, {}};
+  mc::Epi e{reinterpret_cast<u16*>(ws + (long long)blockIdx.y * M * N), nullptr, nullptr, N, 0, MC_EPI_F32RAW, 1.f};
+  mc::tile<BN, 4, DenseA, BMV, NS>(al, W + kb, ldw, M, N, Ks, tm * BMV, tn * BN, e, smem);
+}
+
+// out = epilogue(alpha * sum_z ws[z]) per 8-column chunk: LN fold (rs / cs), bias, GELU, residual -> bf16
+template <bool LNF, bool ACT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, u16* __restrict__ C,
+                                                            const u16* __restrict__ bias, const u16* __restrict__ R,
+                                                            const float* __restrict__ rs, const float* __restrict__ cs,
+                                                            int M, int N, long long ldc, long long ldr, float alpha,
+                                                            int flags) {
+  const unsigned cpr = (unsigned)N >> 3;
+  const long long chunks = (long long)M * cpr;
+  const long long MN = (long long)M * N;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < chunks; i += (long long)gridDim.x * 256) {
+    const unsigned row = (unsigned)(i / cpr);
+    const int c0 = (int)(i - (long long)row * cpr) * 8;
+    const float* p = ws + (long long)row * N + c0;
+    float4 a0 = *reinterpret_cast<const float4*>(p), a1 = *reinterpret_cast<const float4*>(p + 4);
+    for (int z = 1; z < S; ++z) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p + z * MN), b1 = *reinterpret_cast<const float4*>(p + z * MN + 4);
+      a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+      a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+    }
+    float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    if constexpr (LNF) {
+      const float2 st = *reinterpret_cast<const float2*>(rs + 2 * (long long)row);
+      const float4 q0 = *reinterpret_cast<const float4*>(cs + c0), q1 = *reinterpret_cast<const float4*>(cs + c0 + 4);
+      const float q[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = st.y * (v[t] - st.x * q[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] *= alpha;
+    }
+    if (flags & MC_EPI_BIAS) {
+      const uint4 b = *reinterpret_cast<const uint4*>(bias + c0);
+      const float4 lo = unpack4_bf16(uint2{b.x, b.y}), hi = unpack4_bf16(uint2{b.z, b.w});
+      v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w; v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+    }
+    if constexpr (ACT) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = gelu_sig(v[t]);
+    }
+    if (flags & MC_EPI_RESIDUAL) {
+      const uint4 rr = *reinterpret_cast<const uint4*>(R + (long long)row * ldr + c0);
+      const float4 lo = unpack4_bf16(uint2{rr.x, rr.y}), hi = unpack4_bf16(uint2{rr.z, rr.w});
+      v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w; v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+    }
+    const uint2 o0 = pack4_bf16(v[0], v[1], v[2], v[3]), o1 = pack4_bf16(v[4], v[5], v[6], v[7]);
+    *reinterpret_cast<uint4*>(C + (long long)row * ldc + c0) = uint4{o0.x, o0.y, o1.x, o1.y};
+  }
+}
+
+template <int BN, int BMV, int NS = mc::STAGES>
+static int gemm_splitk_go(const void* A, const void* W, float* ws, int M, int N, int Ks, int S, long long lda,
+                          long long ldw, hipStream_t stream) {
+  using Cf = mc::Cfg<BN, 4, BMV, NS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v8sk_kernel<BN, BMV, NS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Cf::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + BN - 1) / BN;
+  const long long nwg = (long long)((M + BMV - 1) / BMV) * tiles_n;
+  if (nwg > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  gemm_bf16_nt_v8sk_kernel<BN, BMV, NS><<<dim3((unsigned)nwg, (unsigned)S), 256, Cf::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, ws, M, N, Ks, lda, ldw, tiles_n, g_tile_group);
+  return (int)hipGetLastError();
+}
+
+// Bytes of fp32 workspace cgs_gemm_bf16_splitk needs.
+CGS_EXPORT long long cgs_splitk_ws_bytes(int M, int N, int splits) { return 4LL * splits * M * N; }
+
+// Split-K GEMM (see gemm_bf16_nt_v8sk_kernel): variant 8 / 10 / 11 / 14 = the v8 tile shapes; splits
+// 2..8 with K % (32 * splits) == 0. epi: bias, residual, LN fold (rs / cs, alpha ignored), GELU -- no GEGLU.
+CGS_EXPORT int cgs_gemm_bf16_splitk(const void* A, const void* W, void* C, const void* bias, const void* R,
+                                    const float* rs, const float* cs, int M, int N, int K, long long lda,
+                                    long long ldw, long long ldc, long long ldr, int epi, float alpha, int splits,
+                                    int variant, float* ws, long long ws_bytes, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (splits < 2 || splits > 8 || K % (32 * splits) || N % 8 || lda % 8 || ldw % 8 || ldc % 8 ||
+      (epi & ~(EPI_BIAS | EPI_RESIDUAL | EPI_LNFOLD | EPI_GELU)) || ((epi & EPI_RESIDUAL) && (!R || ldr % 8)) ||
+      ((epi & EPI_BIAS) && !bias) || ((epi & EPI_LNFOLD) && (!rs || !cs)) || !ws ||
+      ws_bytes < cgs_splitk_ws_bytes(M, N, splits) ||
+      (((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)bias | (uintptr_t)R | (uintptr_t)ws) & 15))
+    return (int)hipErrorInvalidValue;
+  const int Ks = K / splits;
+  int rc;
+  switch (variant) {
+    case 10: rc = gemm_splitk_go<128, 64>(A, W, ws, M, N, Ks, splits, lda, ldw, stream); break;
+    case 11: rc = gemm_splitk_go<64, 128>(A, W, ws, M, N, Ks, splits, lda, ldw, stream); break;
+    case 14: rc = gemm_splitk_go<128, 128, 5>(A, W, ws, M, N, Ks, splits, lda, ldw, stream); break;
+    default: rc = gemm_splitk_go<128, 128>(A, W, ws, M, N, Ks, splits, lda, ldw, stream);
+  }
+  if (rc) return rc;
+  const long long chunks = (long long)M * (N / 8);
+  const long long nb = (chunks + 255) / 256;
+  const unsigned blocks = (unsigned)(nb > 8192 ? 8192 : nb);
+  const bool lnf = (epi & EPI_LNFOLD) != 0, act = (epi & EPI_GELU) != 0;
+#define CGS_SKR(L, G) splitk_reduce_kernel<L, G><<<blocks, 256, 0, stream>>>(ws, splits, (u16*)C, (const u16*)bias, \
+      (const u16*)R, rs, cs, M, N, ldc, ldr, alpha, epi)
+  if (lnf) { if (act) CGS_SKR(true, true); else CGS_SKR(true, false); }
+  else { if (act) CGS_SKR(false, true); else CGS_SKR(false, false); }
+#undef CGS_SKR
+  return (int)hipGetLastError();
+}
+
 template <int BN, int NW>
 static void gemm_v3_go(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                        long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
@@ -680,6 +804,55 @@ static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bia
   return (int)hipGetLastError();
 }
 
+
+// v6 GEMM whose epilogue also writes per-(image, 64-row block, column) sums of squares of its bf16 output
+// (pq::run GNS = 2, the sum-of-squares form of the conv GroupNorm-statistics epilogue) -- for Stable
+// Cascade's ChannelMLP, where the GlobalResponseNorm after Linear -> GELU needs sum_HW h^2 per (image,
+// channel): cgs_grn_apply_gns sums these partials instead of a statistics pass over h.
+template <bool LN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_gns_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias, int M,
+    int N, int K, long long lda, long long ldw, long long ldc, int epi, int tiles_m, int tiles_n, int group_m,
+    const float* rs, const float* cs, float* gnp, int hw) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  mc::Epi e{C, bias, nullptr, ldc, 0, epi, 1.0f, rs, cs};
+  e.gnp = gnp;
+  e.hw = hw;
+  DenseA8 al{A, lda, M, {}};
+  pq::run<DenseA8, LN, 1, 2, false, true, false>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+}
+
+// y = gelu(A W^T + bias) (LN-folded with rs / cs when epi has EPI_LNFOLD) + the sum-of-squares partials:
+// part = [M / 64][N] floats. hw = rows per image, hw % 64 == 0; N % 8 == 0, K % 64 == 0, K >= 128.
+CGS_EXPORT int cgs_gemm_bf16_gelu_gns(const void* A, const void* W, void* C, const void* bias, const float* rs,
+                                      const float* cs, int M, int N, int K, long long lda, long long ldw,
+                                      long long ldc, int epi, float* part, int hw, hipStream_t stream) {
+  if (!part || !bias || hw <= 0 || hw % 64 || M % hw || N % 8 || K % 64 || K < 128 || lda % 8 || ldw % 8 ||
+      ldc % 8 || (epi & ~(EPI_BIAS | EPI_GELU | EPI_LNFOLD)) != 0 || !(epi & EPI_GELU) || !(epi & EPI_BIAS) ||
+      ((epi & EPI_LNFOLD) && (!rs || !cs)) || ((uintptr_t)bias % 8) ||
+      ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C)) % 16) || ((uintptr_t)part % 16))
+    return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const int tiles_n = (N + pq::BN - 1) / pq::BN, tiles_m = (M + pq::BM - 1) / pq::BM;
+  const long long T = (long long)tiles_m * tiles_n;
+  const int grid = (int)(T < num_cus() ? T : num_cus());
+  static bool attr[2] = {false, false};
+  const bool ln = (epi & EPI_LNFOLD) != 0;
+  if (!attr[ln]) {
+    (void)hipFuncSetAttribute(ln ? (const void*)gemm_bf16_nt_v6_gns_kernel<true> : (const void*)gemm_bf16_nt_v6_gns_kernel<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
+    attr[ln] = true;
+  }
+  if (ln)
+    gemm_bf16_nt_v6_gns_kernel<true><<<grid, pq::THREADS, pq::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, M, N, K, lda, ldw, ldc, epi, tiles_m, tiles_n,
+        g_tile_group, rs, cs, part, hw);
+  else
+    gemm_bf16_nt_v6_gns_kernel<false><<<grid, pq::THREADS, pq::LDS, stream>>>(
+        (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, M, N, K, lda, ldw, ldc, epi, tiles_m, tiles_n,
+        g_tile_group, rs, cs, part, hw);
+  return (int)hipGetLastError();
+}
 
 // v6 GEMM (bias / residual epilogue) that also writes per-row LayerNorm statistics partials of its output
 // (pq::run RSO): part = [M][N / 80] (mean, M2) float pairs; cgs_ln_rs_from_partials turns them into the

@@ -302,6 +302,7 @@ __global__ void __launch_bounds__(256) grn2_finalize_kernel(const float* __restr
 // N <= GRN_MAXN images: each block first forms 1 / (mean_C gx + 1e-6) of every image from the
 // finalize block sums (N x C/256 loads), then nx = gx * that inside the element loop.
 #define GRN_MAXN 64
+#define GRN_U 4
 template <int DT, bool GELU>
 __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__ x, const float* __restrict__ gxp,
                                                          const float* __restrict__ bsum, int nblk, int N,
@@ -322,28 +323,41 @@ __global__ void __launch_bounds__(256) grn2_apply_kernel(const u16* __restrict__
   }
   __syncthreads();
   const unsigned cpr = (unsigned)C >> 3;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < chunks; i += (long long)gridDim.x * 256) {
-    // 32-bit index math (chunks < 2^32, checked by the launcher): 64-bit divisions cost ~10x
-    const unsigned iu = (unsigned)i;
-    const unsigned row = iu / cpr;
-    const int c0 = (int)(iu - row * cpr) * 8;
-    const int n = (int)(row / (unsigned)HW);
-    const s16x8 v = reinterpret_cast<const s16x8*>(x)[i];
-    const s16x8 gm = *reinterpret_cast<const s16x8*>(gamma + c0);
-    const s16x8 bt = *reinterpret_cast<const s16x8*>(beta + c0);
-    const float4* np = reinterpret_cast<const float4*>(gxp + (size_t)n * C + c0);
-    const float4 n0 = np[0], n1 = np[1];
-    const float iv = inv_s[n];
-    const float nv[8] = {n0.x * iv, n0.y * iv, n0.z * iv, n0.w * iv, n1.x * iv, n1.y * iv, n1.z * iv, n1.w * iv};
-    s16x8 o;
+  // GRN_U chunks per thread per step, all x loads issued before the math (more bytes in flight per CU:
+  // the one-chunk loop ran at ~3 TB/s on the Stage C tensors)
+  const long long step = (long long)gridDim.x * 256 * GRN_U;
+  for (long long i0 = blockIdx.x * 256LL * GRN_U + threadIdx.x; i0 < chunks; i0 += step) {
+    s16x8 v[GRN_U];
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      f32x2_t f = {cvt_in<DT>((u16)v[j]), cvt_in<DT>((u16)v[j + 1])};
-      if (GELU) f = gelu_sig2(f);
-      o[j] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j]) + f.x * (1.f + cvt_in<DT>((u16)gm[j]) * nv[j]));
-      o[j + 1] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j + 1]) + f.y * (1.f + cvt_in<DT>((u16)gm[j + 1]) * nv[j + 1]));
+    for (int u = 0; u < GRN_U; ++u) {
+      const long long i = i0 + 256LL * u;
+      v[u] = i < chunks ? reinterpret_cast<const s16x8*>(x)[i] : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
-    reinterpret_cast<s16x8*>(y)[i] = o;
+#pragma unroll
+    for (int u = 0; u < GRN_U; ++u) {
+      const long long i = i0 + 256LL * u;
+      if (i >= chunks) break;
+      // 32-bit index math (chunks < 2^32, checked by the launcher): 64-bit divisions cost ~10x
+      const unsigned iu = (unsigned)i;
+      const unsigned row = iu / cpr;
+      const int c0 = (int)(iu - row * cpr) * 8;
+      const int n = (int)(row / (unsigned)HW);
+      const s16x8 gm = *reinterpret_cast<const s16x8*>(gamma + c0);
+      const s16x8 bt = *reinterpret_cast<const s16x8*>(beta + c0);
+      const float4* np = reinterpret_cast<const float4*>(gxp + (size_t)n * C + c0);
+      const float4 n0 = np[0], n1 = np[1];
+      const float iv = inv_s[n];
+      const float nv[8] = {n0.x * iv, n0.y * iv, n0.z * iv, n0.w * iv, n1.x * iv, n1.y * iv, n1.z * iv, n1.w * iv};
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        f32x2_t f = {cvt_in<DT>((u16)v[u][j]), cvt_in<DT>((u16)v[u][j + 1])};
+        if (GELU) f = gelu_sig2(f);
+        o[j] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j]) + f.x * (1.f + cvt_in<DT>((u16)gm[j]) * nv[j]));
+        o[j + 1] = (short)cvt_out<DT>(cvt_in<DT>((u16)bt[j + 1]) + f.y * (1.f + cvt_in<DT>((u16)gm[j + 1]) * nv[j + 1]));
+      }
+      reinterpret_cast<s16x8*>(y)[i] = o;
+    }
   }
 }
 
@@ -867,7 +881,7 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
   dim3 g1((unsigned)((C / 8 + 63) / 64), (unsigned)S, (unsigned)N);
   const long long chunks = (long long)N * HW * (C / 8);
   if (chunks >= (1LL << 32)) return (int)hipErrorInvalidValue;
-  long long nb = (chunks + 255) / 256;
+  long long nb = (chunks + 256 * GRN_U - 1) / (256 * GRN_U);
   const int blocks = (int)(nb > 16384 ? 16384 : nb);
 #define CGS_GRN2(DTV, GV)                                                                                        \
   grn2_sumsq_kernel<DTV, GV><<<g1, 256, 0, stream>>>((const u16*)x, part, HW, C, rows_per, S);                  \
@@ -880,6 +894,68 @@ CGS_EXPORT int cgs_grn_nhwc_v2(const void* x, const void* gamma, const void* bet
     if (pre_gelu) { CGS_GRN2(CGS_F16, true); } else { CGS_GRN2(CGS_F16, false); }
   }
 #undef CGS_GRN2
+  return (int)hipGetLastError();
+}
+
+// GRN pass 2 from the producing GEMM's partials (cgs_gemm_bf16_gelu_gns: part [N][HW / 64][C], the sum of
+// squares over each 64-row block): sum_HW h^2 = their sum; then gx / bsum as grn2_finalize_kernel.
+__global__ void __launch_bounds__(256) grn_gns_finalize_kernel(const float* __restrict__ part, float* __restrict__ gx,
+                                                               float* __restrict__ bsum, int C, int nbk) {
+  __shared__ float red[4];
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  float g = 0.f;
+  if (c < C) {
+    const float* p = part + (size_t)n * nbk * C + c;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // four loads in flight per step
+    int b = 0;
+    for (; b + 4 <= nbk; b += 4) {
+      s0 += p[(size_t)b * C];
+      s1 += p[(size_t)(b + 1) * C];
+      s2 += p[(size_t)(b + 2) * C];
+      s3 += p[(size_t)(b + 3) * C];
+    }
+    for (; b < nbk; ++b) s0 += p[(size_t)b * C];
+    g = sqrtf((s0 + s1) + (s2 + s3));
+    gx[(size_t)n * C + c] = g;
+  }
+  g = wave_sum(g);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[(size_t)n * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// GRN apply with the statistics from GNS partials: y = beta + h * (1 + gamma * nx). ws >= N * (C + ceil(C / 256))
+// floats. h bf16 [N, HW, C] (already GELU'd), HW % 64 == 0, C % 8 == 0, N <= 64.
+CGS_EXPORT int cgs_grn_apply_gns(const void* h, const float* part, const void* gamma, const void* beta, void* y,
+                                 float* ws, int N, int HW, int C, hipStream_t stream) {
+  if (N <= 0 || HW <= 0) return 0;
+  if (C % 8 || HW % 64 || N > GRN_MAXN || (((uintptr_t)h | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) ||
+      ((uintptr_t)part & 3))
+    return (int)hipErrorInvalidValue;
+  const int nblk = (C + 255) / 256;
+  float* gx = ws;
+  float* bsum = ws + (size_t)N * C;
+  grn_gns_finalize_kernel<<<dim3((unsigned)nblk, (unsigned)N), 256, 0, stream>>>(part, gx, bsum, C, HW / 64);
+  const long long chunks = (long long)N * HW * (C / 8);
+  if (chunks >= (1LL << 32)) return (int)hipErrorInvalidValue;
+  const long long nb = (chunks + 256 * GRN_U - 1) / (256 * GRN_U);
+  const int blocks = (int)(nb > 16384 ? 16384 : nb);
+  grn2_apply_kernel<CGS_BF16, false><<<blocks, 256, 0, stream>>>((const u16*)h, gx, bsum, nblk, N, (const u16*)gamma,
+                                                                 (const u16*)beta, (u16*)y, chunks, HW, C);
+  return (int)hipGetLastError();
+}
+
+// cgs_grn_stats from GNS partials instead of a pass over h: gx / bsum land where cgs_grn_stats puts them
+// (ws + N * S * C, S = cgs_grn_slices), so cgs_grn_scale_weight reads them unchanged. HW % 64 == 0.
+CGS_EXPORT int cgs_grn_stats_gns(const float* part, float* ws, int N, int HW, int C, hipStream_t stream) {
+  if (N <= 0 || HW <= 0) return 0;
+  if (C % 8 || HW % 64 || N > GRN_MAXN || ((uintptr_t)part & 3)) return (int)hipErrorInvalidValue;
+  const int S = cgs_grn_slices(N, HW, C);
+  float* gx = ws + (size_t)N * S * C;
+  const int nblk = (C + 255) / 256;
+  grn_gns_finalize_kernel<<<dim3((unsigned)nblk, (unsigned)N), 256, 0, stream>>>(part, gx, gx + (size_t)N * C, C,
+                                                                                 HW / 64);
   return (int)hipGetLastError();
 }
 

@@ -26,6 +26,8 @@ typedef __attribute__((address_space(3))) void mc_lds_void;
 #define MC_EPI_LNFOLD 8   // y = rstd_r * (acc - mean_r * cs[c]) + bias[c]  (LayerNorm folded into the GEMM)
 #define MC_EPI_F32OUT 16  // v7 only: C is fp32 (ldc in floats), no GEGLU / residual (attention scores, K22)
 #define MC_EPI_GELU 32    // GELU(acc * alpha + bias) before the residual (mc::tile, pq::run ACT, skinny; no GEGLU)
+#define MC_EPI_F32RAW 64  // mc::tile only: the raw fp32 accumulators to (float*)C (ldc in floats), no other epilogue
+                          // (split-K partial products, reduced + epilogued by cgs_gemm_bf16_splitk's second pass)
 
 namespace mc {
 
@@ -224,6 +226,22 @@ __device__ __forceinline__ void tile(AL& al, const u16* __restrict__ W, long lon
   // stored at ch ^ (r & (CPR - 1)) so the column-wise fragment writes and row-wise reads are
   // conflict-free without padding (the 4 regions fill exactly the 4-stage ring).
   wait_vmcnt<0>();   // the clamped tail DMAs target slots the epilogue reuses
+  if (e.flags & MC_EPI_F32RAW) {   // split-K partials: straight from the registers, 32 lanes = 128-B runs
+    float* Cf = reinterpret_cast<float*>(e.C);
+    const int erow0 = 4 * (lane >> 5);
+#pragma unroll
+    for (int j = 0; j < C::NJ; ++j) {
+      const int col = n0 + wn + 32 * j + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + erow0;
+          if (row < M && col < N) Cf[(long long)row * e.ldc + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   __syncthreads();   // other waves may still be reading the last stage
   const bool geglu = (e.flags & MC_EPI_GEGLU) != 0;
   const int OW = geglu ? C::WN / 2 : C::WN;

@@ -66,7 +66,9 @@ __device__ __forceinline__ int gg_row160(int r) {
 // GNS: the epilogue also writes GroupNorm partial statistics of the stored (bf16) outputs -- per image,
 // 64-row block (one wave's rows) and column, (mean, M2) by an exact two-pass over the wave's registers
 // (DPP row sums) -- into e.gnp in the gn_partial layout with 64 pixels per block, so the next GroupNorm
-// skips its statistics pass over the tensor (host: rows per image % 256 == 0).
+// skips its statistics pass over the tensor (host: rows per image % 256 == 0). GNS == 2: the sum of squares
+// only (one float per image, 64-row block and column: Cascade's GlobalResponseNorm needs sum_HW h^2, and the
+// one-pass form skips the mean pass and half the DPP reductions).
 // GG: GEGLU epilogue (out = a * gelu(g), N / 2 output columns) from the 16-row-interleaved weights of the
 // 256-wide kernels ([a0..a15, g0..g15, ...], geglu_interleave): the B staging puts, in every 16-column MFMA
 // tile, 8 'a' rows in lanes fq = 0, 1 and their 8 'g' rows in fq = 2, 3, so one v_permlane32_swap of row
@@ -78,7 +80,7 @@ __device__ __forceinline__ int gg_row160(int r) {
 // and 80-column chunk (one wave's columns), (mean, M2) shifted by the row's first value in the chunk -- into
 // e.gnp as [M][N / 80][2] floats; a LayerNorm over these rows then needs only cgs_ln_rs_from_partials
 // instead of a statistics pass over the tensor. Host: N % 160 == 0.
-template <class AL, bool LN = false, int DS = 0, bool GNS = false, bool GG = false, bool ACT = false,
+template <class AL, bool LN = false, int DS = 0, int GNS = 0, bool GG = false, bool ACT = false,
           bool RSO = false>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
@@ -332,8 +334,25 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
 #pragma unroll
       for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
+      if (m_w >= M) return;       // a partial last tile (GEMM rows: M % 256 != 0) -- no block past the tensor
       const int img = m_w / e.hw;
       const int nbk = e.hw >> 6;
+      if constexpr (GNS == 2) {
+        float* dq = e.gnp + (size_t)(img * nbk + ((m_w - img * e.hw) >> 6)) * N;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          float4 q = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 u = unpack4_bf16(pk[i][j]);
+            q.x += u.x * u.x; q.y += u.y * u.y; q.z += u.z * u.z; q.w += u.w * u.w;
+          }
+          q = float4{row16_sum(q.x), row16_sum(q.y), row16_sum(q.z), row16_sum(q.w)};
+          const int col = n_w + colj(j);
+          if (fr == 0 && col < N) *reinterpret_cast<float4*>(dq + col) = q;
+        }
+        return;
+      }
       float* dst = e.gnp + (size_t)(img * nbk + ((m_w - img * e.hw) >> 6)) * N * 2;
 #pragma unroll
       for (int j = 0; j < 5; ++j) {

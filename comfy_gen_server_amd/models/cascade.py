@@ -145,7 +145,8 @@ class _ChannelMLP(nn.Sequential):
             _cast(lin1.weight, x), _cast(lin1.bias, x), None, None))
         if rs is None:
             rs = ops.layernorm_stats(x, eps)
-        h = ops.linear_lnfold(x, rs, w2, cs, b2, act="gelu")
+        # the GEMM epilogue also leaves the GRN statistics partials of h (per image of H * W rows)
+        h = ops.linear_lnfold(x, rs, w2, cs, b2, act="gelu", gns_hw=x.shape[1] * x.shape[2])
         return self._grn_linear2(h, x, residual)
 
     def _grn_linear2(self, h, x, residual):

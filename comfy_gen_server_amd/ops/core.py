@@ -138,6 +138,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
 
         def run_hip(variant, final=False):
             o = dst if dst is not None else torch.empty((M, N), device=x.device, dtype=x.dtype)
+            if isinstance(variant, str):                       # split-K (batch-1 grids)
+                return _splitk_run(a, w, o, bias, r, None, None, M, N, K, epi, variant)
             if (final and row_stats and variant == 6 and not gelu and N % 160 == 0 and K % 64 == 0 and K >= 128
                     and _RSO and _native.has_kernel("cgs_gemm_bf16_rowstats")):
                 part = torch.empty((M, N // 80, 2), device=x.device, dtype=torch.float32)
@@ -186,6 +188,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
                 cands.append(("v8", lambda: run_hip(8)))      # 128 x 128 tiles (short M / N grids)
                 if _underfilled(M, N):    # 64x128 / 128x64 tiles, 4- and 6-stage rings (batch-1 grids)
                     cands += [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
+                    if (a.stride(0) % 8 == 0 and (bias is None or bias.data_ptr() % 16 == 0)
+                            and (r is None or r.data_ptr() % 16 == 0)):
+                        cands += _splitk_cands(M, N, K, epi, run_hip)
             cands.append(("hip", lambda: run_hip(-1)))
             if _LIB_GEMM and not gelu and dst is None:     # vendor GEMM only as an explicit opt-in
                 cands.append(("lib", run_lib))
@@ -196,8 +201,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             count("gemm", "lib")     # explicit opt-in (CGS_GEMM_LIB=1)
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
-        variant = {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, "w6": W6, "w6n160": W6_160,
-                   **_SMALL_NAMES}.get(choice, -2)
+        variant = choice if choice in _SPLITK else {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, "w6": W6,
+                                                    "w6n160": W6_160, **_SMALL_NAMES}.get(choice, -2)
         y = run_hip(variant, final=True).view(*x.shape[:-1], N)
         if rs_part:
             # (no version counter: inference-mode tensors have none; the consumers take the partials only
@@ -1311,12 +1316,34 @@ def lnfold_weights(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch
     return w2, cs, b.to(torch.bfloat16).contiguous()
 
 
+_GRN_GNS = os.environ.get("CGS_GRN_GNS", "1") != "0"
+
+
+def _gelu_gns_ok(M, N, K, hw) -> bool:
+    return (_GRN_GNS and os.environ.get("CGS_GRN_GNS", "1") != "0" and hw is not None and hw > 0 and hw % 64 == 0 and M % hw == 0 and M // hw <= 64
+            and N % 8 == 0 and K % 64 == 0 and K >= 128 and _native.has_kernel("cgs_gemm_bf16_gelu_gns"))
+
+
+def _gelu_gns(a, w, b, rs, cs, M, N, K, epi, hw, device, dtype):
+    """The v6 GELU (+ LN-fold) GEMM whose epilogue also writes per-(image, 64-row block, column) sums of squares
+    partials of its output (returned with it; the caller attaches them to its final view as
+    ``y._cgs_grnpart``): the GlobalResponseNorm over y (``grn_nhwc`` / ``grn_fold_weight``) then takes its
+    statistics from them instead of a pass over y."""
+    out = torch.empty((M, N), device=device, dtype=dtype)
+    part = torch.empty((M // 64) * N, device=device, dtype=torch.float32)
+    _check(_lib().cgs_gemm_bf16_gelu_gns(a.data_ptr(), w.data_ptr(), out.data_ptr(), b.data_ptr(), _ptr(rs), _ptr(cs),
+                                         M, N, K, a.stride(0), K, N, epi, part.data_ptr(), hw, _stream()),
+           "cgs_gemm_bf16_gelu_gns")
+    return out, part
+
+
 def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch.Tensor, b2: torch.Tensor,
-                  geglu: bool = False, act: str | None = None) -> torch.Tensor:
+                  geglu: bool = False, act: str | None = None, gns_hw: int | None = None) -> torch.Tensor:
     """``LN(x) @ W^T + b`` (or the GEGLU of it, with interleaved W' rows) from the raw rows ``x``, the
     row statistics ``rs`` and ``lnfold_weights`` -- the LayerNorm never materialises (K07 folded
     into the GEMM epilogue of the v7 kernel). ``act="gelu"``: GELU of it (Cascade's LayerNorm ->
-    ChannelMLP Linear -> GELU), on the v6 ACT / mc::tile kernels."""
+    ChannelMLP Linear -> GELU), on the v6 ACT / mc::tile kernels. ``gns_hw`` (rows per image): when the
+    v6 kernel runs, its epilogue also leaves the GRN statistics partials of the output (``_gelu_gns``)."""
     K = x.shape[-1]
     a = x.reshape(-1, K)
     if not a.is_contiguous():
@@ -1339,10 +1366,17 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
         if _underfilled(M, N):
             cands += [(f"v{v}", (lambda v=v: run_g(v))) for v in _SMALL_TILE]
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands, default="v6" if N % 160 == 0 else "v8")
+        if choice == "v6" and _gelu_gns_ok(M, N, K, gns_hw):
+            y, part = _gelu_gns(a, w2, b2, rs, cs, M, N, K, epi | EPI_LNFOLD, gns_hw, x.device, x.dtype)
+            y = y.view(*x.shape[:-1], N)
+            y._cgs_grnpart = (part, y.data_ptr(), gns_hw)
+            return y
         return run_g({"v6": 6, "v8": 8, **_SMALL_NAMES}.get(choice, -1)).view(*x.shape[:-1], N)
 
     def run(variant):
         out = torch.empty((M, nout), device=x.device, dtype=x.dtype)
+        if isinstance(variant, str):                           # split-K (batch-1 grids)
+            return _splitk_run(a, w2, out, b2, None, rs, cs, M, N, K, epi | EPI_LNFOLD, variant)
         ws = _v7_ws(M, N, K, x.device) if variant in (-1, 7) else None
         _check(_lib().cgs_gemm_bf16_lnfold_v(a.data_ptr(), w2.data_ptr(), out.data_ptr(), b2.data_ptr(), rs.data_ptr(),
                                              cs.data_ptr(), M, N, K, K, K, nout, epi, _ptr(ws),
@@ -1356,8 +1390,11 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
         cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
         if N % 160 == 0:    # 256x160 tiles (plain or GEGLU): whole rounds where 256x256 leaves a partial one
             cands.append(("v6", lambda: run(6)))
+        if not geglu:
+            cands += _splitk_cands(M, N, K, epi | EPI_LNFOLD, run)
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands + w6, default="v7")
-        variant = {"v8": 8, "v6": 6, "w6": W6, "w6n160": W6_160, **_SMALL_NAMES}.get(choice, -1)
+        variant = choice if choice in _SPLITK else {"v8": 8, "v6": 6, "w6": W6, "w6n160": W6_160,
+                                                    **_SMALL_NAMES}.get(choice, -1)
     elif geglu and N % 160 == 0 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi),
                                  [("v7", lambda: run(7)), ("v6", lambda: run(6))] + w6, default="v7")
@@ -1400,6 +1437,31 @@ _CUS: list = []
 # 12 / 13 = the same with 6 stages, 14 = 128x128 with 5 stages
 _SMALL_TILE = (10, 11, 12, 13, 14)
 _SMALL_NAMES = {f"v{v}": v for v in _SMALL_TILE}
+# split-K forms of the v8 family (cgs_gemm_bf16_splitk): autotune name -> (tile variant, slices)
+_SPLITK = {"sk2v8": (8, 2), "sk4v8": (8, 4), "sk2v10": (10, 2), "sk4v10": (10, 4), "sk2v11": (11, 2),
+           "sk4v11": (11, 4), "sk8v8": (8, 8)}
+
+
+def _splitk_cands(M, N, K, epi, run):
+    """Split-K autotune candidates for an under-filled grid (batch-1 shapes: a 128 x 128 grid under two
+    workgroups per CU): the K slices multiply the workgroup count, one reduce pass applies the epilogue.
+    Opt-in (CGS_SPLITK=1): measured slower than the best single-pass tile on every SDXL batch-1 shape
+    (profiles/r05/splitk.md -- the fp32 partial round trip costs more than the fuller grid gains)."""
+    if (epi & ~(EPI_BIAS | EPI_RESIDUAL | EPI_LNFOLD | EPI_GELU)) or N % 8 or not _underfilled(M, N) \
+            or not _native.has_kernel("cgs_gemm_bf16_splitk") or os.environ.get("CGS_SPLITK", "0") != "1":
+        return []
+    return [(name, (lambda name=name: run(name))) for name, (_, s) in _SPLITK.items()
+            if K % (32 * s) == 0 and K // s >= 256]
+
+
+def _splitk_run(a, w, o, bias, r, rs, cs, M, N, K, epi, name):
+    variant, s = _SPLITK[name]
+    ws = torch.empty(s * M * N, device=a.device, dtype=torch.float32)
+    _check(_lib().cgs_gemm_bf16_splitk(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r), _ptr(rs),
+                                       _ptr(cs), M, N, K, a.stride(0), w.stride(0), N, N if r is not None else 0,
+                                       epi, 1.0, s, variant, ws.data_ptr(), ws.numel() * 4, _stream()),
+           "cgs_gemm_bf16_splitk")
+    return o
 
 
 def _num_cus() -> int:
@@ -1587,6 +1649,16 @@ def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, pre_gelu:
     Linear -> GELU -> GRN of Cascade's ChannelMLP: the GELU is fused into both reads of x)."""
     N, H, W, C = x.shape
     be = backend_for("grn", x, "cgs_grn_nhwc")
+    gp = _grn_part(x, N, H * W, C) if not pre_gelu and be == "hip" else None
+    if gp is not None:        # statistics from the producing GEMM's epilogue (linear_lnfold gns_hw)
+        count("grn", "hip")
+        y = torch.empty_like(x)
+        ws = torch.empty(N * (C + (C + 255) // 256), device=x.device, dtype=torch.float32)
+        g = gamma.to(x.dtype).reshape(-1).contiguous()
+        b = beta.to(x.dtype).reshape(-1).contiguous()
+        _check(_lib().cgs_grn_apply_gns(x.data_ptr(), gp.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                        ws.data_ptr(), N, H * W, C, _stream()), "cgs_grn_apply_gns")
+        return y
     if be == "hip" and x.dtype in (torch.bfloat16, torch.float16) and C % 8 == 0 and N <= 64 and \
             _native.has_kernel("cgs_grn_nhwc_v2"):
         count("grn", "hip")
@@ -1616,6 +1688,15 @@ def grn_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, pre_gelu:
     return torch.addcmul(beta.to(x.dtype).reshape(1, 1, 1, C), x, scale)
 
 
+def _grn_part(x, N, HW, C):
+    """The GNS partials attached by ``_gelu_gns`` when they describe exactly this tensor, else None."""
+    h = getattr(x, "_cgs_grnpart", None)
+    if (h is None or h[1] != x.data_ptr() or h[2] != HW or not x.is_contiguous() or x.dtype != torch.bfloat16
+            or h[0].numel() != N * (HW // 64) * C or N > 64 or C % 8):
+        return None
+    return h[0]
+
+
 def grn_fold_weight(h: torch.Tensor, weight: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
     """The GlobalResponseNorm over ``h`` [N, H, W, K] (already GELU'd) folded into the next Linear's
     weight [O, K]: returns per-image weights Wn [N, O, K] = W * (1 + gamma * nx_n), nx_n =
@@ -1631,8 +1712,12 @@ def grn_fold_weight(h: torch.Tensor, weight: torch.Tensor, gamma: torch.Tensor) 
         hc = h.contiguous()
         S = int(_lib().cgs_grn_slices(N, H * W_, K))
         ws = torch.empty(N * ((S + 1) * K + (K + 255) // 256), device=h.device, dtype=torch.float32)
-        _check(_lib().cgs_grn_stats(hc.data_ptr(), ws.data_ptr(), N, H * W_, K, 0, _DT[h.dtype], _stream()),
-               "cgs_grn_stats")
+        gp = _grn_part(h, N, H * W_, K)
+        if gp is not None:      # statistics from the producing GEMM's epilogue (linear_lnfold gns_hw)
+            _check(_lib().cgs_grn_stats_gns(gp.data_ptr(), ws.data_ptr(), N, H * W_, K, _stream()), "cgs_grn_stats_gns")
+        else:
+            _check(_lib().cgs_grn_stats(hc.data_ptr(), ws.data_ptr(), N, H * W_, K, 0, _DT[h.dtype], _stream()),
+                   "cgs_grn_stats")
         wc = weight.contiguous()
         g = gamma.to(h.dtype).reshape(-1).contiguous()
         out = torch.empty((N, O, K), device=h.device, dtype=h.dtype)

@@ -1135,6 +1135,45 @@ def test_cascade_resblock_lnfold(cuda, N, H, W, c, monkeypatch):
         assert _rel(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W,c", [(2, 8, 8, 320), (2, 24, 24, 320), (3, 16, 8, 640)])
+def test_cascade_grn_stats_from_gemm_epilogue(cuda, N, H, W, c, monkeypatch):
+    """The GELU GEMM's epilogue writes per-(image, 64-row block, column) (mean, M2) partials and the GRN (pass
+    over h, or the weight fold) takes sum_HW h^2 from them instead of its statistics pass: same output as
+    with the pass (CGS_GRN_GNS off) and as the fp32 CPU block."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    from comfy_gen_server_amd.ops import core as C
+    for k in ("GELU_EPI", "LNFOLD", "GRNFOLD", "DWLN"):
+        monkeypatch.setenv(f"CGS_CASCADE_{k}", "1")
+    used = []
+    real = C._grn_part
+
+    def spy(*a):
+        r = real(*a)
+        used.append(r is not None)
+        return r
+    monkeypatch.setattr(C, "_grn_part", spy)
+    torch.manual_seed(8)
+    blk = SC.ResBlock(c)
+    init_random_(blk, seed=5)
+    with torch.no_grad():
+        blk.channelwise[2].gamma.normal_(0, 0.5)
+        blk.channelwise[2].beta.normal_(0, 0.5)
+    x = torch.randn(N, H, W, c)
+    with torch.no_grad():
+        ref = blk(x)
+        g = blk.to(device=cuda, dtype=torch.bfloat16)
+        xd = x.to(cuda, torch.bfloat16)
+        y = g(xd).float().cpu()
+        assert used and all(used), used
+        monkeypatch.setattr(C, "_GRN_GNS", False)
+        used.clear()
+        y0 = g(xd).float().cpu()
+        assert not any(used)
+    assert _rel(y, ref) < 2e-2
+    assert _rel(y, y0) < 5e-3
+
+
 @pytest.mark.parametrize("N,H,W,C,k,rep", [(2, 24, 24, 2048, 3, False), (1, 17, 9, 320, 3, False),
                                            (2, 8, 8, 1280, 7, True), (1, 5, 6, 64, 3, False)])
 def test_dwconv_ln_stats(cuda, N, H, W, C, k, rep):
@@ -1306,3 +1345,50 @@ def test_row_sharded_groupnorm_native(cuda, C, C2, G, silu, pre):
         bands.append(yb)
     y = torch.cat(bands, dim=2)
     assert _rel(y, ref) < 1e-2, _rel(y, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 1280, 5120), (2048, 1280, 1280), (1000, 640, 2560), (333, 320, 1024)])
+@pytest.mark.parametrize("epi", ["bias_res", "bias", "gelu", "ln"])
+@pytest.mark.parametrize("name", ["sk2v8", "sk4v10", "sk2v11"])
+def test_gemm_splitk(cuda, M, N, K, epi, name):
+    """Split-K GEMM (K slices into fp32 partials, one reduce pass with the epilogue) vs fp32 torch."""
+    if epi == "ln" and K > 2048:
+        pytest.skip("LayerNorm statistics kernel: C <= 2048 (the LN-folded GEMMs have K <= 2048)")
+    torch.manual_seed(11)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16)
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi == "bias_res" else None
+    o = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    if epi == "ln":
+        rs = core.layernorm_stats(x, 1e-5)
+        w2, cs, b2 = core.lnfold_weights(w, b, None, None)
+        core._splitk_run(x, w2, o, b2, None, rs, cs, M, N, K, core.EPI_BIAS | core.EPI_LNFOLD, name)
+        ref = F.linear(F.layer_norm(x.float(), (K,), eps=1e-5), w.float(), b.float())
+    else:
+        e = core.EPI_BIAS | (core.EPI_RESIDUAL if r is not None else 0) | (core.EPI_GELU if epi == "gelu" else 0)
+        core._splitk_run(x, w, o, b, r, None, None, M, N, K, e, name)
+        ref = F.linear(x.float(), w.float(), b.float())
+        if epi == "gelu":
+            ref = F.gelu(ref)
+        if r is not None:
+            ref = ref + r.float()
+    assert _rel(o, ref) < 1e-2
+
+
+def test_gemm_splitk_is_a_linear_candidate(cuda, monkeypatch):
+    """ops.linear on a batch-1 shape runs the split-K form when the tuning override picks it."""
+    monkeypatch.setenv("CGS_AUTOTUNE", "1")
+    monkeypatch.setenv("CGS_SPLITK", "1")                      # opt-in candidates (profiles/r05/splitk.md)
+    monkeypatch.setenv("CGS_TUNE_OVERRIDE", '{"gemm|2048|1280|5120|3": "sk4v8"}')
+    torch.manual_seed(12)
+    x = torch.randn(2048, 5120, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(1280, 5120, device=cuda) / 64).to(torch.bfloat16)
+    b = torch.randn(1280, device=cuda).to(torch.bfloat16)
+    r = torch.randn(2048, 1280, device=cuda).to(torch.bfloat16)
+    calls = []
+    real = core._splitk_run
+    monkeypatch.setattr(core, "_splitk_run", lambda *a: calls.append(a[-1]) or real(*a))
+    y = ops.linear(x, w, b, residual=r)
+    assert calls == ["sk4v8"]
+    assert _rel(y, F.linear(x.float(), w.float(), b.float()) + r.float()) < 1e-2
