@@ -92,7 +92,7 @@ def main():
     assert comm.world == args.gpus, f"communicator has {comm.world} ranks, --gpus {args.gpus}"
     from comfy_gen_server_amd.runtime import device as dm
     if not args.cpu:
-        dm.set_device_index(comm.local_rank)
+        dm.set_device_index(comm.device.index if comm.device.type == "cuda" else comm.local_rank)
     from comfy_gen_server_amd.tools.synth import build_pipeline
     from comfy_gen_server_amd.parallel.dp import DataParallelGenerator, Job
     from comfy_gen_server_amd import ops

@@ -94,7 +94,14 @@ class Comm:
                     continue
                 if bucket:
                     flat = torch.cat([b.reshape(-1) for b in bucket])
-                    dist.broadcast(flat, src=src, group=self.group)
+                    if flat.is_cuda and self.backend == "gloo":     # shared-GPU rehearsal: via host memory
+                        h = flat.cpu()
+                        if h.dtype in (torch.bfloat16, torch.float16):
+                            h = h.float()                         # exact; Gloo lacks 16-bit types
+                        dist.broadcast(h, src=src, group=self.group)
+                        flat.copy_(h)
+                    else:
+                        dist.broadcast(flat, src=src, group=self.group)
                     off = 0
                     for b in bucket:
                         n = b.numel()
@@ -338,6 +345,13 @@ def init_from_env(backend=None, timeout_s=600, join=True) -> Comm:
     c.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     c.world = world
     use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if os.environ.get("CGS_SHARED_GPU") == "1" and torch.cuda.is_available():
+        # rehearsal: every rank on the SAME card over Gloo (the 1-GPU development box); device tensors in
+        # the model-parallel collectives are staged through host memory (parallel/coll.py)
+        backend, use_gpu = "gloo", False
+        dev = c.local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(dev)
+        c.device = torch.device("cuda", dev)
     if use_gpu:
         torch.cuda.set_device(c.local_rank)
         c.device = torch.device("cuda", c.local_rank)

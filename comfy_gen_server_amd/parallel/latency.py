@@ -31,7 +31,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import spatial
+from . import coll, spatial
 from .sp import SeqParallel
 
 
@@ -135,7 +135,7 @@ class LatencyParallel:
         else:
             out = apply_model(x[lo:hi], t[lo:hi], **cs)
         parts = [torch.empty_like(out) for _ in range(self.G)]
-        dist.all_gather(parts, out.contiguous(), group=self.cross_group)
+        coll.all_gather(parts, out.contiguous(), group=self.cross_group)
         return torch.cat(parts, 0)
 
     def patch(self, patcher):

@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from . import coll
 
 
 def _world(group):
@@ -35,7 +36,7 @@ def _all_to_all(chunks, group):
     One ``all_to_all_single`` over the stacked chunks (supported by RCCL and Gloo alike)."""
     inp = torch.stack(chunks).contiguous()
     out = torch.empty_like(inp)
-    dist.all_to_all_single(out, inp, group=group)
+    coll.all_to_all_single(out, inp, group=group)
     return list(out.unbind(0))
 
 
@@ -82,8 +83,7 @@ def ring_attention(q, k, v, heads: int, group=None):
         reqs = []
         if step < P - 1:                                    # overlap: ship the block while computing on it
             recv = torch.empty_like(kv)
-            reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, kv, nxt, group),
-                                           dist.P2POp(dist.irecv, recv, prv, group)])
+            reqs = coll.exchange([(kv, nxt)], [(recv, prv)], group)
         o, lse = _partial_attention(q, kv[..., :HD], kv[..., HD:], heads)
         if o_acc is None:
             o_acc, lse_acc = o, lse
@@ -111,7 +111,7 @@ def gather_sequence(x, group=None, dim=1):
     if P == 1:
         return x
     parts = [torch.empty_like(x) for _ in range(P)]
-    dist.all_gather(parts, x.contiguous(), group=group)
+    coll.all_gather(parts, x.contiguous(), group=group)
     return torch.cat(parts, dim=dim)
 
 

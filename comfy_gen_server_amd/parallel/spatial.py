@@ -30,7 +30,8 @@ from __future__ import annotations
 import contextvars
 
 import torch
-import torch.distributed as dist
+
+from . import coll
 
 _CTX: contextvars.ContextVar = contextvars.ContextVar("cgs_spatial", default=None)
 
@@ -54,7 +55,7 @@ class SpatialShard:
             return t
         t = t.contiguous()
         parts = [torch.empty_like(t) for _ in range(self.P)]
-        dist.all_gather(parts, t, group=self.group)
+        coll.all_gather(parts, t, group=self.group)
         return torch.cat(parts, dim=dim)
 
     def halo(self, x, top: int, bottom: int):
@@ -69,7 +70,7 @@ class SpatialShard:
         ext = torch.empty((N, C, top + R + bottom, W), dtype=x.dtype, device=x.device,
                           memory_format=torch.channels_last if cl else torch.contiguous_format)
         ext[:, :, top:top + R] = x
-        ops, fix = [], []
+        sends, recvs, fix = [], [], []
 
         fmt = torch.channels_last if cl else torch.contiguous_format
 
@@ -81,26 +82,25 @@ class SpatialShard:
         if top:
             if above >= 0:
                 buf, dst = slot(0, top)
-                ops.append(dist.P2POp(dist.irecv, buf, self.ranks[above], self.group))
+                recvs.append((buf, self.ranks[above]))
                 if dst is not None:
                     fix.append((dst, buf))
             else:
                 ext[:, :, :top].zero_()
             if below < self.P:    # my last `top` rows are the lower neighbour's top halo
-                ops.append(dist.P2POp(dist.isend, x[:, :, R - top:].contiguous(), self.ranks[below], self.group))
+                sends.append((x[:, :, R - top:].contiguous(), self.ranks[below]))
         if bottom:
             if below < self.P:
                 buf, dst = slot(top + R, bottom)
-                ops.append(dist.P2POp(dist.irecv, buf, self.ranks[below], self.group))
+                recvs.append((buf, self.ranks[below]))
                 if dst is not None:
                     fix.append((dst, buf))
             else:
                 ext[:, :, top + R:].zero_()
             if above >= 0:        # my first `bottom` rows are the upper neighbour's bottom halo
-                ops.append(dist.P2POp(dist.isend, x[:, :, :bottom].contiguous(), self.ranks[above], self.group))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+                sends.append((x[:, :, :bottom].contiguous(), self.ranks[above]))
+        for req in coll.exchange(sends, recvs, self.group):
+            req.wait()
         for dst, buf in fix:
             dst.copy_(buf)
         return ext
@@ -131,7 +131,7 @@ class SpatialShard:
         if self.P == 1:
             return st[None]
         parts = [torch.empty_like(st) for _ in range(self.P)]
-        dist.all_gather(parts, st.contiguous(), group=self.group)
+        coll.all_gather(parts, st.contiguous(), group=self.group)
         return torch.stack(parts)
 
     def group_norm(self, x, groups, weight, bias, eps, silu=False, pre_add=None, x2=None):
