@@ -301,6 +301,12 @@ __device__ __forceinline__ void run(const u16* __restrict__ A, long long lda, co
   // wait for the next unit's in-flight DMAs). LN fold per element: v = acc * (alpha rstd) + (b - alpha
   // mean rstd cs) -- two FMAs.
   auto epilogue = [&]() {
+    // lane-dependent indices re-derived here, opaque to the compiler: copies hoisted out of the K loop (all
+    // 256 VGPRs taken) were spilled, and the scratch reload at the epilogue's start waited vmcnt(0) -- for
+    // the next unit's in-flight DMAs as well
+    int lane_e;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+    const int fr = lane_e & 15, fq = lane_e >> 4;
     const long long ld16 = 16 * e.ldc;
     float2 st[8];
 #pragma unroll
