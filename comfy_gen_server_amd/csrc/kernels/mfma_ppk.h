@@ -231,6 +231,12 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   // acc[.][nq*2+j][t] is column n0 + wc*64 + nq*32 + 8fq + 4j + t (GEGLU: see b_col_perm).
   auto epilogue_t = [&](int m0, int n0, auto hb_c, auto hr_c) {
     constexpr bool HB = decltype(hb_c)::value, HR = decltype(hr_c)::value;
+    // lane-dependent indices re-derived here, opaque to the compiler (as in gemm_w6.hip): hoisted copies
+    // live across the K loop were spilled, and a scratch reload in the epilogue waits vmcnt(0) -- also for
+    // the next unit's in-flight DMAs
+    int lane_e;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+    const int lane = lane_e, fr = lane_e & 15, fq = lane_e >> 4;
     const int ncw = n0 + wc * 64;                 // first (staged) column of this wave
     // bias column offset (from ncw) of acc[.][nq*2+j][0] for this lane
     auto bcol = [&](int nq, int j) {
