@@ -332,7 +332,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_nt_v2_kernel(
   }
 }
 
-static int g_tile_group = 8;   // grouped tile order (rows per group); 1 = row-major
+static int g_tile_group = 4;   // grouped tile order (tile rows per group; 1 = row-major): 4 measured -0.3 % per headline job vs 8 (profiles/r05/tile_group_ab.json)
 CGS_EXPORT void cgs_set_tile_group(int g) { g_tile_group = g < 1 ? 1 : g; }
 
 static int gemm_v2_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,

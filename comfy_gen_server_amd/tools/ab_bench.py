@@ -18,6 +18,11 @@ import time
 import torch
 
 
+# process-wide kernel knobs that live in the native library (set through its setters, not read from the
+# environment at launch): name -> (setter, default)
+_NATIVE_KNOBS = {"CGS_TILE_GROUP": ("cgs_set_tile_group", 4), "CGS_CONV_TILE_GROUP": ("cgs_conv_set_tile_group", 8)}
+
+
 def _apply(env: dict, saved: dict):
     for k in saved:
         if saved[k] is None:
@@ -26,6 +31,11 @@ def _apply(env: dict, saved: dict):
             os.environ[k] = saved[k]
     for k, v in env.items():
         os.environ[k] = v
+    from .. import _native
+    lib = _native.load_kernels()
+    for k, (fn, dflt) in _NATIVE_KNOBS.items():
+        if lib is not None and _native.has_kernel(fn):
+            getattr(lib, fn)(int(os.environ.get(k, dflt)))
 
 
 def _drop_plans(patcher):
