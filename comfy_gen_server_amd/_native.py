@@ -98,6 +98,7 @@ KERNEL_SIGNATURES = {
     "cgs_attn_set_variant": [_I],     # 0 auto (D=64 fast kernel where legal), 1 generic, 2 fast only
     "cgs_set_tile_group": [_I],       # grouped tile order for GEMM v2/v3 (tile rows per group)
     "cgs_conv_set_tile_group": [_I],   # -1 auto (v3 where legal), 2 force the 8-wave 2-stage kernel
+    "cgs_dwconv_set_px": [_I],         # output pixels per thread of the depthwise 3x3 kernel (1 / 2 / 4)
     # out = a * gelu(g) where [a | g] = x rows of width 2*N
     "cgs_geglu": [_P, _P, _I, _I, _I, _P],   # x [M, 2N] -> out [M, N], dtype
     # fused CFG combine: out = u + (c - u) * scale   (fp32 or bf16 denoised)
@@ -209,7 +210,7 @@ KERNEL_SIGNATURES = {
 
 
 _RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_splitk_ws_bytes": ctypes.c_longlong, "cgs_groupnorm_f32_ws": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None,
-            "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None,
+            "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None, "cgs_dwconv_set_px": None,
             "cgs_attn_set_variant": None,
             "cgs_conv_v6_set_loader": None}
 

@@ -197,6 +197,77 @@ __global__ __launch_bounds__(256) void dwconv_nhwc_kernel(const s16x8* __restric
   }
 }
 
+// 3x3 form with PX = 2 or 4 output pixels along W per thread (W % PX == 0, zero padding): each of the three
+// input rows is read once as PX + 2 chunks and reused by the three column taps of all four outputs (9 x 16-B
+// loads of x and 9 of the weights per FOUR outputs instead of per one): the per-output kernel was bound by
+// its L1 / L2 re-reads (~3x its HBM streaming time at Stable Cascade's 24 x 24 x 2048 maps).
+template <int DT, int PX>
+__global__ __launch_bounds__(256) void dwconv3_px_kernel(const s16x8* __restrict__ x, const u16* __restrict__ wt,
+                                                          const u16* __restrict__ b, s16x8* __restrict__ y, int N,
+                                                          int H, int W, int C8) {
+  const int Wq = W / PX;
+  const unsigned total = (unsigned)N * H * Wq * C8;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % (unsigned)C8);
+    const unsigned pq = i / (unsigned)C8;
+    const int wq = (int)(pq % (unsigned)Wq);
+    const unsigned t = pq / (unsigned)Wq;
+    const int ho = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
+    const int w0 = wq * PX;
+    float acc[PX][8];
+    {
+      float bb[8];
+      if (b) {
+        const s16x8 bv = reinterpret_cast<const s16x8*>(b)[c8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = cvt_in<DT>((u16)bv[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < PX; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[q][j] = bb[j];
+    }
+#pragma unroll
+    for (int di = 0; di < 3; ++di) {
+      const int hi = ho + di - 1;
+      if (hi < 0 || hi >= H) continue;
+      const unsigned rowb = ((unsigned)n * H + hi) * W;
+      s16x8 xr[PX + 2];
+#pragma unroll
+      for (int q = 0; q < PX + 2; ++q) {
+        const int wi = w0 + q - 1;
+        xr[q] = (wi >= 0 && wi < W) ? x[(rowb + wi) * (unsigned)C8 + c8] : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int dj = 0; dj < 3; ++dj) {
+        const s16x8 wv = reinterpret_cast<const s16x8*>(wt + (size_t)(di * 3 + dj) * C8 * 8)[c8];
+        float wf[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wf[j] = cvt_in<DT>((u16)wv[j]);
+#pragma unroll
+        for (int q = 0; q < PX; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[q][j] = __builtin_fmaf(cvt_in<DT>((u16)xr[q + dj][j]), wf[j], acc[q][j]);
+      }
+    }
+    const unsigned ob = (((unsigned)n * H + ho) * W + w0) * (unsigned)C8 + c8;
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (short)cvt_out<DT>(acc[q][j]);
+      y[ob + (unsigned)q * C8] = o;
+    }
+  }
+}
+
+static int g_dw_px = 4;
+CGS_EXPORT void cgs_dwconv_set_px(int p) { g_dw_px = p == 1 ? 1 : p == 2 ? 2 : 4; }
+
 CGS_EXPORT int cgs_dwconv_nhwc(const void* x, const void* wt, const void* b, void* y, int N, int H, int W, int C,
                                int k, int replicate, int dtype, hipStream_t stream) {
   if (C % 8 || (k & 1) == 0 || k > 15) return (int)hipErrorInvalidValue;
@@ -205,6 +276,23 @@ CGS_EXPORT int cgs_dwconv_nhwc(const void* x, const void* wt, const void* b, voi
 #define CGS_DW(DTV, KV)                                                                                           \
   dwconv_nhwc_kernel<DTV, KV><<<ew_blocks(total), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b, \
                                                                     (s16x8*)y, N, H, W, C / 8, k, replicate)
+  // Pixels per thread: 4 (measured best or tied from 1 x 24 x 24 x 2048 to 8 x 128 x 128 x 320: 1.4-2x the
+  // one-pixel kernel on the large maps), 2 when W % 4 != 0; cgs_dwconv_set_px(1 / 2) overrides (A/B switch).
+  int px = g_dw_px;
+  if (W % px) px = (W % 2) ? 1 : 2;
+  if (k == 3 && !replicate && px > 1) {
+    const long long tq = total / px;
+#define CGS_DWP(D, P)                                                                                           \
+  dwconv3_px_kernel<D, P><<<ew_blocks(tq), 256, 0, stream>>>((const s16x8*)x, (const u16*)wt, (const u16*)b,       \
+                                                            (s16x8*)y, N, H, W, C / 8)
+    if (dtype == CGS_BF16) {
+      if (px == 4) CGS_DWP(CGS_BF16, 4); else CGS_DWP(CGS_BF16, 2);
+    } else {
+      if (px == 4) CGS_DWP(CGS_F16, 4); else CGS_DWP(CGS_F16, 2);
+    }
+#undef CGS_DWP
+    return (int)hipGetLastError();
+  }
   if (dtype == CGS_BF16) {
     if (k == 3) CGS_DW(CGS_BF16, 3); else if (k == 7) CGS_DW(CGS_BF16, 7); else CGS_DW(CGS_BF16, 0);
   } else {

@@ -181,6 +181,16 @@ def bench_cascade(reps, ab=None):
               params_c_b=round(n_c, 3), params_b_b=round(n_b, 3))
 
 
+def _native_knobs():
+    """Push the env values of the native A/B knobs (tools/ab_bench.py ``_NATIVE_KNOBS``) into the library."""
+    from .ab_bench import _NATIVE_KNOBS
+    from .. import _native
+    lib = _native.load_kernels()
+    for k, (fn, dflt) in _NATIVE_KNOBS.items():
+        if lib is not None and _native.has_kernel(fn):
+            getattr(lib, fn)(int(os.environ.get(k, dflt)))
+
+
 def _cascade_ab(cfgs, rounds, pc, pb, vae, pos, neg, NM, batch=1):
     """Cascade jobs (``batch`` images) alternating between env configurations (``name:ENV=V,...``) in one
     process: captured graph plans are dropped on every switch and re-captured in an untimed job."""
@@ -215,6 +225,7 @@ def _cascade_ab(cfgs, rounds, pc, pb, vae, pos, neg, NM, batch=1):
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(env)
+            _native_knobs()
             drop(pc)
             drop(pb)
             run()                                   # untimed: autotune keys, graph capture

@@ -153,12 +153,17 @@ def test_attention_bias(cuda, Bw, H, Sq, Sk, D, nW, kind):
 
 
 @pytest.mark.parametrize("N,H,W,C,k,rep", [(2, 24, 24, 64, 3, False), (1, 17, 9, 2048, 3, False),
-                                            (1, 32, 31, 192, 3, True), (2, 8, 8, 16, 5, False)])
-def test_depthwise_conv_nhwc(cuda, N, H, W, C, k, rep):
+                                            (1, 32, 31, 192, 3, True), (2, 8, 8, 16, 5, False),
+                                            (1, 4, 8, 2048, 3, False), (3, 5, 12, 8, 3, False),
+                                            (1, 1, 4, 24, 3, False), (2, 24, 24, 2048, 3, True),
+                                            (2, 6, 6, 64, 3, False)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_depthwise_conv_nhwc(cuda, N, H, W, C, k, rep, dt):
+    """W % 4 == 0 zero-padded 3 x 3 maps run the four-pixel kernel, the rest the one-pixel kernel."""
     torch.manual_seed(0)
-    x = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16)
-    w = torch.randn(C, 1, k, k, device=cuda).to(torch.bfloat16)
-    b = torch.randn(C, device=cuda).to(torch.bfloat16)
+    x = torch.randn(N, H, W, C, device=cuda).to(dt)
+    w = torch.randn(C, 1, k, k, device=cuda).to(dt)
+    b = torch.randn(C, device=cuda).to(dt)
     y = ops.depthwise_conv2d_nhwc(x, w.reshape(C, k * k).t().contiguous(), b, k, replicate=rep)
     xn = x.float().permute(0, 3, 1, 2)
     if rep:
@@ -167,6 +172,26 @@ def test_depthwise_conv_nhwc(cuda, N, H, W, C, k, rep):
         ref = F.conv2d(xn, w.float(), b.float(), padding=k // 2, groups=C)
     assert ops.stats().get(("dwconv", "hip"), 0) == 1
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_depthwise_conv_pixels_per_thread_knob(cuda):
+    """The 2 / 4 output-pixels-per-thread forms of the 3 x 3 depthwise kernel agree bit for bit (the same fma
+    order per output) and with the one-pixel kernel to bf16 rounding."""
+    from comfy_gen_server_amd import _native
+    lib = _native.load_kernels()
+    torch.manual_seed(0)
+    x = torch.randn(2, 12, 16, 256, device=cuda).to(torch.bfloat16)
+    w = torch.randn(9, 256, device=cuda).to(torch.bfloat16)
+    b = torch.randn(256, device=cuda).to(torch.bfloat16)
+    outs = []
+    try:
+        for p in (1, 2, 4):
+            lib.cgs_dwconv_set_px(p)
+            outs.append(ops.depthwise_conv2d_nhwc(x, w, b, 3))
+    finally:
+        lib.cgs_dwconv_set_px(4)
+    assert torch.equal(outs[1], outs[2])
+    assert _rel(outs[0], outs[2]) < 1e-2
 
 
 def test_layernorm_no_affine(cuda):
