@@ -33,7 +33,7 @@ def _ln(x, eps=1e-6):
 # all off by default: each measured 0.1-0.8 % SLOWER than the separate passes at batch 1 (in-process A/B,
 # profiles/r04/cascade_fusion_ab_r04k.json) -- the GRN / LayerNorm passes they remove are small at these
 # grids while the extra epilogue work sits on the GEMM's critical path
-_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0"}
+_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0", "ATTNLN": "0"}
 
 
 def _fuse(name: str, rows: int = 0) -> bool:
@@ -41,7 +41,11 @@ def _fuse(name: str, rows: int = 0) -> bool:
     (GELU in the first ChannelMLP GEMM), LNFOLD (LayerNorm folded into it), DWLN (its statistics from the
     depthwise kernel: off -- at Stage C's 1152-pixel grids the per-pixel reduction leaves the kernel
     latency-bound, 33 us vs 11 + 9 us for the two passes, profiles/r04/cascade_fusion_profile.md),
-    GRNFOLD (GRN folded into per-image second-GEMM weights). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
+    GRNFOLD (GRN folded into per-image second-GEMM weights), ATTNLN (the AttnBlock's LayerNorm folded into
+    its fused QKV GEMM: statistics pass + LN-fold epilogue instead of the materialised LN; off -- measured
+    +1.3 % per batch-4 job and +2.5 % at batch 1: the LN-fold epilogue costs the fused QKV GEMM what the
+    statistics-only pass saves, and at batch 1 the plain GEMM's fastest 256x160 tile has no LN-fold form
+    for N = 6144, profiles/r05/cascade_attnln.md). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
     (default 4096) pixels per call -- GELU_EPI + LNFOLD measured 2.5 % faster at batch 4 and 0.6 % slower
     at batch 1 (profiles/r04/cascade_fusion_ab_b4_r04av.json, cascade_fusion_ab_r04k.json)."""
     v = os.environ.get(f"CGS_CASCADE_{name}", _FUSE_DEFAULTS[name])
@@ -219,6 +223,19 @@ class OptimizedAttention(nn.Module, DerivedMixin):
         C = x.shape[-1]
         return x.is_cuda and x.dtype == torch.bfloat16 and C % 64 == 0 and C // self.heads == 64
 
+    def forward_self_ln(self, xs, rs, kv, residual=None, kvp=None):
+        """``forward_self(LN(xs), ...)`` with the LayerNorm (no affine) folded into the fused QKV GEMM: ``rs``
+        the per-row (mean, rstd) of xs (ops.layernorm_stats); the normalised rows are never written."""
+        C = xs.shape[-1]
+        wq, bq = self._fused(("to_q", "to_k", "to_v"), xs)
+        w2, cs, b2 = self._derived_get(("lnfold_qkv", xs.dtype, xs.device),
+                                       lambda: ops.lnfold_weights(wq, bq, None, None))
+        qkv = ops.linear_lnfold(xs, rs, w2, cs, b2)
+        kv2 = kvp if kvp is not None else self.project_kv(kv.to(xs.dtype))
+        o = ops.attention_kv2(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], kv2[..., :C], kv2[..., C:],
+                              self.heads)
+        return self.out_proj(o, residual=residual)
+
     def project_kv(self, kv):
         """[K | V] of the conditioning tokens: the part of forward_self's keys / values that does not
         depend on the image tokens (one fused GEMM)."""
@@ -278,6 +295,16 @@ class AttnBlock(nn.Module):
         return self.attention.attn.project_kv(self._map(clip))
 
     def forward(self, x, kv):
+        at = self.attention.attn
+        if self.self_attn and x.dim() == 4 and at.fused_ok(x) and _fuse("ATTNLN", _rows(x)) \
+                and not any(layers._hooked(getattr(at, n)) for n in ("to_q", "to_k", "to_v")) \
+                and ops.lnfold_available(x, x.shape[-1]):
+            B, H, W, C = x.shape
+            xs = x.reshape(B, H * W, C)
+            kvp = kv[id(self)] if isinstance(kv, dict) else None
+            o = at.forward_self_ln(xs, ops.layernorm_stats(x, 1e-6), None if kvp is not None else self._map(kv),
+                                   residual=xs, kvp=kvp)
+            return o.reshape(B, H, W, C)
         if isinstance(kv, dict):        # static conditioning K/V of a captured step (_UNetStage._static_cond)
             return self.attention(_ln(x), None, self_attn=True, residual=x, kvp=kv[id(self)])
         return self.attention(_ln(x), self._map(kv), self_attn=self.self_attn, residual=x)

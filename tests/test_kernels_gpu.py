@@ -1134,6 +1134,33 @@ def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c, monkeypatch):
     assert _rel(y.cpu(), ref) < 2e-2
 
 
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("N,H,W,c", [(2, 6, 6, 128), (1, 16, 8, 256)])
+def test_cascade_attnblock_lnfold(cuda, N, H, W, c, fold, monkeypatch):
+    """Cascade AttnBlock on the device with its LayerNorm folded into the fused QKV GEMM (ATTNLN=1:
+    statistics pass + ops.linear_lnfold) or materialised (0), plain and with the static conditioning K/V
+    of a captured step, vs the fp32 CPU block."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    monkeypatch.setenv("CGS_CASCADE_ATTNLN", fold)
+    calls = []
+    real = ops.linear_lnfold
+    monkeypatch.setattr(ops, "linear_lnfold", lambda *a, **k: calls.append(1) or real(*a, **k))
+    torch.manual_seed(3)
+    blk = SC.AttnBlock(c, 64, c // 64, self_attn=True)
+    init_random_(blk, seed=5)
+    x = torch.randn(N, H, W, c)
+    kv = torch.randn(N, 5, 64)
+    with torch.no_grad():
+        ref = blk(x, kv)
+        g = blk.to(device=cuda, dtype=torch.bfloat16)
+        xg, kvg = x.to(cuda, torch.bfloat16), kv.to(cuda, torch.bfloat16)
+        y = g(xg, kvg).float().cpu()
+        y2 = g(xg, {id(g): g.static_kv(kvg)}).float().cpu()
+    assert len(calls) == (2 if fold == "1" else 0)
+    assert _rel(y, ref) < 2e-2 and _rel(y2, ref) < 2e-2
+
+
 @pytest.mark.parametrize("N,H,W,c", [(2, 16, 16, 128), (2, 6, 6, 128), (1, 8, 8, 256)])
 def test_cascade_resblock_lnfold(cuda, N, H, W, c, monkeypatch):
     """Cascade ResBlock / FeedForwardBlock on the device: LayerNorm folded into the first GEMM together with
