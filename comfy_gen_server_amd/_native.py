@@ -98,7 +98,8 @@ KERNEL_SIGNATURES = {
     "cgs_attn_set_variant": [_I],     # 0 auto (D=64 fast kernel where legal), 1 generic, 2 fast only
     "cgs_set_tile_group": [_I],       # grouped tile order for GEMM v2/v3 (tile rows per group)
     "cgs_conv_set_tile_group": [_I],   # -1 auto (v3 where legal), 2 force the 8-wave 2-stage kernel
-    "cgs_dwconv_set_px": [_I],         # output pixels per thread of the depthwise 3x3 kernel (1 / 2 / 4)
+    "cgs_dwconv_set_px": [_I],
+    "cgs_affine_layernorm": [_P, _P, _P, _L, _F, _P, _P, _I, _I, _I, _F, _I, _P],         # output pixels per thread of the depthwise 3x3 kernel (1 / 2 / 4)
     # out = a * gelu(g) where [a | g] = x rows of width 2*N
     "cgs_geglu": [_P, _P, _I, _I, _I, _P],   # x [M, 2N] -> out [M, N], dtype
     # fused CFG combine: out = u + (c - u) * scale   (fp32 or bf16 denoised)

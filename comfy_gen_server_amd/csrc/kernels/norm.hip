@@ -531,6 +531,90 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ 
 }
 
 
+// Per-image channel affine followed by a LayerNorm without affine, one pass: xa = x * (add + sc[n, c]) +
+// sh[n, c] (rounded to the storage dtype: the tensor the block's residual path reads) is written, and
+// y = LN(xa) from the same registers. Stable Cascade TimestepBlock -> AttnBlock (``x * (1 + a) + b``, then
+// the attention's LayerNorm2d): one read of x instead of chan_affine's read + write and LayerNorm's
+// second read. sc / sh: [N, C] rows with stride ld (the halves of the mapper GEMM output).
+template <int DT, int LPR>
+__global__ __launch_bounds__(256) void affine_layernorm_kernel(const u16* __restrict__ x, const u16* __restrict__ sc,
+                                                               const u16* __restrict__ sh, long long ld, float add,
+                                                               u16* __restrict__ xa, u16* __restrict__ y, int rows,
+                                                               int HW, int C, float eps) {
+  constexpr int RPB = 256 / LPR;
+  const int lane = threadIdx.x % LPR;
+  const int row = blockIdx.x * RPB + threadIdx.x / LPR;
+  const bool live = row < rows;   // dead rows still join the shuffles (whole wave stays converged)
+  const int nch = C >> 3;
+  const size_t ro = (size_t)(live ? row : 0) * C;
+  const long long n = (live ? row : 0) / HW;
+  float v[LN_MAXK][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    const int ch = lane + LPR * k;
+    if (live && ch < nch) {
+      const s16x8 t = reinterpret_cast<const s16x8*>(x + ro)[ch];
+      const s16x8 a = *reinterpret_cast<const s16x8*>(sc + n * ld + ch * 8);
+      const s16x8 b = *reinterpret_cast<const s16x8*>(sh + n * ld + ch * 8);
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (short)cvt_out<DT>(__builtin_fmaf(cvt_in<DT>((u16)t[j]), add + cvt_in<DT>((u16)a[j]), cvt_in<DT>((u16)b[j])));
+        v[k][j] = cvt_in<DT>((u16)o[j]);
+        s += v[k][j];
+      }
+      reinterpret_cast<s16x8*>(xa + ro)[ch] = o;
+    }
+  }
+  const float mean = group_sum<LPR>(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    const int ch = lane + LPR * k;
+    if (live && ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[k][j] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(group_sum<LPR>(q) / C + eps);
+  if (!live) return;
+#pragma unroll
+  for (int k = 0; k < LN_MAXK; ++k) {
+    const int ch = lane + LPR * k;
+    if (ch < nch) {
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (short)cvt_out<DT>((v[k][j] - mean) * rstd);
+      reinterpret_cast<s16x8*>(y + ro)[ch] = o;
+    }
+  }
+}
+
+CGS_EXPORT int cgs_affine_layernorm(const void* x, const void* scale, const void* shift, long long ld, float add,
+                                    void* xa, void* y, int N, int HW, int C, float eps, int dtype,
+                                    hipStream_t stream) {
+  if (N <= 0 || HW <= 0) return 0;
+  const int nch = C / 8;
+  if (C % 8 || ld % 8 || nch > 64 * LN_MAXK || dtype == CGS_F32 ||
+      (((uintptr_t)x | (uintptr_t)xa | (uintptr_t)y | (uintptr_t)scale | (uintptr_t)shift) & 15))
+    return (int)hipErrorInvalidValue;
+  const long long rows = (long long)N * HW;
+  if (rows >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  const int lpr = nch <= 8 * LN_MAXK ? 8 : nch <= 16 * LN_MAXK ? 16 : nch <= 32 * LN_MAXK ? 32 : 64;
+  const dim3 grid((unsigned)((rows + 256 / lpr - 1) / (256 / lpr)));
+#define CGS_ALN(L)                                                                                                  \
+  if (dtype == CGS_BF16)                                                                                            \
+    affine_layernorm_kernel<CGS_BF16, L><<<grid, 256, 0, stream>>>((const u16*)x, (const u16*)scale, (const u16*)shift, \
+                                                                   ld, add, (u16*)xa, (u16*)y, (int)rows, HW, C, eps); \
+  else                                                                                                              \
+    affine_layernorm_kernel<CGS_F16, L><<<grid, 256, 0, stream>>>((const u16*)x, (const u16*)scale, (const u16*)shift, \
+                                                                  ld, add, (u16*)xa, (u16*)y, (int)rows, HW, C, eps);
+  if (lpr == 8) { CGS_ALN(8) } else if (lpr == 16) { CGS_ALN(16) } else if (lpr == 32) { CGS_ALN(32) } else { CGS_ALN(64) }
+#undef CGS_ALN
+  return (int)hipGetLastError();
+}
+
 // Row statistics only (the LayerNorm folded into the next GEMM's epilogue, MC_EPI_LNFOLD):
 // rs[2r] = mean, rs[2r+1] = rstd of row r. Same row-group layout and reductions as layernorm_kernel.
 template <int DT, int LPR>

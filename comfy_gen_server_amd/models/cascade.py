@@ -27,13 +27,16 @@ from .layers import Conv2d, DerivedMixin, LayerNorm, Linear, module_epoch
 # NHWC helpers
 # ------------------------------------------------------------------------------------------------
 def _ln(x, eps=1e-6):
+    h = getattr(x, "_cgs_ln", None)       # LN(x) already produced with x (TimestepBlock.forward_ln)
+    if h is not None and h[1] == x.data_ptr() and h[2] == eps:
+        return h[0]
     return ops.layer_norm(x, None, None, eps)
 
 
 # all off by default: each measured 0.1-0.8 % SLOWER than the separate passes at batch 1 (in-process A/B,
 # profiles/r04/cascade_fusion_ab_r04k.json) -- the GRN / LayerNorm passes they remove are small at these
 # grids while the extra epilogue work sits on the GEMM's critical path
-_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0", "ATTNLN": "0"}
+_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0", "ATTNLN": "0", "AFFLN": "1"}
 
 
 def _fuse(name: str, rows: int = 0) -> bool:
@@ -45,7 +48,8 @@ def _fuse(name: str, rows: int = 0) -> bool:
     its fused QKV GEMM: statistics pass + LN-fold epilogue instead of the materialised LN; off -- measured
     +1.3 % per batch-4 job and +2.5 % at batch 1: the LN-fold epilogue costs the fused QKV GEMM what the
     statistics-only pass saves, and at batch 1 the plain GEMM's fastest 256x160 tile has no LN-fold form
-    for N = 6144, profiles/r05/cascade_attnln.md). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
+    for N = 6144, profiles/r05/cascade_attnln.md), AFFLN (a TimestepBlock followed by an AttnBlock also
+    writes the attention's LayerNorm from the same pass, ops.channel_affine_layernorm_nhwc). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
     (default 4096) pixels per call -- GELU_EPI + LNFOLD measured 2.5 % faster at batch 4 and 0.6 % slower
     at batch 1 (profiles/r04/cascade_fusion_ab_b4_r04av.json, cascade_fusion_ab_r04k.json)."""
     v = os.environ.get(f"CGS_CASCADE_{name}", _FUSE_DEFAULTS[name])
@@ -327,12 +331,25 @@ class TimestepBlock(nn.Module):
         for name in self.conds:
             setattr(self, f"mapper_{name}", Linear(c_timestep, c * 2, dtype=dtype, device=device))
 
-    def forward(self, x, t):
+    def forward_ln(self, x, t, eps=1e-6):
+        """``forward`` whose output also carries its LayerNorm (no affine) for the next AttnBlock (``_ln``
+        picks it up), from one pass over x."""
+        if not (x.dim() == 4 and x.is_contiguous()):
+            return self.forward(x, t)
+        a, b = self._ab(t)
+        xa, ln = ops.channel_affine_layernorm_nhwc(x, a, b, add=1.0, eps=eps)
+        xa._cgs_ln = (ln, xa.data_ptr(), eps)
+        return xa
+
+    def _ab(self, t):
         t = t.chunk(len(self.conds) + 1, dim=1)
         ab = self.mapper(t[0])
         for i, name in enumerate(self.conds):      # the sum rides the GEMMs' residual epilogue
             ab = getattr(self, f"mapper_{name}")(t[i + 1], residual=ab)
-        a, b = ab.chunk(2, dim=-1)
+        return ab.chunk(2, dim=-1)
+
+    def forward(self, x, t):
+        a, b = self._ab(t)
         if x.dim() == 4 and x.is_contiguous():
             return ops.channel_affine_nhwc(x, a, b, add=1.0)
         return torch.addcmul(b[:, None, None, :], x, 1 + a[:, None, None, :])
@@ -455,13 +472,15 @@ class _UNetStage(nn.Module):
                 n += 1
         return n
 
-    def _run_block(self, block, x, r_embed, clip, skip=None, cnet=None):
+    def _run_block(self, block, x, r_embed, clip, skip=None, cnet=None, nxt=None):
         if isinstance(block, ResBlock):
             x = self._add_cnet(x, cnet)
             return block(x, skip)
         if isinstance(block, AttnBlock):
             return block(x, clip)
         if isinstance(block, TimestepBlock):
+            if isinstance(nxt, AttnBlock) and x.is_cuda and _fuse("AFFLN", _rows(x)):
+                return block.forward_ln(x, r_embed)
             return block(x, r_embed)
         return block(x)
 
@@ -470,8 +489,9 @@ class _UNetStage(nn.Module):
         for down_block, downscaler, repmap in zip(self.down_blocks, self.down_downscalers, self.down_repeat_mappers):
             x = self._downscale(downscaler, x)
             for i in range(len(repmap) + 1):
-                for block in down_block:
-                    x = self._run_block(block, x, r_embed, clip, cnet=cnet)
+                for bi, block in enumerate(down_block):
+                    nxt = down_block[bi + 1] if bi + 1 < len(down_block) else None
+                    x = self._run_block(block, x, r_embed, clip, cnet=cnet, nxt=nxt)
                 if i < len(repmap):
                     x = _pw(repmap[i], x)
             levels.insert(0, x)
@@ -487,7 +507,8 @@ class _UNetStage(nn.Module):
                         skip = levels[i] if k == 0 and i > 0 else None
                         if skip is not None and x.shape[1:3] != skip.shape[1:3]:
                             x = _resize_nhwc(x, skip.shape[1:3])
-                    x = self._run_block(block, x, r_embed, clip, skip=skip, cnet=cnet)
+                    nxt = up_block[k + 1] if k + 1 < len(up_block) else None
+                    x = self._run_block(block, x, r_embed, clip, skip=skip, cnet=cnet, nxt=nxt)
                 if j < len(repmap):
                     x = _pw(repmap[j], x)
             x = self._upscale(upscaler, x)

@@ -19,7 +19,7 @@ from .core import (  # noqa: F401
     conv_transpose2d, conv_transpose_phase_weights, silu, gelu,
     upsample_nearest2x, timestep_embedding, cfg_combine, euler_step, depthwise_conv2d_nhwc,
     depthwise_conv2d_nhwc_lnstats,
-    interpolate, fused_bias_act, channel_affine_nhwc, upfirdn2d, upfirdn2d_reference, vq_nearest, grn_nhwc,
+    interpolate, fused_bias_act, channel_affine_nhwc, channel_affine_layernorm_nhwc, upfirdn2d, upfirdn2d_reference, vq_nearest, grn_nhwc,
     grn_fold_weight, softmax_rows,
     attention_with_probs, philox_randn, euler_ancestral_philox, brownian_increment, step_param, sampler_step_dev,
     step_advance, vae_out_u8, region_accumulate, region_normalize, clip_embed, pooled_gather,

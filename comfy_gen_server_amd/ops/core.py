@@ -1563,6 +1563,30 @@ def channel_affine_nhwc(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tenso
     return (x.float() * (add + scale.reshape(shp).float()) + shift.reshape(shp).float()).to(x.dtype)
 
 
+def channel_affine_layernorm_nhwc(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, add: float = 0.0,
+                                   eps: float = 1e-6):
+    """``(xa, LN(xa))`` with xa = ``channel_affine_nhwc(x, scale, shift, add)`` and LN a LayerNorm over C
+    without affine, from one read of x (Stable Cascade TimestepBlock -> AttnBlock). Same coefficient
+    layout as channel_affine_nhwc."""
+    N, C = x.shape[0], x.shape[-1]
+    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() and C % 8 == 0
+            and C <= 4096 and _native.has_kernel("cgs_affine_layernorm")
+            and backend_for("channel_affine", x, "cgs_affine_layernorm") == "hip"
+            and scale.dtype == shift.dtype == x.dtype and scale.dim() == 2 and shift.dim() == 2
+            and scale.stride(1) == 1 and shift.stride(1) == 1 and scale.stride(0) == shift.stride(0)
+            and scale.stride(0) % 8 == 0 and scale.data_ptr() % 16 == 0 and shift.data_ptr() % 16 == 0):
+        count("channel_affine", "hip")
+        count("layernorm", "hip")
+        xa = torch.empty_like(x)
+        y = torch.empty_like(x)
+        _check(_lib().cgs_affine_layernorm(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), scale.stride(0),
+                                           float(add), xa.data_ptr(), y.data_ptr(), N, x.numel() // (N * C), C,
+                                           float(eps), _DT[x.dtype], _stream()), "cgs_affine_layernorm")
+        return xa, y
+    xa = channel_affine_nhwc(x, scale, shift, add)
+    return xa, layer_norm(xa, None, None, eps)
+
+
 def fused_bias_act(x: torch.Tensor, bias: torch.Tensor | None, negative_slope: float = 0.2,
                    scale: float = 2 ** 0.5) -> torch.Tensor:
     """StyleGAN2 FusedLeakyReLU (K32, ``face/fused_act.py``): leaky_relu(x + bias[c]) * scale,

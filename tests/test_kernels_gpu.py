@@ -1134,6 +1134,49 @@ def test_cascade_channel_mlp_grn_fold(cuda, N, H, W, c, monkeypatch):
     assert _rel(y.cpu(), ref) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W,C", [(2, 24, 24, 2048), (3, 5, 7, 64), (1, 8, 8, 1280), (2, 4, 4, 4096)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_channel_affine_layernorm(cuda, N, H, W, C, dt):
+    """One-pass x * (1 + a[n]) + b[n] and LayerNorm of it (Cascade TimestepBlock -> AttnBlock): xa bit-equal
+    to channel_affine_nhwc, LN(xa) vs the fp32 LayerNorm of xa."""
+    torch.manual_seed(1)
+    x = (torch.randn(N, H, W, C, device=cuda) * 2 + 0.5).to(dt)
+    ab = (torch.randn(N, 2 * C, device=cuda) * 0.5).to(dt)
+    a, b = ab.chunk(2, dim=-1)
+    ops.reset_stats()
+    xa, y = ops.channel_affine_layernorm_nhwc(x, a, b, add=1.0, eps=1e-6)
+    assert ops.stats().get(("channel_affine", "hip"), 0) == 1
+    assert torch.equal(xa, ops.channel_affine_nhwc(x, a, b, add=1.0))
+    ref = F.layer_norm(xa.float(), (C,), eps=1e-6)
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_cascade_stage_affine_layernorm_path(cuda, fused, monkeypatch):
+    """Stage C (C-T-A blocks) with the TimestepBlock writing the next AttnBlock's LayerNorm (AFFLN) == the
+    separate affine + LayerNorm passes."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    monkeypatch.setenv("CGS_CASCADE_AFFLN", fused)
+    calls = []
+    real = ops.channel_affine_layernorm_nhwc
+    monkeypatch.setattr(ops, "channel_affine_layernorm_nhwc", lambda *a, **k: calls.append(1) or real(*a, **k))
+    cfg = dict(c_in=16, c_out=16, c_r=64, c_cond=128, c_hidden=[128, 128], nhead=[2, 2], blocks=[[1, 1], [1, 1]],
+               block_repeat=[[1, 1], [1, 1]], level_config=["CTA", "CTA"], c_clip_text=64, c_clip_text_pooled=64,
+               c_clip_img=768, c_clip_seq=2, switch_level=[False])
+    m = SC.StageC(**cfg)
+    init_random_(m, seed=11)
+    g = torch.Generator().manual_seed(1)
+    args = (torch.randn(2, 16, 12, 12, generator=g), torch.tensor([0.3, 0.7]), torch.randn(2, 7, 64, generator=g),
+            torch.randn(2, 1, 64, generator=g), torch.randn(2, 1, 768, generator=g))
+    with torch.inference_mode():
+        ref = m(*args).float()
+        m = m.to(device=cuda, dtype=torch.bfloat16)
+        out = m(*tuple(a.to(cuda, torch.bfloat16 if a.dim() > 1 else torch.float32) for a in args)).float().cpu()
+    assert (len(calls) > 0) == (fused == "1")
+    assert _rel(out, ref) < 3e-2
+
+
 @pytest.mark.parametrize("fold", ["1", "0"])
 @pytest.mark.parametrize("N,H,W,c", [(2, 6, 6, 128), (1, 16, 8, 256)])
 def test_cascade_attnblock_lnfold(cuda, N, H, W, c, fold, monkeypatch):
