@@ -1072,6 +1072,9 @@ CGS_EXPORT int cgs_flash_attn_fwd_v(const void* q, const void* k, const void* v,
   return rc;
 }
 
+static int g_kv2_rows = 0;   // Q rows per workgroup of the two-source kernel: 0 auto, 128, 256 (A/B switch)
+CGS_EXPORT void cgs_attn_set_kv2_rows(int r) { g_kv2_rows = r == 128 || r == 256 ? r : 0; }
+
 // D = 64 attention over the key concat of two K / V sources (see KV2): keys [0, Sk1) from k1 / v1 ([B, Sk1]
 // rows), keys [Sk1, Sk1 + Sk2) from k2 / v2. Head stride D in every source; no mask.
 CGS_EXPORT int cgs_flash_attn_fwd_kv2(const void* q, const void* k1, const void* v1, const void* k2, const void* v2,
@@ -1086,7 +1089,10 @@ CGS_EXPORT int cgs_flash_attn_fwd_kv2(const void* q, const void* k1, const void*
                      15) == 0;
   if (!al16 || Sk1 <= 0 || Sk2 <= 0 || Sq <= 0 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
   const long long nwg256 = (long long)((Sq + 255) / 256) * B * H;
-  const bool small = nwg256 < num_cus_attn();
+  // 128-row blocks only for tiny grids: at Cascade batch 1 (B x H = 64 / 40, 576 / 1024 queries: 192 / 160
+  // workgroups of 256 rows) the 256-row form measured 13-16 % faster than the 128-row one it used to pick
+  // below one round of CUs (profiles/r05/attn_kv2_rows.md)
+  const bool small = g_kv2_rows == 128 || (g_kv2_rows == 0 && nwg256 * 4 < num_cus_attn());
   const int rows = small ? 128 : 256;
   const int nqb2 = (Sq + rows - 1) / rows;
   const long long nwg2 = (long long)nqb2 * B * H;
