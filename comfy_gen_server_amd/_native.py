@@ -175,6 +175,7 @@ KERNEL_SIGNATURES = {
     "cgs_v6_set_mode": [_I],
     "cgs_attn_set_prio": [_I],
     "cgs_attn_set_kv2_rows": [_I],
+    "cgs_flash_attn_fwd_ks": [_P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _F, _I, _P, _P, _P],
     "cgs_flash_attn_fwd_kv2": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _L, _F, _P],
     "cgs_conv2d_nhwc_gns": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P],
     # row-sharded GroupNorm (parallel/spatial.py): band statistics, then apply with combined (mean, rstd)

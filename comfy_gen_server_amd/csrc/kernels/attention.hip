@@ -339,25 +339,41 @@ struct KV2 {
 // attn_persistent_v2_r04at.log); removed.
 // NW = 8: 256-row Q block, one WG per CU. NW = 4: 128-row Q block, two WGs per CU -- twice the
 // workgroups for the under-filled grids of small batches (batch-1 SDXL level 2: 160 -> 320).
-template <int NW, bool TWO = false, bool PRIO = true>
+// KS > 1 (key split, small grids): the grid is KS x (Q blocks x B x H); split s attends over its run of
+// ceil(tiles / KS) 64-key tiles only and writes its normalised partial O to op + s * ospl and its
+// log-sum-exp to lse + s * B * H * Sq; attn_ks_combine_kernel merges the KS partials. The host
+// guarantees every split has at least one key.
+template <int NW, bool TWO = false, bool PRIO = true, int KS = 1>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
     long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
-    float c, int nqb, float* __restrict__ lse = nullptr, KV2 kv2 = KV2{nullptr, nullptr, 0, 0, 0, 0, 0}) {
+    float c, int nqb, float* __restrict__ lse = nullptr, KV2 kv2 = KV2{nullptr, nullptr, 0, 0, 0, 0, 0},
+    long long ospl = 0) {
   __shared__ __attribute__((aligned(16))) u16 Ks[2][64 * 64];
   __shared__ __attribute__((aligned(16))) u16 Vs[2][64 * 64];
 
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = logical % nqb;
-  const int bh = logical / nqb;
+  int bh = logical / nqb;
+  int k_lo = 0;
+  if constexpr (KS > 1) {
+    const int BH = (int)(gridDim.x / ((unsigned)nqb * KS));
+    const int split = bh / BH;
+    bh -= split * BH;
+    const int tps = ((Sk + 63) / 64 + KS - 1) / KS;
+    k_lo = split * tps * 64;
+    Sk = min(Sk - k_lo, tps * 64);
+    op += split * ospl;
+    lse += (long long)split * BH * Sq;
+  }
   const int b = bh / H, h = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hf = lane >> 5;
 
   const u16* qbase = qp + b * qsb + h * qsh;
-  const u16* kbase = kp + b * ksb + h * ksh;
-  const u16* vbase = vp + b * vsb + h * vsh;
+  const u16* kbase = kp + b * ksb + h * ksh + (long long)k_lo * kss;
+  const u16* vbase = vp + b * vsb + h * vsh + (long long)k_lo * vss;
   u16* obase = op + b * osb + h * osh;
 
   const int q_row = qb * (32 * NW) + wave * 32 + l32;
@@ -1070,6 +1086,84 @@ CGS_EXPORT int cgs_flash_attn_fwd_v(const void* q, const void* k, const void* v,
                                  scale, nullptr, 0, nullptr, stream);
   g_attn_variant = saved;
   return rc;
+}
+
+// Merge of the KS key-split partials: O = sum_s exp(lse_s - L) O_s with L = log sum_s exp(lse_s) (every
+// partial is already normalised by its own row sum). One thread per 8 channels of one (b, q, h) row.
+template <int KS>
+__global__ __launch_bounds__(256) void attn_ks_combine_kernel(const u16* __restrict__ part, const float* __restrict__ lse,
+                                                              u16* __restrict__ o, int B, int H, int Sq,
+                                                              long long ospl, long long osb, long long oss,
+                                                              long long osh) {
+  const long long total = (long long)B * Sq * H * 8;
+  const long long lspl = (long long)B * H * Sq;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c8 = (int)(i & 7);
+    const long long r = i >> 3;                  // (b, q, h) row, h fastest
+    const int h = (int)(r % H);
+    const long long bq = r / H;
+    const int q = (int)(bq % Sq);
+    const int b = (int)(bq / Sq);
+    float l[KS], mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      l[s] = lse[s * lspl + ((long long)b * H + h) * Sq + q];
+      mx = fmaxf(mx, l[s]);
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wsum = 0.f;
+    const long long po = ((long long)b * Sq + q) * H * 64 + h * 64 + c8 * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float w = mx == -INFINITY ? 0.f : __expf(l[s] - mx);
+      wsum += w;
+      const s16x8 v = *reinterpret_cast<const s16x8*>(part + s * ospl + po);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = __builtin_fmaf(w, cvt_in<CGS_BF16>((u16)v[j]), acc[j]);
+    }
+    const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
+    s16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = (short)cvt_out<CGS_BF16>(acc[j] * inv);
+    *reinterpret_cast<s16x8*>(o + (long long)b * osb + (long long)q * oss + (long long)h * osh + c8 * 8) = out;
+  }
+}
+
+// D = 64 self-attention with the keys split KS ways (2 or 4) for under-filled grids (batch-1 SDXL: 160-320
+// workgroups of 256 query rows on 256 CUs): KS x the workgroups, then one merge pass. ws_o: KS * B * Sq * H * 64
+// bf16, ws_lse: KS * B * H * Sq floats. 256-row Q blocks (8 waves).
+CGS_EXPORT int cgs_flash_attn_fwd_ks(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
+                                     long long qsb, long long qss, long long ksb, long long kss, long long vsb,
+                                     long long vss, long long osb, long long oss, float scale, int KS, void* ws_o,
+                                     void* ws_lse, hipStream_t stream) {
+  if ((KS != 2 && KS != 4) || B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0 || !ws_o || !ws_lse) return (int)hipErrorInvalidValue;
+  const bool al16 = ((qss | qsb | kss | ksb | vss | vsb | oss | osb) & 7) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) | reinterpret_cast<uintptr_t>(v) |
+                      reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(ws_o)) & 15) == 0;
+  const int tiles = (Sk + 63) / 64;
+  const int tps = (tiles + KS - 1) / KS;
+  if (!al16 || (long long)(KS - 1) * tps * 64 >= Sk) return (int)hipErrorInvalidValue;   // every split has keys
+  const int nqb = (Sq + 255) / 256;
+  const long long nwg = (long long)nqb * B * H * KS;
+  const long long ospl = (long long)B * Sq * H * 64;
+  if (nwg > 0x7fffffff || ospl * KS > 0x7fffffffffffll) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * 1.4426950408889634f;
+  const long long wsb = (long long)Sq * H * 64, wss = (long long)H * 64;
+#define CGS_KS_GO(KV)                                                                                              \
+  attn_fwd_d64_kernel<8, false, true, KV><<<dim3((unsigned)nwg), 512, 0, stream>>>(                                \
+      (const u16*)q, (const u16*)k, (const u16*)v, (u16*)ws_o, H, Sq, Sk, qsb, qss, 64, ksb, kss, 64, vsb, vss, 64,   \
+      wsb, wss, 64, sl2, nqb, (float*)ws_lse, KV2{nullptr, nullptr, 0, 0, 0, 0, 0}, ospl)
+  if (KS == 2) CGS_KS_GO(2); else CGS_KS_GO(4);
+#undef CGS_KS_GO
+  const long long thr = (long long)B * Sq * H * 8;
+  long long nb = (thr + 255) / 256;
+  const int blocks = (int)(nb > 16384 ? 16384 : nb);
+  if (KS == 2)
+    attn_ks_combine_kernel<2><<<blocks, 256, 0, stream>>>((const u16*)ws_o, (const float*)ws_lse, (u16*)o, B, H, Sq,
+                                                          ospl, osb, oss, 64);
+  else
+    attn_ks_combine_kernel<4><<<blocks, 256, 0, stream>>>((const u16*)ws_o, (const float*)ws_lse, (u16*)o, B, H, Sq,
+                                                          ospl, osb, oss, 64);
+  return (int)hipGetLastError();
 }
 
 static int g_kv2_rows = 0;   // Q rows per workgroup of the two-source kernel: 0 auto, 128, 256 (A/B switch)

@@ -85,6 +85,11 @@ def _skinny_ws(M: int, N: int, K: int, device):
     return torch.empty(n, dtype=torch.uint8, device=device) if n else None
 
 
+# D = 64 self-attention grids below this many 256-row workgroups are tuned among the small-grid forms
+# (128-row blocks, key split): up to two rounds of the CUs (batch-1 SDXL level 1 is 320)
+_ATTN_SMALL_WG = int(os.environ.get("CGS_ATTN_SMALL_WG", "512"))
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, act: str | None = None,
            out: torch.Tensor | None = None, row_stats: bool = False) -> torch.Tensor:
@@ -395,7 +400,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
         # D = 64 self-attention whose 256-query blocks leave CUs idle (batch 1-2 at level 2: B*H*Sq/256
         # < 256 workgroups): the 128-row form of the fast kernel and the generic kernel are measured
         # alternatives
-        if (kp is None and not causal and D == 64 and Sk > 128 and B * heads * ((Sq + 255) // 256) < 256
+        if (kp is None and not causal and D == 64 and Sk > 128 and B * heads * ((Sq + 255) // 256) < _ATTN_SMALL_WG
                 and B * heads * Sq * Sk >= (1 << 22) and _native.has_kernel("cgs_flash_attn_fwd_v")):
             def run_v(var):
                 o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
@@ -404,11 +409,27 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
                     q.stride(0), q.stride(1), D, k.stride(0), k.stride(1), D, v.stride(0), v.stride(1), D,
                     o.stride(0), o.stride(1), D, 1.0 / math.sqrt(D), var, _stream()), "cgs_flash_attn_fwd_v")
                 return o
-            # d64: 256-row Q blocks (8 waves); d64q128: 128-row blocks, 4 waves, two WGs per CU
-            sel = autotune.choose(("attention_grid2", B, heads, Sq, Sk, D),
-                                  [("d64", lambda: run_v(2)), ("d64q128", lambda: run_v(5)),
-                                   ("generic", lambda: run_v(1))], default="d64q128")
+            def run_ks(ks):
+                o = torch.empty((B, Sq, HD), device=q.device, dtype=q.dtype)
+                ws_o = torch.empty((ks * B * Sq * HD,), device=q.device, dtype=q.dtype)
+                ws_l = torch.empty((ks * B * heads * Sq,), device=q.device, dtype=torch.float32)
+                _check(_lib().cgs_flash_attn_fwd_ks(
+                    q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, heads, Sq, Sk, q.stride(0), q.stride(1),
+                    k.stride(0), k.stride(1), v.stride(0), v.stride(1), o.stride(0), o.stride(1), 1.0 / math.sqrt(D),
+                    ks, ws_o.data_ptr(), ws_l.data_ptr(), _stream()), "cgs_flash_attn_fwd_ks")
+                return o
+            # d64: 256-row Q blocks (8 waves); d64q128: 128-row blocks, 4 waves, two WGs per CU; d64ks2 / 4: the
+            # keys split 2 / 4 ways (KS x the workgroups) and the partials merged by log-sum-exp
+            cands = [("d64", lambda: run_v(2)), ("d64q128", lambda: run_v(5)), ("generic", lambda: run_v(1))]
+            tiles = (Sk + 63) // 64
+            if _native.has_kernel("cgs_flash_attn_fwd_ks") and q.data_ptr() % 16 == 0:
+                for ks in (2, 4):
+                    if tiles >= 4 * ks and (ks - 1) * ((tiles + ks - 1) // ks) * 64 < Sk:
+                        cands.append((f"d64ks{ks}", (lambda ks=ks: run_ks(ks))))
+            sel = autotune.choose(("attention_grid2", B, heads, Sq, Sk, D), cands, default="d64q128")
             count("attention", "hip")
+            if sel in ("d64ks2", "d64ks4"):
+                return run_ks(int(sel[-1]))
             return run_v({"d64": 2, "d64q128": 5}.get(sel, 1))
         # The vendor SDPA is a tuning candidate only on explicit request: the hot path is the
         # hand-written kernel (K02/K03), never an SDPA fallback.

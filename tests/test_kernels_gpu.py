@@ -194,6 +194,34 @@ def test_depthwise_conv_pixels_per_thread_knob(cuda):
     assert _rel(outs[0], outs[2]) < 1e-2
 
 
+@pytest.mark.parametrize("ks", ["d64ks2", "d64ks4"])
+@pytest.mark.parametrize("B,H,Sq,Sk,fused", [(2, 20, 1024, 1024, True), (2, 10, 4096, 4096, True),
+                                             (1, 8, 700, 1000, False), (2, 8, 333, 1100, False)])
+def test_attention_key_split(cuda, B, H, Sq, Sk, fused, ks, monkeypatch):
+    """D = 64 self-attention with the keys split 2 / 4 ways and the partials merged by log-sum-exp (the
+    small-grid candidates of ops.attention), forced through the tuning override, vs the fp32 reference;
+    q / k / v as column views of one fused QKV projection where Sq == Sk."""
+    import json
+    torch.manual_seed(4)
+    C = H * 64
+    if fused:
+        qkv = torch.randn(B, Sq, 3 * C, device=cuda).to(torch.bfloat16)
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    else:
+        q = torch.randn(B, Sq, C, device=cuda).to(torch.bfloat16)
+        k = torch.randn(B, Sk, C, device=cuda).to(torch.bfloat16)
+        v = torch.randn(B, Sk, C, device=cuda).to(torch.bfloat16)
+    monkeypatch.setenv("CGS_AUTOTUNE", "1")
+    monkeypatch.setenv("CGS_TUNE_OVERRIDE", json.dumps({f"attention_grid2|{B}|{H}|{Sq}|{Sk}|64": ks}))
+    calls = []
+    lib = _native.load_kernels()
+    real = lib.cgs_flash_attn_fwd_ks
+    monkeypatch.setattr(lib, "cgs_flash_attn_fwd_ks", lambda *a: calls.append(a[17]) or real(*a))
+    o = ops.attention(q, k, v, H)
+    assert calls == [int(ks[-1])]
+    assert _rel(o, core.attention_reference(q.float(), k.float(), v.float(), H)) < 2e-2
+
+
 def test_layernorm_no_affine(cuda):
     x = torch.randn(300, 2048, device=cuda).to(torch.bfloat16)
     y = ops.layer_norm(x, None, None, 1e-6)
