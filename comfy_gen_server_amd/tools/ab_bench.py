@@ -21,7 +21,8 @@ import torch
 # process-wide kernel knobs that live in the native library (set through its setters, not read from the
 # environment at launch): name -> (setter, default)
 _NATIVE_KNOBS = {"CGS_TILE_GROUP": ("cgs_set_tile_group", 4), "CGS_CONV_TILE_GROUP": ("cgs_conv_set_tile_group", 8),
-                 "CGS_DW_PX": ("cgs_dwconv_set_px", 4), "CGS_ATTN_KV2_ROWS": ("cgs_attn_set_kv2_rows", 0)}
+                 "CGS_DW_PX": ("cgs_dwconv_set_px", 4), "CGS_ATTN_KV2_ROWS": ("cgs_attn_set_kv2_rows", 0),
+                 "CGS_GRN_ROWS": ("cgs_grn_set_rows", 1)}
 
 
 def _apply(env: dict, saved: dict):

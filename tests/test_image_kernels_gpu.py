@@ -132,6 +132,29 @@ def test_grn_v2_gpu(cuda, shape, pre_gelu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 24, 24, 8192), (3, 7, 5, 2056), (1, 33, 1, 4096)])
+@pytest.mark.parametrize("pre_gelu", [False, True])
+def test_grn_apply_row_tiled_matches_grid_stride(cuda, shape, pre_gelu):
+    """The row-tiled GRN apply (per-thread channel coefficients, cgs_grn_set_rows(1), the default) vs the
+    grid-stride apply it replaced (0): same values to fp32 rounding of the coefficient product."""
+    from comfy_gen_server_amd import _native
+    lib = _native.load_kernels()
+    N, H, W, C = shape
+    torch.manual_seed(2)
+    x = torch.randn(*shape, device=cuda).to(torch.bfloat16)
+    g = (torch.randn(C, device=cuda) * 0.5).to(torch.bfloat16)
+    b = (torch.randn(C, device=cuda) * 0.1).to(torch.bfloat16)
+    try:
+        lib.cgs_grn_set_rows(0)
+        old = ops.grn_nhwc(x, g, b, pre_gelu=pre_gelu).float()
+        lib.cgs_grn_set_rows(1)
+        new = ops.grn_nhwc(x, g, b, pre_gelu=pre_gelu).float()
+    finally:
+        lib.cgs_grn_set_rows(1)
+    assert ((new - old).norm() / old.norm()).item() < 1e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_grn_gpu(cuda, dtype):
     x, g, b = torch.randn(2, 24, 24, 2048), torch.randn(2048) * 0.5, torch.randn(2048) * 0.1
