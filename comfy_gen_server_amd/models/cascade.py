@@ -36,7 +36,7 @@ def _ln(x, eps=1e-6):
 # all off by default: each measured 0.1-0.8 % SLOWER than the separate passes at batch 1 (in-process A/B,
 # profiles/r04/cascade_fusion_ab_r04k.json) -- the GRN / LayerNorm passes they remove are small at these
 # grids while the extra epilogue work sits on the GEMM's critical path
-_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0", "ATTNLN": "0", "AFFLN": "1"}
+_FUSE_DEFAULTS = {"GELU_EPI": "auto", "LNFOLD": "auto", "GRNFOLD": "0", "DWLN": "0", "ATTNLN": "0", "AFFLN": "1", "TSBATCH": "1"}
 
 
 def _fuse(name: str, rows: int = 0) -> bool:
@@ -49,7 +49,8 @@ def _fuse(name: str, rows: int = 0) -> bool:
     +1.3 % per batch-4 job and +2.5 % at batch 1: the LN-fold epilogue costs the fused QKV GEMM what the
     statistics-only pass saves, and at batch 1 the plain GEMM's fastest 256x160 tile has no LN-fold form
     for N = 6144, profiles/r05/cascade_attnln.md), AFFLN (a TimestepBlock followed by an AttnBlock also
-    writes the attention's LayerNorm from the same pass, ops.channel_affine_layernorm_nhwc). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
+    writes the attention's LayerNorm from the same pass, ops.channel_affine_layernorm_nhwc), TSBATCH (every
+    TimestepBlock's mapper pair of a stage in one GEMM per call, _UNetStage._ts_mapped). "auto": on from ``CGS_CASCADE_FUSE_MIN_ROWS``
     (default 4096) pixels per call -- GELU_EPI + LNFOLD measured 2.5 % faster at batch 4 and 0.6 % slower
     at batch 1 (profiles/r04/cascade_fusion_ab_b4_r04av.json, cascade_fusion_ab_r04k.json)."""
     v = os.environ.get(f"CGS_CASCADE_{name}", _FUSE_DEFAULTS[name])
@@ -341,7 +342,13 @@ class TimestepBlock(nn.Module):
         xa._cgs_ln = (ln, xa.data_ptr(), eps)
         return xa
 
+    def _mappers(self):
+        return [self.mapper] + [getattr(self, f"mapper_{name}") for name in self.conds]
+
     def _ab(self, t):
+        pre = getattr(t, "_cgs_ts", None)          # all mappers of the stage in one GEMM (_ts_mapped)
+        if pre is not None and id(self) in pre:
+            return pre[id(self)].chunk(2, dim=-1)
         t = t.chunk(len(self.conds) + 1, dim=1)
         ab = self.mapper(t[0])
         for i, name in enumerate(self.conds):      # the sum rides the GEMMs' residual epilogue
@@ -471,6 +478,50 @@ class _UNetStage(nn.Module):
                     bufs[k].copy_(v)
                 n += 1
         return n
+
+    def _ts_mapped(self, r_embed):
+        """Every TimestepBlock's ``[a | b]`` (mapper(t0) + mapper_<cond>(t1) + ...) from ONE GEMM: the mappers
+        read only r_embed = [t0 | t1 | ...], so their weights concatenated along K per block and stacked
+        along N over the blocks give all of them at once (the per-block pairs were ~100 launch-bound
+        skinny GEMMs per UNet call). Returns {id(block): [B, 2C] column view} or None."""
+        if not (r_embed.is_cuda and r_embed.dtype in (torch.bfloat16, torch.float16) and _fuse("TSBATCH")):
+            return None
+        blocks = self.__dict__.get("_ts_blocks")
+        if blocks is None:
+            blocks = self.__dict__["_ts_blocks"] = [m for m in self.modules() if isinstance(m, TimestepBlock)]
+        if not blocks or any(layers._hooked(m) for b in blocks for m in b._mappers()):
+            return None
+        key = (r_embed.dtype, r_embed.device, module_epoch(self), blocks[0].mapper.weight.data_ptr())
+        ent = self.__dict__.get("_ts_fused")
+        if ent is None or ent[0] != key:
+            ws, bs, offs, off = [], [], {}, 0
+            for blk in blocks:
+                mods = blk._mappers()
+                w = torch.cat([_cast(m.weight, r_embed) for m in mods], dim=1)
+                b = torch.zeros(w.shape[0], device=r_embed.device, dtype=torch.float32)
+                for m in mods:
+                    if m.bias is not None:
+                        b = b + m.bias.to(device=r_embed.device, dtype=torch.float32)
+                ws.append(w)
+                bs.append(b)
+                offs[id(blk)] = (off, w.shape[0])
+                off += w.shape[0]
+            if len({w.shape[1] for w in ws}) != 1:          # blocks with different condition lists
+                ent = (key, None, None, offs)
+            else:
+                ent = (key, torch.cat(ws, 0).contiguous(), torch.cat(bs).to(r_embed.dtype).contiguous(), offs)
+            self.__dict__["_ts_fused"] = ent
+        if ent[1] is None or ent[1].shape[1] != r_embed.shape[1]:
+            return None
+        ab = ops.linear(r_embed, ent[1], ent[2])
+        return {k: ab[:, o:o + n] for k, (o, n) in ent[3].items()}
+
+    def _with_ts(self, r_embed):
+        pre = self._ts_mapped(r_embed)
+        if pre is not None:
+            r_embed = r_embed.view_as(r_embed)      # a fresh tensor object carrying the mapped coefficients
+            r_embed._cgs_ts = pre
+        return r_embed
 
     def _run_block(self, block, x, r_embed, clip, skip=None, cnet=None, nxt=None):
         if isinstance(block, ResBlock):
@@ -624,7 +675,7 @@ class StageC(_UNetStage):
 
     def forward(self, x, r, clip_text, clip_text_pooled, clip_img, control=None, **kwargs):
         dt = self.clip_txt_mapper.weight.dtype
-        r_embed = self._r_embed(r, dt, kwargs)
+        r_embed = self._with_ts(self._r_embed(r, dt, kwargs))
         def cond():
             return self.gen_c_embeddings(clip_text.to(dt), clip_text_pooled.to(dt), clip_img.to(dt))
         clip = self._static_cond(kwargs, (clip_text, clip_text_pooled, clip_img), lambda: self._attn_kv(cond()))
@@ -726,7 +777,7 @@ class StageB(_UNetStage):
     def forward(self, x, r, effnet, clip, pixels=None, **kwargs):
         dt = self.clip_mapper.weight.dtype
         pix = pixels if pixels is not None else x.new_zeros(x.shape[0], 3, 8, 8)
-        r_embed = self._r_embed(r, dt, kwargs)
+        r_embed = self._with_ts(self._r_embed(r, dt, kwargs))
         p = self.patch_size
         size = (x.shape[2] // p, x.shape[3] // p)
 

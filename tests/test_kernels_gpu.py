@@ -1179,6 +1179,29 @@ def test_channel_affine_layernorm(cuda, N, H, W, C, dt):
     assert _rel(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("batched", ["1", "0"])
+def test_cascade_timestep_mappers_one_gemm(cuda, batched, monkeypatch):
+    """Stage C with every TimestepBlock's mapper pair from one GEMM per call (TSBATCH) == the per-block
+    mapper GEMMs, vs the fp32 CPU model."""
+    from comfy_gen_server_amd.models import cascade as SC
+    from comfy_gen_server_amd.models.layers import init_random_
+    monkeypatch.setenv("CGS_CASCADE_TSBATCH", batched)
+    cfg = dict(c_in=16, c_out=16, c_r=64, c_cond=128, c_hidden=[128, 256], nhead=[2, 4], blocks=[[1, 2], [2, 1]],
+               block_repeat=[[1, 1], [1, 1]], level_config=["CT", "CTA"], c_clip_text=64, c_clip_text_pooled=64,
+               c_clip_img=768, c_clip_seq=2, switch_level=[False])
+    m = SC.StageC(**cfg)
+    init_random_(m, seed=12)
+    g = torch.Generator().manual_seed(2)
+    args = (torch.randn(2, 16, 8, 8, generator=g), torch.tensor([0.2, 0.9]), torch.randn(2, 7, 64, generator=g),
+            torch.randn(2, 1, 64, generator=g), torch.randn(2, 1, 768, generator=g))
+    with torch.inference_mode():
+        ref = m(*args).float()
+        m = m.to(device=cuda, dtype=torch.bfloat16)
+        out = m(*tuple(a.to(cuda, torch.bfloat16 if a.dim() > 1 else torch.float32) for a in args)).float().cpu()
+    assert ("_ts_fused" in m.__dict__) == (batched == "1")
+    assert _rel(out, ref) < 3e-2
+
+
 @pytest.mark.parametrize("fused", ["1", "0"])
 def test_cascade_stage_affine_layernorm_path(cuda, fused, monkeypatch):
     """Stage C (C-T-A blocks) with the TimestepBlock writing the next AttnBlock's LayerNorm (AFFLN) == the
