@@ -1466,10 +1466,13 @@ _SPLITK = {"sk2v8": (8, 2), "sk4v8": (8, 4), "sk2v10": (10, 2), "sk4v10": (10, 4
 def _splitk_cands(M, N, K, epi, run):
     """Split-K autotune candidates for an under-filled grid (batch-1 shapes: a 128 x 128 grid under two
     workgroups per CU): the K slices multiply the workgroup count, one reduce pass applies the epilogue.
-    Opt-in (CGS_SPLITK=1): measured slower than the best single-pass tile on every SDXL batch-1 shape
-    (profiles/r05/splitk.md -- the fp32 partial round trip costs more than the fuller grid gains)."""
+    Candidates by default from K = 4096 (CGS_SPLITK=1: every K, 0: never): slower than the best single-pass
+    tile on every SDXL batch-1 shape (profiles/r05/splitk.md -- the fp32 partial round trip costs more than
+    the fuller grid gains at K <= 5120), -3.3 % per Cascade batch-1 job on Stage C's K = 8192 ChannelMLP
+    projection (profiles/r05/splitk_cascade.md)."""
+    mode = os.environ.get("CGS_SPLITK", "auto")
     if (epi & ~(EPI_BIAS | EPI_RESIDUAL | EPI_LNFOLD | EPI_GELU)) or N % 8 or not _underfilled(M, N) \
-            or not _native.has_kernel("cgs_gemm_bf16_splitk") or os.environ.get("CGS_SPLITK", "0") != "1":
+            or not _native.has_kernel("cgs_gemm_bf16_splitk") or mode == "0" or (mode != "1" and K < 4096):
         return []
     return [(name, (lambda name=name: run(name))) for name, (_, s) in _SPLITK.items()
             if K % (32 * s) == 0 and K // s >= 256]
