@@ -24,6 +24,9 @@
 #define EPI_BIAS 1
 #define EPI_RESIDUAL 2
 #define CONV_UP2X 16
+#ifndef CGS_CONV_PFE
+#define CGS_CONV_PFE 0   // v6 conv epilogue-operand prefetch (pq::run PFE): off, the peeled K loop spills
+#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -705,8 +708,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   e.gnp = a.gnp;
   e.hw = a.Ho * a.Wo;
-  pq::run<decltype(al), false, DS, GNS>(al, a.w, K, M, a.Cout, K, e, smem, (M + pq::BM - 1) / pq::BM, a.tiles_n,
-                                           a.group_m);
+  pq::run<decltype(al), false, DS, GNS, false, false, false, CGS_CONV_PFE>(al, a.w, K, M, a.Cout, K, e, smem,
+                                                                          (M + pq::BM - 1) / pq::BM, a.tiles_n,
+                                                                          a.group_m);
 }
 
 static int conv_num_cus() {

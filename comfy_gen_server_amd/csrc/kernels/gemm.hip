@@ -819,7 +819,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   e.gnp = gnp;
   e.hw = hw;
   DenseA8 al{A, lda, M, {}};
-  pq::run<DenseA8, LN, 1, 2, false, true, false>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+  pq::run<DenseA8, LN, 1, 2, false, true, false, 0>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
 }
 
 // y = gelu(A W^T + bias) (LN-folded with rs / cs when epi has EPI_LNFOLD) + the sum-of-squares partials:

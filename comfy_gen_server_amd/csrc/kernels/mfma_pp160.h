@@ -26,6 +26,17 @@
 
 namespace pq {
 
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+// Loads the compiler does not track: no s_waitcnt is inserted for their results, so the caller must retire
+// them with its own counted wait before reading the registers (pq::run's epilogue-operand prefetch).
+__device__ __forceinline__ void untracked_load(u32x4v& d, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p));
+}
+__device__ __forceinline__ void untracked_load(u32x2v& d, const void* p) {
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(p));
+}
+
 constexpr int BM = 256, BN = 160, BK = 64;
 constexpr int THREADS = 512;
 constexpr int A_BYTES = BM * 128;
@@ -80,8 +91,10 @@ __device__ __forceinline__ int gg_row160(int r) {
 // and 80-column chunk (one wave's columns), (mean, M2) shifted by the row's first value in the chunk -- into
 // e.gnp as [M][N / 80][2] floats; a LayerNorm over these rows then needs only cgs_ln_rs_from_partials
 // instead of a statistics pass over the tensor. Host: N % 160 == 0.
+// PFE: epilogue operands (bias, LayerNorm-fold statistics, residual) prefetched one K-tile ahead -- see
+// `prefetch` -- (1) or loaded in the epilogue (0: the conv gathers, whose peeled K loop spilled).
 template <class AL, bool LN = false, int DS = 0, int GNS = 0, bool GG = false, bool ACT = false,
-          bool RSO = false>
+          bool RSO = false, int PFE = 1>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   const int tid = threadIdx.x;
@@ -207,17 +220,76 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  // epilogue variants are separate straight-line paths (flags are wave-uniform), so the store-only
-  // path carries no load and hence no vmcnt wait on the next tile's in-flight DMAs
+  // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain;
+  // GEGLU: the weight row of acc[.][j][0] relative to the wave's first column (gg_row160 of staged row 16 j + 4 fq)
+  auto colj = [&](int j) {
+    if constexpr (GG) return gg_row160(grp * 80 + 16 * j + 4 * fq) - grp * 80;
+    return j < 4 ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : 64 + 4 * fq;
+  };
+  const bool hb = (e.flags & MC_EPI_BIAS) != 0, hr = (e.flags & MC_EPI_RESIDUAL) != 0;
+  // Epilogue operands. PFE: loaded right after the counted wait of the unit's second-to-last K-tile, by loads
+  // the compiler does not track. They then sit in the vmcnt queue between the next unit's first K-tile
+  // (issued before them) and its second (issued after), so the last K-tile's own counted wait (wait_tile)
+  // retires them and the epilogue reads registers. Loaded in the epilogue they were younger than both of the
+  // next unit's prefetched K-tiles and waited for all of them (the residual shapes ran 17-23 % slower than
+  // store-only, docs/OPEN_ITEMS.md round 5); compiler-tracked prefetch loads still got a vmcnt(0) (its
+  // wait-count analysis does not credit the counted waits behind the per-group LDS-DMAs).
+  u32x2v pbias[5];
+  u32x4v pcs[5];
+  u32x2v prs[4];
+  u32x4v prw4[4][2];
+  u32x2v prw2[4];
+  auto prefetch = [&](int m0, int n0, bool hb, bool hr) {
+    const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
+    if (hb) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        int col = n_w + colj(j);
+        col = col < N ? col : N - 4;
+        if constexpr (PFE) untracked_load(pbias[j], e.bias + col);
+        else pbias[j] = *reinterpret_cast<const u32x2v*>(e.bias + col);
+      }
+    }
+    if constexpr (LN) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        int col = n_w + colj(j);
+        col = col < N ? col : N - 4;
+        if constexpr (PFE) untracked_load(pcs[j], e.cs + col);
+        else pcs[j] = *reinterpret_cast<const u32x4v*>(e.cs + col);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int row = m_w + 16 * i + fr;
+        row = row < M ? row : M - 1;
+        if constexpr (PFE) untracked_load(prs[i], e.rs + 2 * (long long)row);
+        else prs[i] = *reinterpret_cast<const u32x2v*>(e.rs + 2 * (long long)row);
+      }
+    } else if (hr) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int row = m_w + 16 * i + fr;
+        row = row < M ? row : M - 1;
+        const u16* rrow = e.R + (long long)row * e.ldr;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          int col = n_w + 32 * p + 8 * fq;
+          col = col < N ? col : N - 8;
+          if constexpr (PFE) untracked_load(prw4[i][p], rrow + col);
+          else prw4[i][p] = *reinterpret_cast<const u32x4v*>(rrow + col);
+        }
+        int col = n_w + 64 + 4 * fq;
+        col = col < N ? col : N - 4;
+        if constexpr (PFE) untracked_load(prw2[i], rrow + col);
+        else prw2[i] = *reinterpret_cast<const u32x2v*>(rrow + col);
+      }
+    }
+  };
+  // epilogue variants are separate straight-line paths (flags are wave-uniform)
   auto epilogue_t = [&](int m0, int n0, auto has_bias_c, auto has_res_c) {
     constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
     const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
-    // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain;
-    // GEGLU: the weight row of acc[.][j][0] relative to n_w (gg_row160 of staged row 16 j + 4 fq)
-    auto colj = [&](int j) {
-      if constexpr (GG) return gg_row160(grp * 80 + 16 * j + 4 * fq) - grp * 80;
-      return j < 4 ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : 64 + 4 * fq;
-    };
+    if constexpr (PFE == 0) prefetch(m0, n0, HB, HR);
     // column tile 4 (8 B per lane and row): row blocks i / i+1 are paired with v_permlane16_swap so a
     // lane stores 16 B (fq even: row block i, cols 64 + 8 (fq / 2) .. + 7; fq odd: row block i + 1)
     auto store_t4 = [&](int i, uint2 a, uint2 b) {
@@ -230,25 +302,17 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     };
     float4 bv[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      int col = n_w + colj(j);
-      col = col < N ? col : N - 4;
-      bv[j] = HB ? unpack4_bf16(*reinterpret_cast<const uint2*>(e.bias + col)) : float4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int j = 0; j < 5; ++j) bv[j] = HB ? unpack4_bf16(uint2{pbias[j].x, pbias[j].y}) : float4{0.f, 0.f, 0.f, 0.f};
     if constexpr (LN) {
       // LayerNorm folded in (MC_EPI_LNFOLD, see mfma_ppk.h): acc = rstd_r * (acc - mean_r * cs[c])
       float4 cv[5];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        int col = n_w + colj(j);
-        col = col < N ? col : N - 4;
-        cv[j] = *reinterpret_cast<const float4*>(e.cs + col);
-      }
+      for (int j = 0; j < 5; ++j)
+        cv[j] = float4{__uint_as_float(pcs[j].x), __uint_as_float(pcs[j].y), __uint_as_float(pcs[j].z),
+                       __uint_as_float(pcs[j].w)};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        int row = m_w + 16 * i + fr;
-        row = row < M ? row : M - 1;
-        const float2 st = *reinterpret_cast<const float2*>(e.rs + 2 * (long long)row);
+        const float2 st = float2{__uint_as_float(prs[i].x), __uint_as_float(prs[i].y)};
         const float mr = st.x * st.y;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -259,23 +323,16 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         }
       }
     }
-    uint2 rw[4][5];   // residual words, all loads issued before the first store (one wait)
+    uint2 rw[4][5];   // residual words
     if (HR) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        int row = m_w + 16 * i + fr;
-        row = row < M ? row : M - 1;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-          int col = n_w + 32 * p + 8 * fq;
-          col = col < N ? col : N - 8;
-          const uint4 q4 = *reinterpret_cast<const uint4*>(e.R + (long long)row * e.ldr + col);
-          rw[i][2 * p] = uint2{q4.x, q4.y};
-          rw[i][2 * p + 1] = uint2{q4.z, q4.w};
+          rw[i][2 * p] = uint2{prw4[i][p].x, prw4[i][p].y};
+          rw[i][2 * p + 1] = uint2{prw4[i][p].z, prw4[i][p].w};
         }
-        int col = n_w + 64 + 4 * fq;
-        col = col < N ? col : N - 4;
-        rw[i][4] = *reinterpret_cast<const uint2*>(e.R + (long long)row * e.ldr + col);
+        rw[i][4] = uint2{prw2[i].x, prw2[i].y};
       }
     }
     auto val = [&](int i, int j) {
@@ -451,7 +508,6 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   };
   using T0 = std::false_type;
   using T1 = std::true_type;
-  const bool hb = (e.flags & MC_EPI_BIAS) != 0, hr = (e.flags & MC_EPI_RESIDUAL) != 0;
   auto epilogue = [&](int m0, int n0) {
     if constexpr (LN) {                     // folded LayerNorm: no residual form (host-checked)
       if (hb) epilogue_t(m0, n0, T1{}, T0{});
@@ -487,7 +543,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
+    // one K-tile; PF: the unit's second-to-last, which issues the epilogue-operand prefetch after its counted wait
+    auto ktile = [&](int kt, bool PF) {
       const unsigned char* S = smem + slot * STAGE;
       const int slot2 = slot >= 1 ? slot - 1 : 2;      // (slot + 2) % 3
       // phase 0: fragments k 0..31; DMA the K-tile two ahead in the stream into the slot vacated
@@ -510,11 +567,19 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       read_frags(S, 1);
       if constexpr ((DS & 4) == 0) stage_part(1, kst, slot2);
       wait_tile();
+      if (PFE && PF) prefetch(m0, n0, hb, hr);
       pp::wait_lgkm0();
       pp::barrier();
       mma();
       pp::barrier();
       slot = slot == 2 ? 0 : slot + 1;
+    };
+    if constexpr (PFE) {   // the last two K-tiles peeled: the prefetched registers live only from there on
+      for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, false);
+      ktile(nk - 2, true);
+      ktile(nk - 1, false);
+    } else {
+      for (int kt = 0; kt < nk; ++kt) ktile(kt, false);
     }
     epilogue(m0, n0);
     if (!has_next) break;

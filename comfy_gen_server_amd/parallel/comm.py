@@ -23,6 +23,16 @@ import torch
 import torch.distributed as dist
 
 
+# ``Comm.broadcast_state_dict`` on a receiving rank when the source's checkpoint is not a flat
+# {name: tensor} dict (nested upscaler ``.pth`` files, A1111 hypernetworks, PhotoMaker ``.bin``): no table
+# can describe it, so every rank reads the file itself.
+LOAD_LOCALLY = object()
+
+
+def is_flat_tensor_dict(sd) -> bool:
+    return isinstance(sd, dict) and all(isinstance(k, str) and torch.is_tensor(v) for k, v in sd.items())
+
+
 class Comm:
     def __init__(self):
         self.rank = 0
@@ -116,19 +126,26 @@ class Comm:
         table over the control group, then the tensors in same-dtype buckets over the data plane (RCCL over
         xGMI on the GPU); the other ranks allocate and receive them on ``device`` without touching the file.
         ``sd`` is None on the receivers. An exception object in place of ``sd`` on ``src`` is re-raised on
-        every rank (a failed load fails the node everywhere)."""
+        every rank (a failed load fails the node everywhere). A source dict that is not flat
+        (``is_flat_tensor_dict``) is not sent: the receivers get ``LOAD_LOCALLY`` and read the file
+        themselves."""
         if not self.enabled:
             return sd
         if self.rank == src:
             if isinstance(sd, BaseException):
                 self.broadcast_object({"error": f"{type(sd).__name__}: {sd}"}, src=src)
                 raise sd
+            if not is_flat_tensor_dict(sd):
+                self.broadcast_object({"local": True}, src=src)
+                return sd
             table = [(k, tuple(v.shape), str(v.dtype).replace("torch.", "")) for k, v in sd.items()]
             self.broadcast_object({"table": table}, src=src)
         else:
             msg = self.broadcast_object(None, src=src)
             if "error" in msg:
                 raise RuntimeError(f"checkpoint load failed on rank {src}: {msg['error']}")
+            if msg.get("local"):
+                return LOAD_LOCALLY
             table = msg["table"]
             sd = {k: torch.empty(shape, dtype=getattr(torch, dt), device=device) for k, shape, dt in table}
         xdev = self.device if self.backend == "nccl" else torch.device("cpu")

@@ -71,7 +71,10 @@ class SPMD:
 
     def load_state_dict(self, path, device, return_metadata, load_local):
         """R3 inside an SPMD prompt: rank 0 reads the checkpoint, every other rank of the prompt receives
-        it (``Comm.broadcast_state_dict``) -- one disk read per node. A failed read fails every rank."""
+        it (``Comm.broadcast_state_dict``) -- one disk read per node. A failed read fails every rank. A
+        checkpoint that is not a flat tensor dict (nested ``.pth`` upscalers, hypernetworks, ``.bin``
+        files) is read by every rank itself."""
+        from ..parallel.comm import LOAD_LOCALLY, is_flat_tensor_dict
         comm = self.comm
         if self.rank == 0:
             try:
@@ -81,10 +84,12 @@ class SPMD:
                 raise
             sd, meta = res if return_metadata else (res, None)
             comm.broadcast_state_dict(sd, device)
-            if return_metadata:
+            if return_metadata and is_flat_tensor_dict(sd):
                 comm.broadcast_object(meta)
         else:
             sd = comm.broadcast_state_dict(None, device)
+            if sd is LOAD_LOCALLY:
+                return load_local()
             meta = comm.broadcast_object(None) if return_metadata else None
             self.loads_received += 1
         return (sd, meta) if return_metadata else sd

@@ -6,6 +6,10 @@ configurations (env flags set before each job; captured graph plans dropped on e
 re-captured in an untimed job), and the median wall time per configuration is reported.
 
 python -m comfy_gen_server_amd.tools.ab_bench --cfg "base:" --cfg "noskip:CGS_SKIPCAT=0" [--rounds 3]
+
+``CGS_LIB=<path>`` in a configuration runs it on another build of libcgs_kernels.so (e.g. the previous
+commit's, ``tools/build_rev_lib.sh HEAD``): the ops fetch the library handle per call, so the switch is a
+handle swap inside the same process.
 """
 from __future__ import annotations
 
@@ -25,6 +29,23 @@ _NATIVE_KNOBS = {"CGS_TILE_GROUP": ("cgs_set_tile_group", 4), "CGS_CONV_TILE_GRO
                  "CGS_GRN_ROWS": ("cgs_grn_set_rows", 1)}
 
 
+_LIBS: dict = {}
+
+
+def _use_lib(path):
+    """Make `path` (None: the in-tree build) the kernel library every op launches from."""
+    from .. import _native
+    if "" not in _LIBS:
+        _LIBS[""] = _native.load_kernels()
+    key = os.path.abspath(path) if path else ""
+    if key not in _LIBS:
+        import ctypes
+        lib = ctypes.CDLL(key, mode=ctypes.RTLD_LOCAL)
+        _native._declare(lib)
+        _LIBS[key] = lib
+    _native._kernels = _LIBS[key]
+
+
 def _apply(env: dict, saved: dict):
     for k in saved:
         if saved[k] is None:
@@ -34,6 +55,7 @@ def _apply(env: dict, saved: dict):
     for k, v in env.items():
         os.environ[k] = v
     from .. import _native
+    _use_lib(os.environ.get("CGS_LIB") or None)
     lib = _native.load_kernels()
     for k, (fn, dflt) in _NATIVE_KNOBS.items():
         if lib is not None and _native.has_kernel(fn):

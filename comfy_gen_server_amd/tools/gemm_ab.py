@@ -3,6 +3,7 @@ non-persistent, 256x160 -- vs the 8-wave v6 / v7 kernels vs hipBLASLt through AT
 check of every HIP variant.
 
 python -m comfy_gen_server_amd.tools.gemm_ab [out.md] [--rounds R] [--iters N] [--shapes a,b,...] [--v6modes 1,65]
+    [--cmp path/to/other/libcgs_kernels.so]
 
 ``--v6modes``: extra columns "v6m<m>" = v6 under cgs_v6_set_mode(m) (pq::run DS bits; 64 / 128 = A / B DMAs
 through buffer descriptors), interleaved with the others in the same rounds.
@@ -58,6 +59,7 @@ def main(argv):
     rounds, iters, only = 3, 10, None
     v6modes = []
     out_md = None
+    cmp_path = None
     i = 0
     while i < len(argv):
         if argv[i] == "--rounds":
@@ -66,12 +68,19 @@ def main(argv):
             iters = int(argv[i + 1]); i += 2
         elif argv[i] == "--shapes":
             only = set(argv[i + 1].split(",")); i += 2
+        elif argv[i] == "--cmp":     # another build of the library: its v6 / v7 as columns v6b / v7b
+            cmp_path = argv[i + 1]; i += 2
         elif argv[i] == "--v6modes":
             v6modes = [int(v) for v in argv[i + 1].split(",")]; i += 2
         else:
             out_md = argv[i]; i += 1
     lib = _native.load_kernels()
     assert lib is not None, _native.kernels_error()
+    lib2 = None
+    if cmp_path:
+        import ctypes
+        lib2 = ctypes.CDLL(cmp_path, mode=ctypes.RTLD_LOCAL)
+        _native._declare(lib2)
     dev = torch.device("cuda", 0)
     stream = core._stream()
     rows = ["| shape | M | N | K | epi | w6 TF/s | w6 non-persistent | w6 256x160 | v6 TF/s | v7 TF/s | hipBLASLt TF/s "
@@ -114,7 +123,7 @@ def main(argv):
         csp = None if cs is None else cs.data_ptr()
         rsp = None if rs is None else rs.data_ptr()
 
-        def var(v):
+        def var(v, lib=lib):
             def f():
                 if ln:
                     e = lib.cgs_gemm_bf16_lnfold_v(a.data_ptr(), w_run.data_ptr(), out.data_ptr(), b_run.data_ptr(),
@@ -143,6 +152,11 @@ def main(argv):
             f = var(v)
             if f() == 0:
                 cands[vn] = f
+        if lib2 is not None:
+            for vn, v in (("v6b", 6), ("v7b", 7)):
+                f = var(v, lib2)
+                if f() == 0:
+                    cands[vn] = f
         for m in v6modes:
             def fm(m=m, f6=var(6)):
                 lib.cgs_v6_set_mode(m)
