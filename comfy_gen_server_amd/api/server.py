@@ -218,12 +218,12 @@ class PromptServer:
                     filename = f"{stem} ({i}){ext}"
                     filepath = os.path.join(full_output_folder, filename)
                     i += 1
-            os.makedirs(full_output_folder, exist_ok=True)
-            if image_save_function is not None:
+            if image_save_function is not None:     # validates its reference first; creates the folder itself
                 err = image_save_function(image, post, filepath)
                 if err is not None:
                     return err
             else:
+                os.makedirs(full_output_folder, exist_ok=True)
                 with open(filepath, "wb") as f:
                     f.write(image.file.read())
             return web.json_response({"name": filename, "subfolder": subfolder, "type": image_upload_type})
@@ -271,6 +271,7 @@ class PromptServer:
                     original_pil = original_pil.convert("RGBA")
                     mask_pil = Image.open(image.file).convert("RGBA")
                     original_pil.putalpha(mask_pil.getchannel("A"))
+                    os.makedirs(os.path.dirname(filepath), exist_ok=True)   # only once the reference checked out
                     original_pil.save(filepath, compress_level=4, pnginfo=metadata)
                 return None
             return image_upload(post, image_save_function)
@@ -406,7 +407,8 @@ class PromptServer:
                 c = self.cluster
                 stats["cluster"] = {"world": c.world, "generation": c.gen, "regroups": c.regroups,
                                     "dead": sorted(c.dead), "busy": {str(r): p for r, p in dict(c.busy).items()},
-                                    "spmd_sizes": sorted(c.ctxs)}
+                                    "spmd_sizes": sorted(c.ctxs), "regroup_failures": getattr(c, "regroup_failures", 0),
+                                    "replaced": dict(getattr(c, "_respawns", {})), "groups_ok": getattr(c, "groups_ok", True)}
             return web.json_response(stats)
 
         @routes.get("/prompt")

@@ -1141,6 +1141,12 @@ CGS_EXPORT int cgs_gemm_bf16_w6(const void* A, const void* W, void* C, const voi
                                 hipStream_t stream);
 constexpr int kVariantW6 = 16, kVariantW6n160 = 17;
 
+// w6's pointer alignment (cgs_gemm_bf16_w6 returns hipErrorInvalidValue otherwise)
+static bool w6_ptrs_ok(const void* A, const void* W, const void* C, const void* bias, const void* R, int epi) {
+  return ((uintptr_t)A | (uintptr_t)W | (uintptr_t)C) % 16 == 0 && (!(epi & EPI_RESIDUAL) || (uintptr_t)R % 16 == 0) &&
+         (!(epi & EPI_BIAS) || (uintptr_t)bias % 16 == 0);
+}
+
 static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                          long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                          int variant, hipStream_t stream, void* ws = nullptr, long long ws_bytes = 0) {
@@ -1186,10 +1192,13 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
     return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
   }
   if (variant == kVariantW6 || variant == kVariantW6n160) {
+    // a table choice made by shape: a call outside w6's stride / alignment domain (16-B bias / residual
+    // pointers, views with lda != K) runs on the auto path instead of failing
     const int bn = variant == kVariantW6 ? 256 : 160;
-    if (!cgs_gemm_w6_ok(M, N, K, lda, ldw, ldc, ldr, epi, bn)) return (int)hipErrorInvalidValue;
-    return cgs_gemm_bf16_w6(A, W, C, bias, R, nullptr, nullptr, M, N, K, lda, ldw, ldc, ldr, epi, alpha, 0, 4, 0, bn,
-                            stream);
+    if (cgs_gemm_w6_ok(M, N, K, lda, ldw, ldc, ldr, epi, bn) && w6_ptrs_ok(A, W, C, bias, R, epi))
+      return cgs_gemm_bf16_w6(A, W, C, bias, R, nullptr, nullptr, M, N, K, lda, ldw, ldc, ldr, epi, alpha, 0, 4, 0,
+                              bn, stream);
+    variant = -1;
   }
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && (!(epi & EPI_GEGLU) || (N % 160 == 0 && !(epi & EPI_RESIDUAL))) &&
       ((uintptr_t)bias % 8 == 0))
@@ -1275,11 +1284,12 @@ static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, 
     return gemm_v8_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream,
                           variant < 0 ? 8 : variant, rs, cs);
   }
-  if (variant == kVariantW6 || variant == kVariantW6n160) {
+  if (variant == kVariantW6 || variant == kVariantW6n160) {    // outside w6's domain: the v6 / v7 choice below
     const int bn = variant == kVariantW6 ? 256 : 160;
-    if (!cgs_gemm_w6_ok(M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, bn)) return (int)hipErrorInvalidValue;
-    return cgs_gemm_bf16_w6(A, W, C, bias, nullptr, rs, cs, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, 0, 4, 0,
-                            bn, stream);
+    if (cgs_gemm_w6_ok(M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, bn) && w6_ptrs_ok(A, W, C, bias, nullptr, epi))
+      return cgs_gemm_bf16_w6(A, W, C, bias, nullptr, rs, cs, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, 0, 4,
+                              0, bn, stream);
+    variant = -1;
   }
   // v6 (256x160) for the N = 640 / 1280 projections (the cross-attention query), v7 otherwise
   if (variant == 8 || (variant >= 10 && variant <= 14))

@@ -127,20 +127,32 @@ def full_type_name(klass):
     return klass.__qualname__ if m == "builtins" else m + "." + klass.__qualname__
 
 
-def _jsonable(v):
-    """Best-effort JSON for the Yjs output map (tensors -> shape summary, bytes -> hex prefix)."""
+def _jsonable(v, total=None):
+    """Best-effort JSON for the Yjs output map (tensors -> shape summary, bytes -> size). A batch split over
+    the ranks of an SPMD prompt (a LATENT with ``dp_shard``, an IMAGE carrying the shard mark) is described
+    as the whole batch -- the value one GPU running the prompt whole would publish -- not as this rank's shard."""
     try:
         json.dumps(v)
         return v
     except TypeError:
         pass
     if isinstance(v, torch.Tensor):
-        return {"tensor": list(v.shape), "dtype": str(v.dtype)}
+        shape = list(v.shape)
+        sh = getattr(v, "_cgs_dp_shard", None)
+        if sh is not None and shape:
+            shape[0] = int(sh[2])
+        elif total is not None and shape:
+            shape[0] = int(total)
+        return {"tensor": shape, "dtype": str(v.dtype)}
     if isinstance(v, (bytes, bytearray)):
         return {"bytes": len(v)}
     if isinstance(v, (list, tuple)):
         return [_jsonable(x) for x in v]
     if isinstance(v, dict):
+        if "dp_shard" in v:
+            off, n, tot = v["dp_shard"]
+            return {str(k): _jsonable(x, tot if (torch.is_tensor(x) and x.dim() and x.shape[0] == n) else None)
+                    for k, x in v.items() if k != "dp_shard"}
         return {str(k): _jsonable(x) for k, x in v.items()}
     return str(v)
 

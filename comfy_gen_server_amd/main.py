@@ -52,6 +52,10 @@ def apply_args(args):
     if os.environ.get("CGS_REGISTER_TINY") == "1":     # tests: the tiny synthetic family's checkpoints load
         from .tools.synth import register_tiny_family
         register_tiny_family()
+    from .nodes import helpers as NH
+    pm = getattr(args, "preview_method", None)
+    NH.set_flags(preview_method=getattr(pm, "value", pm) or "none",
+                 disable_metadata=bool(getattr(args, "disable_metadata", False)))
     if args.cpu:
         dm.set_cpu_mode(True)
     elif args.cuda_device is not None:

@@ -187,11 +187,17 @@ def attention(q, k, v, heads, mask=None, causal=False, key_padding=None):
     rows = max(1, min(Sq, SCORE_BUDGET // max(1, heads * ld)))
     s = torch.empty((heads, rows, ld), device=q.device, dtype=F32)
     full_mask = None
-    if mask is not None:
-        full_mask = mask.to(F32)
+    if mask is not None:     # normalised as attention_reference does: bool keep-mask -> 0 / -inf,
+        m = mask               # [Sq, Sk] -> [1, 1, Sq, Sk], [B, Sq, Sk] -> [B, 1, Sq, Sk]
+        if m.dtype == torch.bool:
+            m = torch.zeros(m.shape, device=m.device, dtype=F32).masked_fill(~m, float("-inf"))
+        full_mask = m.to(F32)
         while full_mask.dim() < 4:
-            full_mask = full_mask.unsqueeze(0)
-        full_mask = full_mask.expand(B, heads, Sq, Sk)
+            full_mask = full_mask.unsqueeze(0) if full_mask.dim() < 3 else full_mask.unsqueeze(1)
+        try:
+            full_mask = full_mask.expand(B, heads, Sq, Sk)
+        except RuntimeError:
+            return None
     scale = 1.0 / math.sqrt(D)
     for b in range(B):
         for r0 in range(0, Sq, rows):

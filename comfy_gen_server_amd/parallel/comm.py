@@ -200,16 +200,38 @@ class Comm:
         self.subsets[self.world] = self
         return self.subsets
 
-    def reinit(self, port: int, gen: int, addr: str = "127.0.0.1", timeout_s: float = 600.0):
-        """Re-rendezvous after a rank death: leave the broken process group (a member is gone, so its
-        collectives can never complete) and join generation ``gen`` over a fresh TCPStore on ``port``
-        (hosted by rank 0), together with the survivors and the respawned rank. Never re-execs the
-        process (the GPU context stays)."""
-        if dist.is_initialized():
+    def leave(self, timeout_s: float = 60.0) -> bool:
+        """Tear down the process group (after a rank death its collectives can never complete), bounded:
+        the teardown runs on a helper thread and this returns False if it has not finished within
+        ``timeout_s`` -- an RCCL communicator with a dead peer can block in its destructor. The caller then
+        replaces the process (a worker exits non-zero and the coordinator spawns a fresh child; nothing
+        re-execs a process that touched the GPU). True when there was nothing to tear down."""
+        import threading
+        from ..utils.telemetry import maybe_fault
+        if not dist.is_initialized():
+            self.subsets = {}
+            return True
+        err = []
+
+        def teardown():
             try:
+                maybe_fault("teardown", str(self.rank))
                 dist.destroy_process_group()
-            except Exception:        # pragma: no cover - a broken group may not tear down cleanly
-                pass
+            except Exception as ex:  # noqa: BLE001 - a broken group may not tear down cleanly
+                err.append(ex)
+        t = threading.Thread(target=teardown, name="cgs-pg-teardown", daemon=True)
+        t.start()
+        t.join(timeout_s)
+        if t.is_alive():
+            return False
+        self.subsets = {}
+        self.group = None
+        self.ctrl = None
+        return True
+
+    def join(self, port: int, gen: int, addr: str = "127.0.0.1", timeout_s: float = 600.0):
+        """Join process-group generation ``gen`` over a fresh TCPStore on ``port`` (hosted by rank 0), with
+        every other rank of the node (survivors and respawned ranks alike)."""
         self.degraded = False
         self.gen = gen
         self.group = None
@@ -223,6 +245,14 @@ class Comm:
         self.ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s)) \
             if self.backend == "nccl" else None
         return self
+
+    def reinit(self, port: int, gen: int, addr: str = "127.0.0.1", timeout_s: float = 600.0,
+               teardown_timeout_s: float = 60.0):
+        """Re-rendezvous after a rank death: ``leave`` (bounded) then ``join`` generation ``gen``. Raises
+        ``TimeoutError`` if the teardown does not finish."""
+        if not self.leave(teardown_timeout_s):
+            raise TimeoutError(f"rank {self.rank}: process-group teardown did not finish in {teardown_timeout_s} s")
+        return self.join(port, gen, addr, timeout_s)
 
     def all_gather(self, t):
         """Concatenate ``t`` (same shape on every rank) along dim 0 across ranks."""

@@ -15,7 +15,10 @@ Per queued prompt the coordinator picks a mode (``choose_mode``):
 
 Transport: JSON messages over ``multiprocessing.connection`` (authenticated local socket) -- run
 requests and interrupts down, WS events and completions up. Rank 0 forwards a worker's events to the
-submitting client (``sid``); binary preview frames of remote ranks are not forwarded.
+submitting client (``sid``): JSON events as they are; binary frames (latent previews, ``SaveImageWebsocket``
+images) encoded on the worker and shipped as ``op: "binary"`` (base64 of the frame payload); writes to the
+Yjs ``outputs`` map as ``op: "yjs"`` / ``"yjs_flush"``, applied to rank 0's map and broadcast from there
+(reference ``main.py:152-160``, ``server.py:754-791`` / ``:825-832``, ``execution.py:334-345``).
 
 Ranks keep one executor for single prompts (its own cross-prompt cache) and one per SPMD rank prefix
 [0, k) (k = the powers of two below N, and N): a prefix's executor only sees that prefix's prompts, so
@@ -23,11 +26,18 @@ its caches stay identical on its members and they all reach the same collectives
 SPMD on the largest prefix <= b while the other ranks keep serving single prompts; an SPMD prompt waits
 only for its own ranks.
 
+Scheduling: the dispatch loop never runs a prompt itself. A single prompt goes to an idle rank (workers
+first); an SPMD prompt reserves its prefix in queue order and runs on its own thread once those ranks are
+idle, while the loop keeps handing single prompts to the ranks outside the prefix (reserved ranks take
+none, so a waiting SPMD prompt is not starved).
+
 Elastic: a worker whose connection drops is marked dead -- its single prompt re-runs on a survivor, an
 SPMD prompt it was part of re-runs on the prefix below it (shards re-queued to the surviving GPUs,
-SURVEY §5.3) -- and a replacement process is started. Once it has connected and no rank is busy, every
-rank leaves the broken process group and rendezvouses again (``Comm.reinit``, generation + 1), and the
-node is whole. Nothing re-execs a process that touched the GPU.
+SURVEY §5.3) -- and a replacement process is started. Once it has connected and no rank is busy, a
+re-rendezvous runs on its own thread, all or nothing: every rank leaves the broken process group (bounded:
+a worker whose teardown hangs exits and is replaced), and only if all left cleanly does every rank join
+generation + 1. Until it succeeds prompts run single (any live rank). Nothing re-execs a process that
+touched the GPU.
 """
 from __future__ import annotations
 
@@ -146,9 +156,38 @@ def choose_mode(prompt: dict, extra_data: dict | None, world: int, latency_defau
 # ------------------------------------------------------------------------------------------------
 # worker side
 # ------------------------------------------------------------------------------------------------
+PREVIEW_IMAGE, UNENCODED_PREVIEW_IMAGE = 1, 2     # api.server.BinaryEventTypes (the WS binary frame types)
+
+
+def encode_preview(image_data) -> bytes:
+    """(image type, PIL image, max size) -> the PREVIEW_IMAGE payload: a big-endian image-type word (1 JPEG,
+    2 PNG) and the encoded image, as ``PromptServer.send_image`` frames it."""
+    import io
+    import struct
+    from PIL import Image
+    image_type, image, max_size = image_data
+    if max_size is not None:
+        image = image.copy()
+        image.thumbnail((max_size, max_size), Image.LANCZOS if hasattr(Image, "LANCZOS") else Image.Resampling.LANCZOS)
+    bio = io.BytesIO()
+    bio.write(struct.pack(">I", 2 if image_type == "PNG" else 1))
+    image.save(bio, format=image_type, quality=95, compress_level=1)
+    return bio.getvalue()
+
+
+class RemoteOutputMap:
+    """Worker-side stand-in for the server's Yjs ``outputs`` map: writes go up to rank 0, whose map holds
+    the node's state and broadcasts it (``yjs_flush``)."""
+
+    def __init__(self, server):
+        self.server = server
+
+    def set(self, key, value):
+        self.server._up({"op": "yjs", "key": key, "value": value})
+
+
 class RemoteServer:
-    """Worker-side stand-in for ``PromptServer``: WS events go up to rank 0."""
-    output_map = None
+    """Worker-side stand-in for ``PromptServer``: WS events (JSON and binary) and Yjs writes go up to rank 0."""
 
     def __init__(self, conn, lock):
         self.conn, self.lock = conn, lock
@@ -156,20 +195,30 @@ class RemoteServer:
         self.last_node_id = None
         self.last_prompt_id = None
         self.metrics = {}
+        self.output_map = RemoteOutputMap(self)
 
-    def send_sync(self, event, data, sid=None):
-        if not isinstance(event, str):        # binary preview frames stay local
-            return
+    def _up(self, msg):
         try:
-            send_msg(self.conn, {"op": "event", "event": event, "data": data, "sid": sid}, self.lock)
+            send_msg(self.conn, msg, self.lock)
         except (OSError, EOFError):
             pass
+
+    def send_sync(self, event, data, sid=None):
+        if isinstance(event, str):
+            self._up({"op": "event", "event": event, "data": data, "sid": sid})
+            return
+        import base64
+        if event == UNENCODED_PREVIEW_IMAGE:    # encoded here: the worker's CPU, not rank 0's, pays for it
+            event, data = PREVIEW_IMAGE, encode_preview(data)
+        if isinstance(data, (bytes, bytearray)):
+            self._up({"op": "binary", "event": int(event), "data": base64.b64encode(bytes(data)).decode("ascii"),
+                      "sid": sid})
 
     def queue_updated(self):
         pass
 
     def broadcast_yjs_updates(self):
-        pass
+        self._up({"op": "yjs_flush"})
 
 
 def _forward_progress(server):
@@ -180,6 +229,8 @@ def _forward_progress(server):
         dm.throw_exception_if_processing_interrupted()
         server.send_sync("progress", {"value": value, "max": total, "prompt_id": server.last_prompt_id,
                                       "node": server.last_node_id}, server.client_id)
+        if preview_image is not None:
+            server.send_sync(UNENCODED_PREVIEW_IMAGE, preview_image, server.client_id)
     progress.set_progress_bar_global_hook(hook)
 
 
@@ -250,15 +301,29 @@ def worker_main(comm, address, authkey: bytes, respawned: bool = False):
         op = m.get("op")
         if op == "stop":
             break
-        if op == "regroup":           # re-rendezvous after a rank death (generation m["gen"])
+        if op == "exit":              # the coordinator replaces this process (its group state is unknown)
+            break
+        if op == "teardown":          # re-rendezvous, phase 1: leave the broken process group (bounded)
+            ctxs.clear()
+            ex_spmd.clear()
+            ok = comm.leave(float(m.get("timeout", TEARDOWN_TIMEOUT_S)))
+            send_msg(conn, {"op": "torn_down", "rank": comm.rank, "gen": int(m["gen"]), "ok": ok}, lock)
+            if not ok:                # a teardown that hangs: this process is replaced by a fresh child
+                logging.error("rank %d: process-group teardown hung; exiting for a replacement", comm.rank)
+                try:
+                    conn.close()
+                finally:
+                    os._exit(75)
+            continue
+        if op == "join":              # phase 2: every rank left cleanly -> join generation m["gen"]
             ok, err = True, ""
             try:
-                comm.reinit(int(m["port"]), int(m["gen"]), timeout_s=float(m.get("timeout", 120.0)))
+                comm.join(int(m["port"]), int(m["gen"]), timeout_s=float(m.get("timeout", REGROUP_TIMEOUT_S)))
                 build()
-            except Exception as ex:    # noqa: BLE001 - reported; the coordinator keeps the node degraded
-                logging.exception("rank %d: regroup failed", comm.rank)
+            except Exception as ex:    # noqa: BLE001 - reported; the coordinator replaces this rank
+                logging.exception("rank %d: joining generation %s failed", comm.rank, m.get("gen"))
                 ok, err = False, str(ex)
-            send_msg(conn, {"op": "regrouped", "rank": comm.rank, "gen": int(m["gen"]), "ok": ok, "error": err}, lock)
+            send_msg(conn, {"op": "joined", "rank": comm.rank, "gen": int(m["gen"]), "ok": ok, "error": err}, lock)
             continue
         if op == "free":              # POST /free forwarded by rank 0 (same order as the prompts)
             if m.get("unload_models") or m.get("free_memory"):
@@ -312,6 +377,7 @@ def worker_main(comm, address, authkey: bytes, respawned: bool = False):
 MAX_RESPAWNS = 3              # per rank: a rank that keeps dying stays dead
 SPMD_WAIT_LOG_S = 30.0        # an SPMD prompt waiting this long for its ranks to go idle is logged
 REGROUP_TIMEOUT_S = 120.0
+TEARDOWN_TIMEOUT_S = float(os.environ.get("CGS_TEARDOWN_TIMEOUT_S", "30"))
 
 
 class Coordinator:
@@ -340,10 +406,15 @@ class Coordinator:
         self._retries: dict = {}      # prompt id -> re-runs after a rank death
         self._respawns: dict = {}     # rank -> respawns so far
         self._spawned: dict = {}      # rank -> replacement process not yet in the process group
-        self._regroup_acks: dict = {}
+        self._acks: dict = {}         # (op, rank) -> a worker's re-rendezvous acknowledgement
         self.procs: list = []         # replacement processes (the launcher owns the first ones)
         self.gen = 0
         self.regroups = 0
+        self.regroup_failures = 0
+        self.regrouping = False       # a re-rendezvous is running (its own thread): workers take no prompts
+        self.groups_ok = True         # every rank is in the current generation's process groups (SPMD allowed)
+        self._spmd_queue: list = []   # waiting SPMD prompts in arrival order: {"members": set of ranks}
+        self._started: dict = {}      # prompt id -> wall time its rank(s) were assigned
         self._last_gc, self._need_gc = time.perf_counter(), False
         self._accepted = threading.Condition()
         threading.Thread(target=self._accept_loop, daemon=True).start()
@@ -407,9 +478,19 @@ class Coordinator:
             op = m.get("op")
             if op == "event":
                 self.server.send_sync(m["event"], m["data"], m.get("sid"))
-            elif op == "regrouped":
+            elif op == "binary":
+                import base64
+                self.server.send_sync(int(m["event"]), base64.b64decode(m["data"]), m.get("sid"))
+            elif op == "yjs":
+                om = getattr(self.server, "output_map", None)
+                if om is not None:
+                    om.set(m["key"], m["value"])
+            elif op == "yjs_flush":
+                if getattr(self.server, "output_map", None) is not None:
+                    self.server.broadcast_yjs_updates()
+            elif op in ("torn_down", "joined"):
                 with self.cv:
-                    self._regroup_acks[r] = m
+                    self._acks[(op, r)] = m
                     self.cv.notify_all()
             elif op == "done":
                 with self.cv:
@@ -476,46 +557,112 @@ class Coordinator:
             return
         self.procs.append(p)
         self._spawned[r] = p
+        _LAUNCH.setdefault("procs", {})[r] = p
         logging.warning("respawned rank %d (pid %d)", r, p.pid)
 
-    def _maybe_regroup(self):
-        """Every dead rank has a connected replacement and no rank is busy: all ranks leave the broken
-        process group and rendezvous again as generation gen + 1 (rank 0 hosts the new TCPStore)."""
+    def _kick_regroup(self):
+        """Start the re-rendezvous (on its own thread, so the dispatch loop keeps serving) once every dead
+        rank has a connected replacement and no rank is busy."""
         with self.cv:
-            if not self.dead or self.busy:
+            if self.regrouping or not self.dead or self.busy:
                 return
             if any(r not in self._spawned or self._spawned[r].poll() is not None or r not in self.conns
                    for r in self.dead):
                 return                    # every replacement is up and has said hello
-            gen, port = self.gen + 1, _free_port()
-            self._regroup_acks = {}
-        logging.warning("re-rendezvous of %d ranks (generation %d)", self.world, gen)
-        for r in range(1, self.world):
-            try:
-                send_msg(self.conns[r], {"op": "regroup", "gen": gen, "port": port, "timeout": REGROUP_TIMEOUT_S},
-                         self.locks[r])
-            except OSError:
-                logging.error("regroup: rank %d unreachable", r)
-                return
+            self.regrouping, self.groups_ok = True, False
+            self._acks = {}
+        threading.Thread(target=self._regroup, name="cgs-regroup", daemon=True).start()
+
+    def _regroup(self):
+        """All-or-nothing re-rendezvous as generation gen + 1 (rank 0 hosts the new TCPStore):
+        phase 1 every rank leaves the old process group (bounded: a worker whose teardown hangs exits and is
+        replaced), phase 2 -- only if every rank left cleanly -- every rank joins the new generation. Any
+        failure leaves ``groups_ok`` False (prompts run single, on any live rank) and replaces the ranks whose
+        group state is unknown; the next attempt starts once their replacements are up."""
+        gen, port = self.gen + 1, _free_port()
+        workers = list(range(1, self.world))
+        ok = False
         try:
-            self.comm.reinit(port, gen, timeout_s=REGROUP_TIMEOUT_S)
-            self._build_contexts()
-        except Exception:   # noqa: BLE001
-            logging.exception("regroup failed on rank 0; the node stays degraded")
-            return
-        deadline = time.time() + REGROUP_TIMEOUT_S
-        self._wait(lambda: len(self._regroup_acks) >= self.world - 1 or time.time() > deadline)
-        with self.cv:
-            bad = [r for r in range(1, self.world) if not self._regroup_acks.get(r, {}).get("ok")]
-            if bad:
-                logging.error("regroup: ranks %s did not rejoin", bad)
+            logging.warning("re-rendezvous of %d ranks (generation %d): teardown", self.world, gen)
+            bad = self._phase("teardown", "torn_down", workers, {"gen": gen, "timeout": TEARDOWN_TIMEOUT_S},
+                              TEARDOWN_TIMEOUT_S + 15.0, lambda: self.comm.leave(TEARDOWN_TIMEOUT_S))
+            if bad is None:
+                logging.critical("rank 0's process-group teardown hung: SPMD stays off (single prompts only)")
                 return
-            self.gen = gen
-            self.regroups += 1
-            self.dead.clear()
-            self._spawned.clear()
-            self.cv.notify_all()
-        logging.warning("node whole again (generation %d, %d ranks)", gen, self.world)
+            if bad:
+                logging.error("regroup: ranks %s did not leave the old group cleanly; replacing them", bad)
+                for r in bad:
+                    self._force_replace(r)
+                return
+
+            def join0():
+                self.comm.join(port, gen, timeout_s=REGROUP_TIMEOUT_S)
+                self._build_contexts()
+                return True
+            logging.warning("re-rendezvous of %d ranks (generation %d): join", self.world, gen)
+            bad = self._phase("join", "joined", workers, {"gen": gen, "port": port, "timeout": REGROUP_TIMEOUT_S},
+                              REGROUP_TIMEOUT_S + 15.0, join0)
+            if bad is None or bad:
+                logging.error("regroup: generation %d incomplete (rank 0 %s, failed workers %s)", gen,
+                              "failed" if bad is None else "ok", bad or [])
+                for r in bad or []:
+                    self._force_replace(r)
+                return
+            with self.cv:
+                self.gen = gen
+                self.regroups += 1
+                self.dead.clear()
+                self._spawned.clear()
+            ok = True
+            logging.warning("node whole again (generation %d, %d ranks)", gen, self.world)
+        except Exception:   # noqa: BLE001 - never let the regroup thread die silently
+            logging.exception("regroup failed")
+        finally:
+            with self.cv:
+                self.regrouping = False
+                self.groups_ok = ok
+                self.regroup_failures += 0 if ok else 1
+                self.cv.notify_all()
+
+    def _phase(self, op, ack, workers, payload, timeout_s, local):
+        """Send ``op`` to every worker, run ``local()`` on rank 0, wait up to ``timeout_s`` for the ``ack``s.
+        Returns the workers that failed or did not answer, or None if rank 0's own part failed."""
+        bad = set()
+        for r in workers:
+            try:
+                send_msg(self.conns[r], dict(payload, op=op), self.locks[r])
+            except (OSError, KeyError):
+                bad.add(r)
+        try:
+            ok0 = bool(local())
+        except Exception:   # noqa: BLE001
+            logging.exception("regroup %s failed on rank 0", op)
+            ok0 = False
+        deadline = time.time() + timeout_s
+        # a rank whose connection drops meanwhile (_rank_died pops it) will not answer; a dead rank's connected
+        # replacement will
+        self._wait(lambda: all((ack, r) in self._acks or r in bad or r not in self.conns for r in workers)
+                   or time.time() > deadline)
+        with self.cv:
+            bad |= {r for r in workers if not self._acks.get((ack, r), {}).get("ok")}
+        return sorted(bad) if ok0 else None
+
+    def _force_replace(self, r):
+        """A worker whose process-group state is unknown: ask it to exit, kill it if it does not, and let
+        ``_rank_died`` (its connection drops) spawn the replacement."""
+        conn, proc = self.conns.get(r), _LAUNCH.get("procs", {}).get(r)
+        if conn is not None:
+            try:
+                send_msg(conn, {"op": "exit"}, self.locks[r])
+            except OSError:
+                pass
+        if proc is not None:
+            try:
+                proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+        if r not in self.dead:
+            self._rank_died(r)
 
     def interrupt_all(self):
         for r in list(self.busy):
@@ -529,10 +676,13 @@ class Coordinator:
         self.q.task_done(item_id, outputs_ui,
                          status=self.q.ExecutionStatus(status_str="success" if success else "error",
                                                        completed=success, messages=messages))
-        with self.q.mutex:                       # which rank(s) served it: /history metrics
+        with self.q.mutex:                       # which rank(s) served it, and when: /history metrics
             h = self.q.history.get(prompt_id)
             if h is not None:
-                h.setdefault("metrics", {})["ranks"] = self.ran_on.get(prompt_id)
+                mt = h.setdefault("metrics", {})
+                mt["ranks"] = self.ran_on.get(prompt_id)
+                mt["started_at"] = self._started.pop(prompt_id, None)    # its rank(s) assigned (epoch s)
+                mt["finished_at"] = time.time()
         sid = self._sids.pop(prompt_id, None)
         if sid is not None:
             self.server.send_sync("executing", {"node": None, "prompt_id": prompt_id}, sid)
@@ -555,6 +705,8 @@ class Coordinator:
     def spmd_size(self, prompt, extra):
         """(mode, k): the execution mode of a prompt and the rank prefix [0, k) it runs on."""
         mode = choose_mode(prompt, extra, self.world, self.latency_default, subsets=True)
+        if not self.groups_ok:        # a re-rendezvous is running or failed: no collectives until it succeeds
+            return "single", 1
         L = self.prefix()
         if mode == "latency":
             return ("latency", self.world) if L == self.world else ("single", 1)
@@ -576,10 +728,14 @@ class Coordinator:
                     self._sids[prompt_id] = sid
                 mode, k = self.spmd_size(prompt, extra)
                 if mode in ("spmd", "latency"):
-                    self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode, k)
+                    # its own thread: the loop goes on handing single prompts to the ranks outside the prefix;
+                    # the prefix is reserved now, in queue order, so later single prompts cannot starve it
+                    ticket = self._reserve(k)
+                    threading.Thread(target=self._run_spmd, args=(item_id, prompt_id, prompt, extra, outputs, mode,
+                                                                   k, ticket), daemon=True).start()
                 else:
                     self._run_single(item_id, prompt_id, prompt, extra, outputs)
-            self._maybe_regroup()
+            self._kick_regroup()
             self._housekeeping()
 
     def _housekeeping(self):
@@ -614,14 +770,28 @@ class Coordinator:
             while not pred():
                 self.cv.wait(timeout=1.0)
 
-    def _run_single(self, item_id, prompt_id, prompt, extra, outputs):
-        self._wait(lambda: any(r not in self.busy for r in self.live()))
+    def _reserve(self, k):
+        """Queue an SPMD prompt on the rank prefix [0, k): single prompts stay off those ranks from now on."""
+        ticket = {"members": set(range(k))}
         with self.cv:
-            idle = [r for r in self.live() if r not in self.busy]
-            r = max(idle)             # workers first: rank 0 also serves HTTP / WS
+            self._spmd_queue.append(ticket)
+        return ticket
+
+    def _idle_for_single(self):
+        """Ranks a single prompt may take: live, not busy, not reserved by a waiting SPMD prompt, and (during a
+        re-rendezvous) rank 0 only -- the workers are inside it."""
+        reserved = set().union(*(t["members"] for t in self._spmd_queue)) if self._spmd_queue else set()
+        return [r for r in self.live() if r not in self.busy and r not in reserved
+                and not (self.regrouping and r != 0)]
+
+    def _run_single(self, item_id, prompt_id, prompt, extra, outputs):
+        self._wait(lambda: bool(self._idle_for_single()))
+        with self.cv:
+            r = max(self._idle_for_single())    # workers first: rank 0 also serves HTTP / WS
             self.busy[r] = prompt_id
             self._inflight[r] = (item_id, prompt_id, prompt, extra, outputs)
             self.ran_on[prompt_id] = r
+            self._started[prompt_id] = time.time()
         if r == 0:
             threading.Thread(target=self._local_single, args=(prompt_id, prompt, extra, outputs), daemon=True).start()
         else:
@@ -653,30 +823,44 @@ class Coordinator:
                 self._finish_single(0, msg)
                 self.cv.notify_all()
 
-    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd", k=None):
+    def _run_spmd(self, item_id, prompt_id, prompt, extra, outputs, mode="spmd", k=None, ticket=None):
         from ..utils import imageio
         from . import spmd
         k = k or self.world
         members = list(range(k))
+        if ticket is None:
+            ticket = self._reserve(k)
         t_wait = time.perf_counter()
         logged = [False]
+
+        def changed():    # a member died, or the groups went away (a re-rendezvous failed): choose again
+            return any(r in self.dead for r in members) or (not self.groups_ok and not self.regrouping)
 
         def members_idle():
             if not logged[0] and time.perf_counter() - t_wait > SPMD_WAIT_LOG_S:
                 logged[0] = True
                 logging.warning("SPMD prompt %s has waited %.0f s for ranks %s (busy: %s)", prompt_id,
                                 time.perf_counter() - t_wait, members, dict(self.busy))
-            return all(r not in self.busy for r in members) or any(r in self.dead for r in members)
+            first = self._spmd_queue and self._spmd_queue[0] is ticket     # FIFO among SPMD prompts
+            return (first and not self.regrouping and self.groups_ok and all(r not in self.busy for r in members)) \
+                or changed()
         self._wait(members_idle)
-        if any(r in self.dead for r in members):     # a member died while we waited: choose again
+        with self.cv:
+            redo = changed()
+            if not redo:
+                for r in members:
+                    self.busy[r] = prompt_id
+                self._started[prompt_id] = time.time()
+            if ticket in self._spmd_queue:
+                self._spmd_queue.remove(ticket)
+            self.cv.notify_all()
+        if redo:
             mode, k = self.spmd_size(prompt, extra)
             if mode == "single":
                 return self._run_single(item_id, prompt_id, prompt, extra, outputs)
             return self._run_spmd(item_id, prompt_id, prompt, extra, outputs, mode, k)
         ctx, ex_spmd = self.ctxs[k], self.ex_spmds[k]
         with self.cv:
-            for r in members:
-                self.busy[r] = prompt_id
             self.spmd_waiting[prompt_id] = {}
             self.ran_on[prompt_id] = ("all" if k == self.world else members) if mode == "spmd" else "latency"
         # the workers' SPMD executors get the PNG metadata (SaveImage's hidden EXTRA_PNGINFO: every rank
@@ -786,6 +970,7 @@ def launch(n: int, argv):
     for r in range(1, n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), CGS_SCHED_ROLE="worker", PYTHONPATH=pypath)
         procs.append(subprocess.Popen([sys.executable, "-m", "comfy_gen_server_amd.main"] + list(argv), env=env))
+    _LAUNCH["procs"] = {r: p for r, p in zip(range(1, n), procs)}
     return listener, procs
 
 

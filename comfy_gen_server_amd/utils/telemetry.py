@@ -232,6 +232,10 @@ def maybe_fault(site: str, key: str):
         if site == "step" and kind == "step":
             _fired.add(item)
             raise InjectedFault(f"injected fault at sampler step {key}")
+        if site == "teardown" and kind == "teardown_hang":    # a process-group teardown that never returns
+            _fired.add(item)
+            logging.error("injected hang in the process-group teardown (rank %s)", key)
+            time.sleep(3600)
         if site == "rank" and kind == "rank_exit":
             _fired.add(item)
             logging.error("injected rank exit (rank %s)", key)

@@ -110,6 +110,9 @@ def test_upload_mask_applies_alpha_and_keeps_text(env):  # noqa: F811
             r = await c.post("/upload/mask", data=_form(mb.getvalue(), f"bad{i}.png", original_ref=bad))
             assert r.status == code, (bad, r.status)
             assert not os.path.exists(env / "input" / f"bad{i}.png"), bad       # nothing written
+            r = await c.post("/upload/mask", data=_form(mb.getvalue(), f"bad{i}.png", original_ref=bad,
+                                                        subfolder=f"newdir{i}"))
+            assert r.status == code and not os.path.exists(env / "input" / f"newdir{i}"), bad   # not even a folder
     _run(env, fn)
 
 

@@ -141,6 +141,29 @@ def test_attention_f32(cuda, B, heads, Sq, Sk, D, kind):
     assert _err(o, ref) < 1e-5
 
 
+@pytest.mark.parametrize("kind", ["float3d", "bool3d", "bool2d"])
+def test_attention_f32_mask_forms(cuda, kind):
+    """Masks in the forms custom nodes pass through optimized_attention: a per-image [B, Sq, Sk] float bias
+    (broadcast over heads, not over images), a bool keep-mask (False -> -inf, not an additive 0 / 1) and a
+    2-D [Sq, Sk] keep-mask."""
+    torch.manual_seed(6)
+    B, heads, Sq, Sk, D = 3, 2, 48, 40, 32
+    q, k, v = (torch.randn(B, S, heads * D, device=cuda) for S in (Sq, Sk, Sk))
+    if kind == "float3d":
+        mask = torch.randn(B, Sq, Sk, device=cuda)
+        add = mask[:, None]
+    else:
+        keep = torch.rand((B, Sq, Sk) if kind == "bool3d" else (Sq, Sk), device=cuda) > 0.3
+        keep[..., 0] = True                      # every row keeps a key
+        mask = keep
+        add = torch.zeros(keep.shape, device=cuda).masked_fill(~keep, float("-inf"))
+        add = add[:, None] if kind == "bool3d" else add[None, None]
+    o = ops.attention(q, k, v, heads, mask=mask)
+    ref = _attn_ref(q, k, v, heads, add.expand(B, heads, Sq, Sk))
+    assert ops.stats().get(("attention", "hip"), 0) == 1 and not _lib_calls()
+    assert _err(o, ref) < 1e-5
+
+
 def test_attention_f32_chunked(cuda, monkeypatch):
     """Score chunks smaller than the query length (the 1 GiB bound at VAE sizes)."""
     from comfy_gen_server_amd.ops import f32
