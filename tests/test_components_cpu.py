@@ -33,6 +33,36 @@ def test_queue_journal_replays_pending_and_history(tmp_path):
     assert "p-a" in q2.history and q2.history["p-a"]["outputs"] == {"1": {"images": []}}
 
 
+def test_queue_journal_one_record_per_mutation_and_replay(tmp_path):
+    """Every mutation is one journal record (deleting the last pending item is one ``delete``, not a
+    delete plus a wipe); history deletes / wipes and queue deletes survive a restart; a torn last line
+    (crash mid-write) is ignored."""
+    import json
+    j = tmp_path / "queue.jsonl"
+    q = PromptQueue(_Srv(), journal_path=str(j))
+    for n, pid in enumerate(["a", "b", "c", "d"]):
+        q.put((n, pid, {}, {}, []))
+    assert q.delete_queue_item(lambda it: it[1] == "b")
+    for _ in range(2):
+        item, i = q.get(timeout=1)
+        q.task_done(i, {}, q.ExecutionStatus("success", True, []))
+    q.delete_history_item("a")
+    assert q.delete_queue_item(lambda it: it[1] == "d")            # the last pending item
+    assert not q.delete_queue_item(lambda it: it[1] == "zz")
+    ops = [json.loads(ln)["op"] for ln in j.read_text().splitlines()]
+    assert ops == ["put"] * 4 + ["delete", "done", "done", "history_delete", "delete"], ops
+    with open(j, "a") as f:
+        f.write('{"op": "put", "item": [9, "torn"')               # crash mid-write
+    q2 = PromptQueue(_Srv(), journal_path=str(j))
+    assert q2.get_current_queue() == ([], []) and list(q2.history) == ["c"]
+    assert q2.history["c"]["status"]["status_str"] == "success"
+    q2.put((10, "e", {}, {}, []))
+    q2.wipe_history()
+    q3 = PromptQueue(_Srv(), journal_path=str(j))
+    assert q3.history == {} and [it[1] for it in q3.get_current_queue()[1]] == ["e"]
+    assert q3.get_history(max_items=5) == {}
+
+
 def test_image_format_decorator_converts_by_annotation():
     img = torch.rand(1, 12, 10, 3)
     seen = {}
