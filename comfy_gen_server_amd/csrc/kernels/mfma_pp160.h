@@ -92,7 +92,8 @@ __device__ __forceinline__ int gg_row160(int r) {
 // e.gnp as [M][N / 80][2] floats; a LayerNorm over these rows then needs only cgs_ln_rs_from_partials
 // instead of a statistics pass over the tensor. Host: N % 160 == 0.
 // PFE: epilogue operands (bias, LayerNorm-fold statistics, residual) prefetched one K-tile ahead -- see
-// `prefetch` -- (1) or loaded in the epilogue (0: the conv gathers, whose peeled K loop spilled).
+// `prefetch` -- with the last two K-tiles peeled (1), or only bias / LN statistics, inside the K loop (2: the
+// conv gathers, whose peeled loop and whose prefetched residual spilled), or loaded in the epilogue (0).
 template <class AL, bool LN = false, int DS = 0, int GNS = 0, bool GG = false, bool ACT = false,
           bool RSO = false, int PFE = 1>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
@@ -239,14 +240,14 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   u32x2v prs[4];
   u32x4v prw4[4][2];
   u32x2v prw2[4];
-  auto prefetch = [&](int m0, int n0, bool hb, bool hr) {
+  auto prefetch = [&](int m0, int n0, bool hb, bool hr, bool tracked = PFE == 0) {
     const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
     if (hb) {
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
         int col = n_w + colj(j);
         col = col < N ? col : N - 4;
-        if constexpr (PFE) untracked_load(pbias[j], e.bias + col);
+        if (!tracked) untracked_load(pbias[j], e.bias + col);
         else pbias[j] = *reinterpret_cast<const u32x2v*>(e.bias + col);
       }
     }
@@ -255,14 +256,14 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       for (int j = 0; j < 5; ++j) {
         int col = n_w + colj(j);
         col = col < N ? col : N - 4;
-        if constexpr (PFE) untracked_load(pcs[j], e.cs + col);
+        if (!tracked) untracked_load(pcs[j], e.cs + col);
         else pcs[j] = *reinterpret_cast<const u32x4v*>(e.cs + col);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int row = m_w + 16 * i + fr;
         row = row < M ? row : M - 1;
-        if constexpr (PFE) untracked_load(prs[i], e.rs + 2 * (long long)row);
+        if (!tracked) untracked_load(prs[i], e.rs + 2 * (long long)row);
         else prs[i] = *reinterpret_cast<const u32x2v*>(e.rs + 2 * (long long)row);
       }
     } else if (hr) {
@@ -275,12 +276,12 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         for (int p = 0; p < 2; ++p) {
           int col = n_w + 32 * p + 8 * fq;
           col = col < N ? col : N - 8;
-          if constexpr (PFE) untracked_load(prw4[i][p], rrow + col);
+          if (!tracked) untracked_load(prw4[i][p], rrow + col);
           else prw4[i][p] = *reinterpret_cast<const u32x4v*>(rrow + col);
         }
         int col = n_w + 64 + 4 * fq;
         col = col < N ? col : N - 4;
-        if constexpr (PFE) untracked_load(prw2[i], rrow + col);
+        if (!tracked) untracked_load(prw2[i], rrow + col);
         else prw2[i] = *reinterpret_cast<const u32x2v*>(rrow + col);
       }
     }
@@ -290,6 +291,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
     const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
     if constexpr (PFE == 0) prefetch(m0, n0, HB, HR);
+    else if constexpr (PFE == 2) prefetch(m0, n0, false, HR, true);    // the residual
     // column tile 4 (8 B per lane and row): row blocks i / i+1 are paired with v_permlane16_swap so a
     // lane stores 16 B (fq even: row block i, cols 64 + 8 (fq / 2) .. + 7; fq odd: row block i + 1)
     auto store_t4 = [&](int i, uint2 a, uint2 b) {
@@ -567,14 +569,16 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       read_frags(S, 1);
       if constexpr ((DS & 4) == 0) stage_part(1, kst, slot2);
       wait_tile();
-      if (PFE && PF) prefetch(m0, n0, hb, hr);
+      if (PFE && PF) prefetch(m0, n0, hb, PFE == 1 && hr);
       pp::wait_lgkm0();
       pp::barrier();
       mma();
       pp::barrier();
       slot = slot == 2 ? 0 : slot + 1;
     };
-    if constexpr (PFE) {   // the last two K-tiles peeled: the prefetched registers live only from there on
+    if constexpr (PFE == 2) {   // not peeled: the prefetch registers stay allocated through the K loop
+      for (int kt = 0; kt < nk; ++kt) ktile(kt, kt == nk - 2);
+    } else if constexpr (PFE) {   // the last two K-tiles peeled: the prefetched registers live only from there on
       for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, false);
       ktile(nk - 2, true);
       ktile(nk - 1, false);

@@ -37,6 +37,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ab-gns", action="store_true",
+                    help="alternate GroupNorm statistics from the conv epilogues on / off (same process)")
     a = ap.parse_args(argv)
     from ..models.layers import init_random_fast_
     from ..runtime.sd import VAE
@@ -59,6 +61,23 @@ def main(argv=None):
     best = min(ts)
     print(json.dumps({"batch": a.batch, "decode_ms": round(best * 1e3, 2), "conv_tflop": round(fl / 1e12, 2),
                       "conv_tflops_per_s_upper_bound": round(fl / best / 1e12, 1)}), flush=True)
+    if a.ab_gns:
+        from ..ops import core
+        res = {True: [], False: []}
+        with torch.inference_mode():
+            for _ in range(a.reps):
+                for on in (True, False):
+                    core._GNS = on
+                    m.decode(z)
+                    torch.cuda.synchronize()
+                    t = time.perf_counter()
+                    m.decode(z)
+                    torch.cuda.synchronize()
+                    res[on].append(time.perf_counter() - t)
+        core._GNS = True
+        print(json.dumps({"gns_on_ms": round(min(res[True]) * 1e3, 2), "gns_off_ms": round(min(res[False]) * 1e3, 2),
+                          "runs_on": [round(x * 1e3, 2) for x in res[True]],
+                          "runs_off": [round(x * 1e3, 2) for x in res[False]]}), flush=True)
 
 
 if __name__ == "__main__":
