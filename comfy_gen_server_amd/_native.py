@@ -183,6 +183,10 @@ KERNEL_SIGNATURES = {
     "cgs_groupnorm_band_stats": [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "cgs_groupnorm_apply_stats": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "cgs_groupnorm_nhwc_part": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P],
+    # the same with a row stride (elements) for pre_add: a column slice of the batched time-embedding GEMM
+    "cgs_groupnorm_nhwc_part_pld": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P],
+    "cgs_groupnorm_nhwc_ws_pld": [_P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _I, _I, _P],
+    "cgs_groupnorm_nhwc_dual_pld": [_P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _F, _I, _I, _P],
     "cgs_gemm_bf16_v7ws": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _L, _P],
     "cgs_conv2d_nhwc_v7ws": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P],
     # K29 FreeU low-frequency filter: x, y, coef ws, B, C, H, W, x strides x4, y strides x4, t, scale, dtype

@@ -164,7 +164,7 @@ template <bool STATS_ONLY = false>
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ part, const void* __restrict__ gamma,
                                                          const void* __restrict__ beta, const void* __restrict__ pre_add,
                                                          float* __restrict__ ab, int HW, int C, int G, int ppb, int nb,
-                                                         float eps, int wdt) {
+                                                         float eps, int wdt, int pld) {
   // STATS_ONLY (row-sharded GroupNorm, parallel/spatial.py): ab[(n G + g) * 2] = (mean, M2) of this rank's
   // band; the ranks' triples are Chan-combined on the host side and applied by gn_ab_from_stats_kernel.
   // one 256-thread block per (n, g): ONE pass over the per-(block, channel) (mean, M2) partials, each
@@ -179,8 +179,9 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
   __shared__ float red[3][4];
   auto chan_shift = [&](int c) -> float {
     if (!pre_add) return 0.f;
-    return (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[n * C + c])
-                             : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[n * C + c]) : ((const float*)pre_add)[n * C + c]);
+    const size_t i = (size_t)n * pld + c;     // pld: pre_add row stride (a column slice of a wider projection)
+    return (wdt == CGS_BF16) ? bf2f(((const u16*)pre_add)[i])
+                             : (wdt == CGS_F16 ? h2f(((const u16*)pre_add)[i]) : ((const float*)pre_add)[i]);
   };
   float cnt = 0.f, mean = 0.f, m2 = 0.f;
   constexpr int U = 8;
@@ -318,7 +319,7 @@ static int gn_apply_launch(const void* x, const void* x2, int C1, void* y, const
 // ws: workspace of cgs_groupnorm_workspace() bytes (torch-allocated so it is graph-capturable).
 static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const void* gamma, const void* beta,
                           const void* pre_add, void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
-                          hipStream_t stream) {
+                          hipStream_t stream, int pld) {
   // channel slices of <= 2048 (the per-lane register budget of gn_partial), equal and 8-aligned
   const int ns = (C + 2047) / 2048;
   if (C % 8 || C % G || C % (8 * ns) || C > 8192 || C1 % 8 || C1 > C) return (int)hipErrorInvalidValue;
@@ -346,7 +347,8 @@ static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const 
   else if (km == 1) { CGS_GN_PARTIAL(1) } else if (km == 2) { CGS_GN_PARTIAL(2) } else if (km == 3) { CGS_GN_PARTIAL(3) } else { CGS_GN_PARTIAL(4) }
 #undef CGS_GN_PARTIAL
 #undef CGS_GN_PARTIAL_PK
-  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
+  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype,
+                                                    pld);
   return gn_apply_launch(x, x2, C1, y, ab, N, HW, C, silu, dtype, stream);
 }
 
@@ -374,7 +376,7 @@ static int groupnorm_stats_impl(const void* x, const void* x2, int C1, const voi
   else if (km == 3) { CGS_GN_PARTIAL(3, 1) } else { CGS_GN_PARTIAL(4, 1) }
 #undef CGS_GN_PARTIAL
   gn_finalize_kernel<true><<<dim3(G, N), 256, 0, stream>>>(part, nullptr, nullptr, pre_add, stats, HW, C, G, ppb, nb,
-                                                          0.f, dtype);
+                                                          0.f, dtype, C);
   return (int)hipGetLastError();
 }
 
@@ -445,21 +447,48 @@ CGS_EXPORT int cgs_groupnorm_nhwc_part(const void* x, void* y, const void* gamma
                                        int silu, int dtype, hipStream_t stream) {
   if (C % 8 || C % G || ppb <= 0 || HW % ppb || !part || !ab) return (int)hipErrorInvalidValue;
   const int nb = HW / ppb;
-  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype);
+  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype, C);
   return gn_apply_launch(x, nullptr, C, y, ab, N, HW, C, silu, dtype, stream);
 }
 
 CGS_EXPORT int cgs_groupnorm_nhwc_ws(const void* x, void* y, const void* gamma, const void* beta, const void* pre_add,
                                      void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
                                      hipStream_t stream) {
-  return groupnorm_impl(x, nullptr, C, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream);
+  return groupnorm_impl(x, nullptr, C, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream, C);
 }
 
 // GroupNorm over the channel concat of x ([N, HW, C1]) and x2 ([N, HW, C - C1]) without materialising it.
 CGS_EXPORT int cgs_groupnorm_nhwc_dual(const void* x, const void* x2, int C1, void* y, const void* gamma,
                                        const void* beta, const void* pre_add, void* ws, int N, int HW, int C, int G,
                                        float eps, int silu, int dtype, hipStream_t stream) {
-  return groupnorm_impl(x, x2, C1, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream);
+  return groupnorm_impl(x, x2, C1, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream, C);
+}
+
+// The same three entry points with a row stride ``pld`` (elements, >= C) for pre_add: the UNet's ResBlock
+// time-embedding projections are ONE GEMM per forward ([N, sum of the blocks' C]) and each block's GroupNorm
+// reads its column slice in place (models/unet.py, UNetModel._emb_proj).
+CGS_EXPORT int cgs_groupnorm_nhwc_ws_pld(const void* x, void* y, const void* gamma, const void* beta,
+                                         const void* pre_add, int pld, void* ws, int N, int HW, int C, int G, float eps,
+                                         int silu, int dtype, hipStream_t stream) {
+  if (pre_add && pld < C) return (int)hipErrorInvalidValue;
+  return groupnorm_impl(x, nullptr, C, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream, pld);
+}
+
+CGS_EXPORT int cgs_groupnorm_nhwc_dual_pld(const void* x, const void* x2, int C1, void* y, const void* gamma,
+                                           const void* beta, const void* pre_add, int pld, void* ws, int N, int HW,
+                                           int C, int G, float eps, int silu, int dtype, hipStream_t stream) {
+  if (pre_add && pld < C) return (int)hipErrorInvalidValue;
+  return groupnorm_impl(x, x2, C1, y, gamma, beta, pre_add, ws, N, HW, C, G, eps, silu, dtype, stream, pld);
+}
+
+CGS_EXPORT int cgs_groupnorm_nhwc_part_pld(const void* x, void* y, const void* gamma, const void* beta,
+                                           const void* pre_add, int pld, const float* part, float* ab, int N, int HW,
+                                           int C, int G, int ppb, float eps, int silu, int dtype, hipStream_t stream) {
+  if (C % 8 || C % G || ppb <= 0 || HW % ppb || !part || !ab || (pre_add && pld < C)) return (int)hipErrorInvalidValue;
+  const int nb = HW / ppb;
+  gn_finalize_kernel<<<dim3(G, N), 256, 0, stream>>>(part, gamma, beta, pre_add, ab, HW, C, G, ppb, nb, eps, dtype,
+                                                    pld);
+  return gn_apply_launch(x, nullptr, C, y, ab, N, HW, C, silu, dtype, stream);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -18,13 +18,14 @@ MI355X design choices:
 from __future__ import annotations
 
 import logging
+import os
 
 import torch
 import torch.nn as nn
 
 from .. import ops
 from .attention import BasicTransformerBlock, SpatialTransformer, _Seq
-from .layers import Conv2d, Conv3d, GroupNorm, Linear
+from .layers import Conv2d, Conv3d, DerivedMixin, GroupNorm, Linear, _hooked, module_epoch
 
 
 def _SKIPCAT():
@@ -85,7 +86,11 @@ class ResBlock(nn.Module):
     def _out(self, h, emb_silu, skip):
         pre = None
         if not self.skip_t_emb and emb_silu is not None:
-            pre = self.emb_layers[1](emb_silu).to(h.dtype)          # [B, C]
+            pj, off = getattr(emb_silu, "_cgs_emb_proj", None), self.__dict__.get("_cgs_emb_off")
+            if pj is not None and off is not None:     # this block's columns of the batched projection (a view)
+                pre = pj[:, off:off + self.out_channels]
+            else:
+                pre = self.emb_layers[1](emb_silu).to(h.dtype)          # [B, C]
         h = ops.group_norm(h, 32, self.out_layers[0].weight, self.out_layers[0].bias,
                            self.out_layers[0].eps, silu=True, pre_add=pre)
         return self.out_layers[3](h, residual=skip)
@@ -300,7 +305,7 @@ def _apply_control(h, control, name):
     return h
 
 
-class UNetModel(nn.Module):
+class UNetModel(nn.Module, DerivedMixin):
     def __init__(self, in_channels=4, model_channels=320, out_channels=4, num_res_blocks=2,
                  channel_mult=(1, 2, 4, 4), transformer_depth=1, transformer_depth_middle=None,
                  transformer_depth_output=None, context_dim=None, num_heads=-1, num_head_channels=-1,
@@ -422,6 +427,33 @@ class UNetModel(nn.Module):
         self.out = _Seq(GroupNorm(32, ch, **kw), nn.SiLU(), Conv2d(model_channels, out_channels, 3, padding=1, **kw))
 
     # ------------------------------------------------------------------------------------------
+    def _emb_proj(self, emb_silu):
+        """Every ResBlock's time-embedding projection (reference openaimodel.py:245-264, one Linear per block) as
+        ONE GEMM per forward: [N, sum of the blocks' channels]. Each block's GroupNorm then reads its column slice
+        in place (``ops.group_norm`` pre_add with a row stride) -- ~22 skinny launches per SDXL step become one.
+        None (per-block projections) off the device, with hooked / cast-on-the-fly layers or CGS_EMB_BATCH=0."""
+        if not emb_silu.is_cuda or os.environ.get("CGS_EMB_BATCH", "1") == "0":
+            return None
+        blocks = self.__dict__.get("_cgs_emb_blocks")
+        if blocks is None:
+            blocks, off = [], 0
+            for m in self.modules():
+                if isinstance(m, ResBlock) and not m.skip_t_emb:
+                    m.__dict__["_cgs_emb_off"] = off
+                    off += m.out_channels
+                    blocks.append(m)
+            self.__dict__["_cgs_emb_blocks"] = blocks
+        lins = [b.emb_layers[1] for b in blocks]
+        if not lins or any(_hooked(ln) or ln.bias is None or ln.weight.dtype != emb_silu.dtype
+                           or ln.weight.device != emb_silu.device for ln in lins):
+            return None
+        key = (module_epoch(self), lins[0].weight.data_ptr(), lins[-1].weight.data_ptr())
+        wb = self._derived_get("emb_proj", lambda: None)
+        if wb is None or wb[0] != key:
+            wb = (key, torch.cat([ln.weight for ln in lins]).contiguous(), torch.cat([ln.bias for ln in lins]))
+            self.__dict__["_derived"]["emb_proj"] = wb
+        return ops.linear(emb_silu, wb[1], wb[2])
+
     def forward(self, x, timesteps=None, context=None, y=None, control=None, transformer_options=None, **kwargs):
         to = transformer_options if transformer_options is not None else {}
         num_video_frames = kwargs.get("num_video_frames", self.default_num_video_frames)
@@ -450,6 +482,9 @@ class UNetModel(nn.Module):
             le = self.label_emb[0]
             emb = le[2](ops.silu(le[0](y.to(dt))), residual=emb)
         emb_silu = ops.silu(emb)
+        proj = self._emb_proj(emb_silu)
+        if proj is not None:
+            emb_silu._cgs_emb_proj = proj
 
         hs = []
         h = x

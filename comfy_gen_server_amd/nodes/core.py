@@ -777,29 +777,29 @@ class CheckpointLoader:
                                                 embedding_directory=folder_paths.get_folder_paths("embeddings"))[:3]
 
 
+def _diffusers_roots():
+    return [r for r in folder_paths.get_folder_paths("diffusers") if os.path.isdir(r)]
+
+
 class DiffusersLoader:
+    """A diffusers folder (``model_index.json`` at its top) under any registered ``diffusers`` root; the
+    choice list names folders relative to their root (reference ``nodes.py`` DiffusersLoader)."""
+
     @classmethod
     def INPUT_TYPES(cls):
-        paths = []
-        for search_path in folder_paths.get_folder_paths("diffusers"):
-            if os.path.exists(search_path):
-                for root, subdir, files in os.walk(search_path, followlinks=True):
-                    if "model_index.json" in files:
-                        paths.append(os.path.relpath(root, start=search_path))
-        return {"required": {"model_path": (paths,), }}
+        found = [os.path.relpath(d, start=root) for root in _diffusers_roots()
+                 for d, _, names in os.walk(root, followlinks=True) if "model_index.json" in names]
+        return {"required": {"model_path": (found,)}}
     RETURN_TYPES = ("MODEL", "CLIP", "VAE")
     FUNCTION = "load_checkpoint"
     CATEGORY = "advanced/loaders/deprecated"
 
     def load_checkpoint(self, model_path, output_vae=True, output_clip=True):
         from ..runtime.diffusers import load_diffusers
-        for search_path in folder_paths.get_folder_paths("diffusers"):
-            if os.path.exists(search_path):
-                path = os.path.join(search_path, model_path)
-                if os.path.exists(path):
-                    model_path = path
-                    break
-        return load_diffusers(model_path, output_vae=output_vae, output_clip=output_clip,
+        # the first root holding the folder wins; an absolute / unknown path is passed through as given
+        full = next((os.path.join(root, model_path) for root in _diffusers_roots()
+                     if os.path.exists(os.path.join(root, model_path))), model_path)
+        return load_diffusers(full, output_vae=output_vae, output_clip=output_clip,
                               embedding_directory=folder_paths.get_folder_paths("embeddings"))
 
 
@@ -831,20 +831,18 @@ class LoraLoader:
     FUNCTION = "load_lora"
     CATEGORY = "loaders"
 
+    def _lora_state(self, lora_name):
+        """The LoRA file's tensors, kept for the next call with the same file (one cached file per node)."""
+        path = folder_paths.get_full_path("loras", lora_name)
+        cached = self.loaded_lora
+        if cached is None or cached[0] != path:
+            cached = self.loaded_lora = (path, load_state_dict(path, safe_load=True))
+        return cached[1]
+
     def load_lora(self, model, clip, lora_name, strength_model, strength_clip):
-        if strength_model == 0 and strength_clip == 0:
+        if strength_model == 0 and strength_clip == 0:      # nothing to patch: the inputs pass through
             return (model, clip)
-        lora_path = folder_paths.get_full_path("loras", lora_name)
-        lora = None
-        if self.loaded_lora is not None:
-            if self.loaded_lora[0] == lora_path:
-                lora = self.loaded_lora[1]
-            else:
-                self.loaded_lora = None
-        if lora is None:
-            lora = load_state_dict(lora_path, safe_load=True)
-            self.loaded_lora = (lora_path, lora)
-        return sdl.load_lora_for_models(model, clip, lora, strength_model, strength_clip)
+        return sdl.load_lora_for_models(model, clip, self._lora_state(lora_name), strength_model, strength_clip)
 
 
 class LoraLoaderModelOnly(LoraLoader):

@@ -740,32 +740,58 @@ def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor | None, bias: 
             bias = bias.to(device=x.device, dtype=x.dtype).contiguous()
         xc = x.contiguous(memory_format=torch.channels_last)
         y = torch.empty((N, C, H, W), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
-        pa = None
+        pa, pld = None, C
         if pre_add is not None:
-            pa = pre_add.to(x.dtype).contiguous()
+            pa = pre_add.to(x.dtype)
+            # a [N, C] column slice of a wider row-major tensor (the UNet's batched time-embedding projection)
+            # is read in place through a row stride; anything else is made contiguous
+            if not (pa.dim() == 2 and pa.shape == (N, C) and pa.stride(1) == 1 and pa.stride(0) >= C
+                    and _native.has_kernel("cgs_groupnorm_nhwc_ws_pld")):
+                pa = pa.contiguous()
+            pld = pa.stride(0) if pa.dim() == 2 and N > 1 else C
+        strided = pa is not None and pld != C
         gp = getattr(x, "_cgs_gnpart", None) if x2 is None else None
         if gp is not None and gp[1] == x.data_ptr() and xc is x and gp[0].numel() == N * (H * W // 64) * C * 2 \
                 and _native.has_kernel("cgs_groupnorm_nhwc_part"):
             # statistics from the producing conv's epilogue (conv2d(gn_stats=True)): finalize + apply only
             ab = torch.empty(N * C * 2, device=x.device, dtype=torch.float32)
-            _check(_lib().cgs_groupnorm_nhwc_part(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
-                                                  _ptr(pa), gp[0].data_ptr(), ab.data_ptr(), N, H * W, C, groups, 64,
-                                                  float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
-                   "cgs_groupnorm_nhwc_part")
+            if strided:
+                _check(_lib().cgs_groupnorm_nhwc_part_pld(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
+                                                          pa.data_ptr(), pld, gp[0].data_ptr(), ab.data_ptr(), N,
+                                                          H * W, C, groups, 64, float(eps), 1 if silu else 0,
+                                                          _DT[x.dtype], _stream()), "cgs_groupnorm_nhwc_part_pld")
+            else:
+                _check(_lib().cgs_groupnorm_nhwc_part(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
+                                                      _ptr(pa), gp[0].data_ptr(), ab.data_ptr(), N, H * W, C, groups,
+                                                      64, float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
+                       "cgs_groupnorm_nhwc_part")
             return y
         wsb = int(_lib().cgs_groupnorm_workspace(N, H * W, C))
         ws = torch.empty((wsb + 3) // 4, device=x.device, dtype=torch.float32)
         if x2 is None:
-            _check(_lib().cgs_groupnorm_nhwc_ws(xc.data_ptr(), y.data_ptr(), weight.data_ptr(),
-                                                _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups, float(eps),
-                                                1 if silu else 0, _DT[x.dtype], _stream()),
-                   "cgs_groupnorm_nhwc_ws")
+            if strided:
+                _check(_lib().cgs_groupnorm_nhwc_ws_pld(xc.data_ptr(), y.data_ptr(), weight.data_ptr(), _ptr(bias),
+                                                        pa.data_ptr(), pld, ws.data_ptr(), N, H * W, C, groups,
+                                                        float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
+                       "cgs_groupnorm_nhwc_ws_pld")
+            else:
+                _check(_lib().cgs_groupnorm_nhwc_ws(xc.data_ptr(), y.data_ptr(), weight.data_ptr(),
+                                                    _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups,
+                                                    float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
+                       "cgs_groupnorm_nhwc_ws")
         else:
             x2c = x2.contiguous(memory_format=torch.channels_last)
-            _check(_lib().cgs_groupnorm_nhwc_dual(xc.data_ptr(), x2c.data_ptr(), C1, y.data_ptr(), weight.data_ptr(),
-                                                  _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W, C, groups,
-                                                  float(eps), 1 if silu else 0, _DT[x.dtype], _stream()),
-                   "cgs_groupnorm_nhwc_dual")
+            if strided:
+                _check(_lib().cgs_groupnorm_nhwc_dual_pld(xc.data_ptr(), x2c.data_ptr(), C1, y.data_ptr(),
+                                                          weight.data_ptr(), _ptr(bias), pa.data_ptr(), pld,
+                                                          ws.data_ptr(), N, H * W, C, groups, float(eps),
+                                                          1 if silu else 0, _DT[x.dtype], _stream()),
+                       "cgs_groupnorm_nhwc_dual_pld")
+            else:
+                _check(_lib().cgs_groupnorm_nhwc_dual(xc.data_ptr(), x2c.data_ptr(), C1, y.data_ptr(),
+                                                      weight.data_ptr(), _ptr(bias), _ptr(pa), ws.data_ptr(), N, H * W,
+                                                      C, groups, float(eps), 1 if silu else 0, _DT[x.dtype],
+                                                      _stream()), "cgs_groupnorm_nhwc_dual")
         return y
     if x2 is not None:
         x = torch.cat([x, x2], dim=1)

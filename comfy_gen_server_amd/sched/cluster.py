@@ -21,10 +21,9 @@ Yjs ``outputs`` map as ``op: "yjs"`` / ``"yjs_flush"``, applied to rank 0's map 
 (reference ``main.py:152-160``, ``server.py:754-791`` / ``:825-832``, ``execution.py:334-345``).
 
 Ranks keep one executor for single prompts (its own cross-prompt cache) and one per SPMD rank prefix
-[0, k) (k = the powers of two below N, and N): a prefix's executor only sees that prefix's prompts, so
-its caches stay identical on its members and they all reach the same collectives. A batch b < N runs
-SPMD on the largest prefix <= b while the other ranks keep serving single prompts; an SPMD prompt waits
-only for its own ranks.
+[0, k) (k = 2..N): a prefix's executor only sees that prefix's prompts, so its caches stay identical on
+its members and they all reach the same collectives. A batch b < N runs SPMD on the prefix of size b while
+the other ranks keep serving single prompts; an SPMD prompt waits only for its own ranks.
 
 Scheduling: the dispatch loop never runs a prompt itself. A single prompt goes to an idle rank (workers
 first); an SPMD prompt reserves its prefix in queue order and runs on its own thread once those ranks are
@@ -235,15 +234,20 @@ def _forward_progress(server):
 
 
 def _spmd_sizes(world: int):
-    """Rank prefixes that get their own SPMD groups: the powers of two below the node size, and the node.
-    A batch b < world runs on the largest prefix <= b (SPMD over a subset) and leaves the other ranks to
-    single prompts; each prefix keeps its own executor (identical caches on its members), so few sizes
-    keep few cached model copies."""
-    out, k = [], 2
-    while k < world:
-        out.append(k)
-        k *= 2
-    return out + ([world] if world > 1 else [])
+    """Rank prefixes that get their own SPMD groups: every size 2..world (``CGS_SPMD_PREFIXES=pow2``: the powers
+    of two below the node size, and the node). A batch b < world runs on the prefix of size b (SPMD over a
+    subset: a batch of 3 on an 8-GPU node uses 3 ranks, not 2) and leaves the other ranks to single prompts.
+    Each prefix keeps its own executor (identical caches on its members), i.e. its own cached model copies
+    once used: with 288 GB of HBM per MI355X, seven SDXL-sized copies (~7 GB each) fit beside the working set."""
+    if world <= 1:
+        return []
+    if os.environ.get("CGS_SPMD_PREFIXES", "all") == "pow2":
+        out, k = [], 2
+        while k < world:
+            out.append(k)
+            k *= 2
+        return out + [world]
+    return list(range(2, world + 1))
 
 
 def worker_main(comm, address, authkey: bytes, respawned: bool = False):

@@ -120,6 +120,8 @@ def test_spmd_prefix_prompt_does_not_block_single_prompts(tmp_path_factory):
         a = _post(url + "/prompt", {"prompt": big})["prompt_id"]
         singles = [_post(url + "/prompt", {"prompt": _graph(60 + i, 1, f"s{i}")})["prompt_id"] for i in range(2)]
         h = _wait(url, [a] + singles, timeout=300)
+        c = _post(url + "/prompt", {"prompt": _graph(65, 3, "three")})["prompt_id"]
+        h.update(_wait(url, [c], timeout=300))
     finally:
         _stop(proc)
     assert all(e["status"]["status_str"] == "success" for e in h.values()), {k: v["status"] for k, v in h.items()}
@@ -128,6 +130,9 @@ def test_spmd_prefix_prompt_does_not_block_single_prompts(tmp_path_factory):
     for s in singles:     # overlap in time with the SPMD prompt
         assert h[s]["metrics"]["started_at"] < h[a]["metrics"]["finished_at"], (h[s]["metrics"], h[a]["metrics"])
         assert h[s]["metrics"]["finished_at"] < h[a]["metrics"]["finished_at"], (h[s]["metrics"], h[a]["metrics"])
+    # a batch of 3 on 4 ranks runs on the 3-rank prefix (every prefix size has its groups)
+    assert h[c]["status"]["status_str"] == "success", h[c]["status"]
+    assert h[c]["metrics"]["ranks"] == [0, 1, 2] and h[c]["metrics"]["images_per_rank"] == {"0": 1, "1": 1, "2": 1}
 
 
 def test_hung_teardown_rank_is_replaced_and_node_regroups(tmp_path_factory, monkeypatch):
