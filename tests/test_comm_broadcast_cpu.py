@@ -8,7 +8,6 @@ two Gloo ranks on the CPU:
 * a failed read on rank 0 fails rank 1 too.
 """
 import os
-import socket
 import types
 
 import pytest
@@ -17,18 +16,15 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _worker(rank, world, port, tmp, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+    import datetime
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from comfy_gen_server_amd.parallel import comm as C
     from comfy_gen_server_amd.sched.spmd import SPMD
-    c = C.init_from_env(backend="gloo", timeout_s=60)
+    # a file rendezvous: no TCP port to race for when the suite runs in parallel workers
+    dist.init_process_group("gloo", init_method=f"file://{tmp}/rdzv", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=120))
+    c = C.init_from_env(backend="gloo", timeout_s=120)
     ctx = types.SimpleNamespace(comm=c, rank=c.rank, loads_received=0)
     reads = []
 
@@ -72,11 +68,10 @@ def test_spmd_checkpoint_broadcast_flat_nested_and_failure(tmp_path):
     torch.save(nested, tmp_path / "nested.pth")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, 0, str(tmp_path), q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=180) for _ in procs)
+    res = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
