@@ -694,7 +694,9 @@ static void conv_v5_go(ConvArgs& a, hipStream_t stream) {
 
 // LD: 0 ConvGatherA8 (generic: UP2X, big filters), 1 ConvGatherK (64-bit offsets: an input >= 2 GiB),
 // 2 ConvGatherKD (buffer_load ... lds, the default where it applies)
-template <int LD, int DS = 0, bool GNS = false>
+// NJ: 16-column MFMA tiles per wave group -- 5 (256 x 160 tiles) or 4 (256 x 128: Cout = 128 / 256 / 384 ...,
+// variant 18)
+template <int LD, int DS = 0, bool GNS = false, int NJ = 5, int PFE = CGS_CONV_PFE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.N * a.Ho * a.Wo;
@@ -708,9 +710,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
   e.gnp = a.gnp;
   e.hw = a.Ho * a.Wo;
-  pq::run<decltype(al), false, DS, GNS, false, false, false, CGS_CONV_PFE>(al, a.w, K, M, a.Cout, K, e, smem,
-                                                                          (M + pq::BM - 1) / pq::BM, a.tiles_n,
-                                                                          a.group_m);
+  pq::run<decltype(al), false, DS, GNS, false, false, false, PFE, NJ>(al, a.w, K, M, a.Cout, K, e, smem,
+                                                                              (M + pq::BM - 1) / pq::BM, a.tiles_n,
+                                                                              a.group_m);
 }
 
 static int conv_num_cus() {
@@ -725,21 +727,25 @@ static int conv_num_cus() {
 
 int v6_conv_ds();   // gemm.hip: v6 DMA placement for convs (CGS_V6_CONV_DS / cgs_v6_set_mode)
 
-template <int LD, int DS, bool GNS = false>
+template <int LD, int DS, bool GNS = false, int NJ = 5, int PFE = CGS_CONV_PFE>
 static void conv_v6_launch(ConvArgs& a, int grid, hipStream_t stream) {
+  constexpr int lds = pq::Geo<NJ>::LDS;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<LD, DS, GNS>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_nhwc_v6_kernel<LD, DS, GNS, NJ, PFE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  conv_nhwc_v6_kernel<LD, DS, GNS><<<grid, pq::THREADS, pq::LDS, stream>>>(a);
+  conv_nhwc_v6_kernel<LD, DS, GNS, NJ, PFE><<<grid, pq::THREADS, lds, stream>>>(a);
 }
 
 
-static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
+
+static void conv_v6_go(ConvArgs& a, hipStream_t stream, bool n128 = false) {
   const int M = a.N * a.Ho * a.Wo;
-  a.tiles_n = (a.Cout + pq::BN - 1) / pq::BN;
+  if (a.gnp) n128 = false;   // the GroupNorm-statistics epilogue: 160-wide tiles only
+  const int bn = n128 ? pq::Geo<4>::BN : pq::BN;
+  a.tiles_n = (a.Cout + bn - 1) / bn;
   const long long T = (long long)((M + pq::BM - 1) / pq::BM) * a.tiles_n;
   const int grid = (int)(T < conv_num_cus() ? T : conv_num_cus());
   const int ds = v6_conv_ds();
@@ -750,6 +756,11 @@ static void conv_v6_go(ConvArgs& a, hipStream_t stream) {
     constexpr int L = decltype(lc)::value;
     if (a.gnp) {   // GroupNorm statistics epilogue (split-DMA main loop only)
       conv_v6_launch<L, 51, true>(a, grid, stream);
+      return;
+    }
+    if (n128) {    // 256 x 128 tiles: the default DMA placement only; no epilogue-operand prefetch (NJ = 4 has
+                   // the registers for the peeled form, but it measured 1-3 % slower, profiles/r06/conv_n128_ab.log)
+      conv_v6_launch<L, 51, false, 4, 0>(a, grid, stream);
       return;
     }
     switch (ds) {
@@ -841,6 +852,11 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream, void* ws
   if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
       ((uintptr_t)a.bias % 8) == 0) {
     conv_v6_go(a, stream);
+    return (int)hipGetLastError();
+  }
+  if (variant == 18 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
+      ((uintptr_t)a.bias % 8) == 0 && a.Cout % 128 == 0) {
+    conv_v6_go(a, stream, true);
     return (int)hipGetLastError();
   }
   if (variant == 8) {

@@ -43,15 +43,26 @@ constexpr int A_BYTES = BM * 128;
 constexpr int B_BYTES = BN * 128;
 constexpr int STAGE = A_BYTES + B_BYTES;
 constexpr int LDS = 3 * STAGE;     // 156 KiB
+// NJ = 4 (run<..., NJ>): the 256 x 128 form -- 2 groups x 64 columns, no column tile 4 -- for Cout = 128 convs
+// (the VAE's full-resolution ResnetBlocks: a 160-wide tile wastes 20 % of its columns there, a 256-wide one half).
+template <int NJ>
+struct Geo {
+  static constexpr int BN = 32 * NJ, GW = 16 * NJ;             // tile / wave-group columns
+  static constexpr int B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES, LDS = 3 * STAGE;
+  static constexpr int NBG = (BN + 63) / 64;                    // 64-row B DMA pieces (the last: group 0 only
+  static constexpr bool B_HALF = BN % 64 != 0;                  //   when BN % 64 == 32)
+};
 
 // Tile column staged at B row r. Wave group g reads rows g*80 + 16j + (4fq + t) as MFMA column tile
 // j; the tile pairs (0,1) and (2,3) are interleaved so that the lane holds 8 consecutive columns
 // (32p + 8fq + 4(j&1) + t) -> 16-B epilogue stores covering 64 contiguous bytes per row; tile 4
 // keeps its 16 plain columns (8-B stores).
+template <int NJ = 5>
 __device__ __forceinline__ int b_col160(int r) {
-  const int g = r >= 80, l = r - 80 * g, j = l >> 4, q = l & 15;
-  if (j >= 4) return 80 * g + 64 + q;
-  return 80 * g + 32 * (j >> 1) + 8 * (q >> 2) + 4 * (j & 1) + (q & 3);
+  constexpr int GW = 16 * NJ;
+  const int g = r >= GW, l = r - GW * g, j = l >> 4, q = l & 15;
+  if (j >= 4) return GW * g + 64 + q;
+  return GW * g + 32 * (j >> 1) + 8 * (q >> 2) + 4 * (j & 1) + (q & 3);
 }
 
 // GEGLU staging (run<..., GG>): staged B row r of group g = r / 80, tile j, row q in the tile -> output column
@@ -95,9 +106,13 @@ __device__ __forceinline__ int gg_row160(int r) {
 // `prefetch` -- with the last two K-tiles peeled (1), or only bias / LN statistics, inside the K loop (2: the
 // conv gathers, whose peeled loop and whose prefetched residual spilled), or loaded in the epilogue (0).
 template <class AL, bool LN = false, int DS = 0, int GNS = 0, bool GG = false, bool ACT = false,
-          bool RSO = false, int PFE = 1>
+          bool RSO = false, int PFE = 1, int NJ = 5>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
+  static_assert(NJ == 5 || NJ == 4, "column tiles per wave group");
+  static_assert(NJ == 5 || (!GG && !RSO && !LN), "NJ = 4: plain / residual / GroupNorm-statistics epilogues");
+  using Gm = Geo<NJ>;
+  constexpr int BN = Gm::BN, GW = Gm::GW, STAGE = Gm::STAGE;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -132,9 +147,9 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 #pragma unroll
     for (int g = 0; g < 4; ++g) al.setup(g, m0 + g * 64 + lrow);
 #pragma unroll
-    for (int g = 0; g < 3; ++g) {
+    for (int g = 0; g < Gm::NBG; ++g) {
       const int r = g * 64 + lrow;
-      int n = n0 + (GG ? gg_row160(r < BN ? r : BN - 1) : b_col160(r < BN ? r : BN - 1));
+      int n = n0 + (GG ? gg_row160(r < BN ? r : BN - 1) : b_col160<NJ>(r < BN ? r : BN - 1));
       n = n < N ? n : N - 1;
       if constexpr ((DS & 128) != 0) boff[g] = (uint32_t)(((long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7))) * 2);
       else bsrc[g] = W + (long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7));
@@ -146,7 +161,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     else mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * 8192);
   };
   auto dma_b = [&](int g, int kt, int slot) {
-    if (g < 2 || grp == 0) {  // B rows 128..159: group 0 only
+    if (g >= Gm::NBG) return;
+    if (!Gm::B_HALF || g < Gm::NBG - 1 || grp == 0) {  // BN = 160: B rows 128..159 by group 0 only
       if constexpr ((DS & 128) != 0)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (mc_lds_void*)(smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192),
                                                  16, boff[g], kt * BK * 2, 0, 0);
@@ -190,14 +206,14 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     stage_part(0, kt, slot);
     if constexpr ((DS & 3) != 0) stage_part(1, kt, slot);
   };
-  auto wait_tile = [&]() {   // all but the 7 (group 0) / 6 (group 1) youngest DMAs retired
-    if (grp == 0) mc::wait_vmcnt<7>();
-    else mc::wait_vmcnt<6>();
+  auto wait_tile = [&]() {   // all but one K-tile's DMAs (BN = 160: 7 in group 0, 6 in group 1) retired
+    if (grp == 0) mc::wait_vmcnt<4 + Gm::NBG>();
+    else mc::wait_vmcnt<4 + Gm::NBG - (Gm::B_HALF ? 1 : 0)>();
   };
 
-  f32x4 acc[4][5];
+  f32x4 acc[4][NJ];
   const int fr = lane & 15, fq = lane >> 4;
-  bf16x8 af[4], bfr[5];
+  bf16x8 af[4], bfr[NJ];
   auto read_frags = [&](const unsigned char* S, int kk) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -207,8 +223,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     }
     const unsigned char* SB = S + A_BYTES;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int r = grp * 80 + 16 * j + fr;
+    for (int j = 0; j < NJ; ++j) {
+      const int r = grp * GW + 16 * j + fr;
       const int c = (4 * kk + fq) ^ ((r >> 1) & 7);
       bfr[j] = *reinterpret_cast<const bf16x8*>(SB + r * 128 + 16 * c);
     }
@@ -218,7 +234,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   // column of acc[.][j][0] for this lane (b_col160): pairs (0,1), (2,3) interleaved, tile 4 plain;
@@ -235,16 +251,16 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   // next unit's prefetched K-tiles and waited for all of them (the residual shapes ran 17-23 % slower than
   // store-only, docs/OPEN_ITEMS.md round 5); compiler-tracked prefetch loads still got a vmcnt(0) (its
   // wait-count analysis does not credit the counted waits behind the per-group LDS-DMAs).
-  u32x2v pbias[5];
-  u32x4v pcs[5];
+  u32x2v pbias[NJ];
+  u32x4v pcs[NJ];
   u32x2v prs[4];
   u32x4v prw4[4][2];
   u32x2v prw2[4];
   auto prefetch = [&](int m0, int n0, bool hb, bool hr, bool tracked = PFE == 0) {
-    const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
+    const int m_w = m0 + wm * 64, n_w = n0 + grp * GW;
     if (hb) {
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         int col = n_w + colj(j);
         col = col < N ? col : N - 4;
         if (!tracked) untracked_load(pbias[j], e.bias + col);
@@ -253,7 +269,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     }
     if constexpr (LN) {
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         int col = n_w + colj(j);
         col = col < N ? col : N - 4;
         if (!tracked) untracked_load(pcs[j], e.cs + col);
@@ -279,17 +295,19 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           if (!tracked) untracked_load(prw4[i][p], rrow + col);
           else prw4[i][p] = *reinterpret_cast<const u32x4v*>(rrow + col);
         }
-        int col = n_w + 64 + 4 * fq;
-        col = col < N ? col : N - 4;
-        if (!tracked) untracked_load(prw2[i], rrow + col);
-        else prw2[i] = *reinterpret_cast<const u32x2v*>(rrow + col);
+        if constexpr (NJ == 5) {
+          int col = n_w + 64 + 4 * fq;
+          col = col < N ? col : N - 4;
+          if (!tracked) untracked_load(prw2[i], rrow + col);
+          else prw2[i] = *reinterpret_cast<const u32x2v*>(rrow + col);
+        }
       }
     }
   };
   // epilogue variants are separate straight-line paths (flags are wave-uniform)
   auto epilogue_t = [&](int m0, int n0, auto has_bias_c, auto has_res_c) {
     constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
-    const int m_w = m0 + wm * 64, n_w = n0 + grp * 80;
+    const int m_w = m0 + wm * 64, n_w = n0 + grp * GW;
     if constexpr (PFE == 0) prefetch(m0, n0, HB, HR);
     else if constexpr (PFE == 2) prefetch(m0, n0, false, HR, true);    // the residual
     // column tile 4 (8 B per lane and row): row blocks i / i+1 are paired with v_permlane16_swap so a
@@ -302,9 +320,9 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       if (row < M && col < N)
         *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{rx[0], ry[0], rx[1], ry[1]};
     };
-    float4 bv[5];
+    float4 bv[NJ];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) bv[j] = HB ? unpack4_bf16(uint2{pbias[j].x, pbias[j].y}) : float4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) bv[j] = HB ? unpack4_bf16(uint2{pbias[j].x, pbias[j].y}) : float4{0.f, 0.f, 0.f, 0.f};
     if constexpr (LN) {
       // LayerNorm folded in (MC_EPI_LNFOLD, see mfma_ppk.h): acc = rstd_r * (acc - mean_r * cs[c])
       float4 cv[5];
@@ -325,7 +343,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         }
       }
     }
-    uint2 rw[4][5];   // residual words
+    uint2 rw[4][NJ];   // residual words
     if (HR) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -334,7 +352,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           rw[i][2 * p] = uint2{prw4[i][p].x, prw4[i][p].y};
           rw[i][2 * p + 1] = uint2{prw4[i][p].z, prw4[i][p].w};
         }
-        rw[i][4] = uint2{prw2[i].x, prw2[i].y};
+        if constexpr (NJ == 5) rw[i][4] = uint2{prw2[i].x, prw2[i].y};
       }
     }
     auto val = [&](int i, int j) {
@@ -375,11 +393,11 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       return;
     }
     if constexpr (GNS) {
-      uint2 pk[4][5];
+      uint2 pk[4][NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 5; ++j) pk[i][j] = val(i, j);
+        for (int j = 0; j < NJ; ++j) pk[i][j] = val(i, j);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m_w + 16 * i + fr;
@@ -391,15 +409,17 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
                 uint4{pk[i][2 * p].x, pk[i][2 * p].y, pk[i][2 * p + 1].x, pk[i][2 * p + 1].y};
         }
       }
+      if constexpr (NJ == 5) {
 #pragma unroll
-      for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
+        for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
+      }
       if (m_w >= M) return;       // a partial last tile (GEMM rows: M % 256 != 0) -- no block past the tensor
       const int img = m_w / e.hw;
       const int nbk = e.hw >> 6;
       if constexpr (GNS == 2) {
         float* dq = e.gnp + (size_t)(img * nbk + ((m_w - img * e.hw) >> 6)) * N;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           float4 q = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -414,7 +434,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
       float* dst = e.gnp + (size_t)(img * nbk + ((m_w - img * e.hw) >> 6)) * N * 2;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         float4 u[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) u[i] = unpack4_bf16(pk[i][j]);
@@ -496,7 +516,8 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           *reinterpret_cast<uint4*>(e.C + (long long)row * e.ldc + col) = uint4{lo.x, lo.y, hi.x, hi.y};
       }
     }
-    if constexpr ((DS & 32) != 0) {   // A/B reference: 8-B stores for column tile 4
+    if constexpr (NJ == 4) {
+    } else if constexpr ((DS & 32) != 0) {   // A/B reference: 8-B stores for column tile 4
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m_w + 16 * i + fr, col = n_w + 64 + 4 * fq;
@@ -544,7 +565,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // one K-tile; PF: the unit's second-to-last, which issues the epilogue-operand prefetch after its counted wait
     auto ktile = [&](int kt, bool PF) {
       const unsigned char* S = smem + slot * STAGE;
