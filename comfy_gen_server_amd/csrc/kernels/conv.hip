@@ -969,9 +969,114 @@ __global__ __launch_bounds__(256) void conv_nhwc_smalln_kernel(ConvArgs a) {
   }
 }
 
+// The same narrow-output conv for its production form -- 3 x 3, stride 1, pad 1, one source, Cin % 32 == 0 (the
+// VAE decoder's conv_out, 128 -> 3 at full resolution; the UNet's 320 -> 4) -- with each 32-channel chunk of the
+// workgroup's 18 x 18 input halo staged through LDS once (register-staged, double-buffered: the next chunk's loads
+// are in flight while this one computes). The direct-load form re-read every input vector for each of the nine
+// taps from L1 / L2, and with several workgroups per CU the halos did not stay in L1 (2.3 ms per 8-image decode,
+// ~9x the input's bytes through L2). Pixel stride 80 B in LDS: the 16 lanes of a fragment read (16 consecutive
+// pixels, one 16-B chunk) hit distinct banks.
+#define SNL_PX 40   // u16 per staged pixel: 32 channels + 8 pad
+__global__ __launch_bounds__(256) void conv_nhwc_smalln_lds_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 halo[2][18 * 18 * SNL_PX];
+  constexpr int NV = 18 * 18 * 4, NS = (NV + 255) / 256;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_x = (a.Wo + 15) >> 4, tiles_y = (a.Ho + 15) >> 4;
+  const int bid = blockIdx.x;
+  const int n = bid / (tiles_x * tiles_y);
+  const int trem = bid - n * tiles_x * tiles_y;
+  const int ty = trem / tiles_x, tx = trem - ty * tiles_x;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int y0 = ty * 16 - 1, x0 = tx * 16 - 1;
+  const u16* img = a.in + (long long)n * a.H * a.W * a.Cin;
+  // staging slots of this thread: vector v = tid + 256 s -> (halo pixel v >> 2, 16-B chunk v & 3)
+  long long soff[NS];
+  bool sok[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int v = tid + 256 * s, p = v >> 2, ch = v & 3;
+    const int py = p / 18, px = p - py * 18, iy = y0 + py, ix = x0 + px;
+    sok[s] = v < NV && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    soff[s] = sok[s] ? ((long long)iy * a.W + ix) * a.Cin + 8 * ch : 0;
+  }
+  const s16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  s16x8 r[NS];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) r[s] = sok[s] ? *reinterpret_cast<const s16x8*>(img + soff[s] + c) : zero8;
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int v = tid + 256 * s;
+      if (v < NV) *reinterpret_cast<s16x8*>(&halo[buf][(v >> 2) * SNL_PX + 8 * (v & 3)]) = r[s];
+    }
+  };
+  const bool cv = fr < a.Cout;
+  const u16* wrow = a.w + (long long)(cv ? fr : 0) * 9 * a.Cin + 8 * fq;
+  f32x4 acc[SN_MB];
+#pragma unroll
+  for (int b = 0; b < SN_MB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 zb = {};
+  load(0);
+  put(0);
+  __syncthreads();
+  int buf = 0;
+  for (int c = 0; c < a.Cin; c += 32) {
+    const bool more = c + 32 < a.Cin;
+    if (more) load(c + 32);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const bf16x8 bfr = cv ? *reinterpret_cast<const bf16x8*>(wrow + (ky * 3 + kx) * a.Cin + c) : zb;
+#pragma unroll
+        for (int b = 0; b < SN_MB; ++b) {
+          const int p = (wave * SN_MB + b + ky) * 18 + fr + kx;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(&halo[buf][p * SNL_PX + 8 * fq]);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[b], 0, 0, 0);
+        }
+      }
+    if (more) put(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (!cv) return;
+  const float bv = (a.flags & EPI_BIAS) ? bf2f(a.bias[fr]) : 0.f;
+#pragma unroll
+  for (int b = 0; b < SN_MB; ++b) {
+    const int oy = ty * 16 + wave * SN_MB + b;
+    if (oy >= a.Ho) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int x = tx * 16 + fq * 4 + q;
+      if (x < a.Wo) {
+        const long long row = ((long long)n * a.Ho + oy) * a.Wo + x;
+        float v = acc[b][q] + bv;
+        if (a.flags & EPI_RESIDUAL) v += bf2f(a.res[row * a.Cout + fr]);
+        a.out[row * a.Cout + fr] = f2bf(v);
+      }
+    }
+  }
+}
+
+// CGS_SMALLN_LDS (default 1) / cgs_conv_smalln_set_lds: the LDS-staged form where it applies (A/B)
+static int g_smalln_lds = -1;
+static bool smalln_lds() {
+  if (g_smalln_lds < 0) g_smalln_lds = getenv("CGS_SMALLN_LDS") ? atoi(getenv("CGS_SMALLN_LDS")) != 0 : 1;
+  return g_smalln_lds != 0;
+}
+CGS_EXPORT void cgs_conv_smalln_set_lds(int on) { g_smalln_lds = on != 0; }
+
 static int conv_smalln_launch(const ConvArgs& a, hipStream_t stream) {
   const long long nwg = (long long)a.N * ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16);
   if (nwg > 0x7fffffffLL || nwg < 1) return (int)hipErrorInvalidValue;
+  if (smalln_lds() && a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && !(a.flags & CONV_UP2X) &&
+      a.in2 == nullptr && a.Cin % 32 == 0 && a.Ho == a.H && a.Wo == a.W && a.Cout <= 16 &&
+      (long long)a.H * a.W * a.Cin < (1ll << 31)) {
+    conv_nhwc_smalln_lds_kernel<<<(unsigned)nwg, 256, 0, stream>>>(a);
+    return (int)hipGetLastError();
+  }
   if (a.kh == 3 && a.kw == 3) conv_nhwc_smalln_kernel<3><<<(unsigned)nwg, 256, 0, stream>>>(a);
   else if (a.kh == 1 && a.kw == 1) conv_nhwc_smalln_kernel<1><<<(unsigned)nwg, 256, 0, stream>>>(a);
   else conv_nhwc_smalln_kernel<0><<<(unsigned)nwg, 256, 0, stream>>>(a);
