@@ -212,6 +212,7 @@ KERNEL_SIGNATURES = {
     "cgs_gemm_skinny_ws_bytes": [_I, _I, _I],
     # v6 GEMM + per-row LayerNorm statistics partials; partials -> (mean, rstd) rows
     "cgs_gemm_bf16_rowstats": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _P],
+    "cgs_gemm_bf16_rowstats_v": [_P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _I, _F, _P, _I, _P],
     "cgs_ln_rs_from_partials": [_P, _P, _I, _I, _F, _P],
     # v6 conv gather override (-1 auto, 1 ConvGatherK, 0 ConvGatherA8): in-process A/B
     "cgs_conv_v6_set_loader": [_I],

@@ -690,7 +690,8 @@ struct DenseKB {
 
 // ------------------------------------------------------------------------------------------------
 // v6: 256 x 160 x 64 ping-pong (mfma_pp160.h): whole-round tile counts on the SDXL channel widths.
-template <bool LN = false, int DS = 0, bool GG = false, bool ACT = false, bool RSO = false>
+// NI: 16-row MFMA blocks per wave -- 4 (256 x 160 tiles) or 2 (128 x 160: variant 19, the short-M grids)
+template <bool LN = false, int DS = 0, bool GG = false, bool ACT = false, bool RSO = false, int NI = 4>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
     const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
@@ -707,11 +708,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     al.lda = lda;
     al.M = M;
     al.init();
-    pq::run<DenseKB, LN, DS, false, GG, ACT, RSO>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+    pq::run<DenseKB, LN, DS, false, GG, ACT, RSO, 1, 5, NI>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
   } else {
     DenseA8 al{A, lda, M, {}};
-    pq::run<DenseA8, LN, DS, false, GG, ACT, RSO>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
+    pq::run<DenseA8, LN, DS, false, GG, ACT, RSO, 1, 5, NI>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n, group_m);
   }
+}
+// The one-wave-group form (pq::run W = 4): 128 x 80 tiles, 4 waves, two workgroups per CU -- variant 20 (the
+// batch-1 grids: M = 2048 x N = 1280 is 256 tiles, one per CU, where 256 x 160 gives 64 and 128 x 160 128).
+template <bool LN = false, bool RSO = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_bf16_nt_v6w4_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, u16* __restrict__ C, const u16* __restrict__ bias,
+    const u16* __restrict__ R, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+    int epi, float alpha, int tiles_m, int tiles_n, int group_m, const float* rs = nullptr, const float* cs = nullptr,
+    float* rso = nullptr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  mc::Epi e{C, bias, R, ldc, ldr, epi, alpha, rs, cs};
+  e.gnp = rso;
+  DenseA8 al{A, lda, M, {}};
+  pq::run<DenseA8, LN, 1, false, false, false, RSO, 1, 5, 2, 4>(al, W, ldw, M, N, K, e, smem, tiles_m, tiles_n,
+                                                                 group_m);
 }
 static int num_cus() {
   static int n = 0;
@@ -741,29 +757,69 @@ int v6_conv_ds() {
 }
 CGS_EXPORT void cgs_v6_set_mode(int m) { g_v6_ds = m; g_v6_conv_ds = m; }
 
-template <bool LN, int DS, bool GG = false, bool ACT = false, bool RSO = false>
+template <bool LN, int DS, bool GG = false, bool ACT = false, bool RSO = false, int NI = 4>
 static void gemm_v6_go(int grid, const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N,
                        int K, long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
                        int tiles_m, int tiles_n, hipStream_t stream, const float* rs, const float* cs,
                        float* rso = nullptr) {
+  constexpr int lds = pq::Geo<5, NI>::LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT, RSO>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, pq::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT, RSO, NI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT, RSO><<<grid, pq::THREADS, pq::LDS, stream>>>(
+  gemm_bf16_nt_v6_kernel<LN, DS, GG, ACT, RSO, NI><<<grid, pq::THREADS, lds, stream>>>(
       (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
       tiles_m, tiles_n, g_tile_group, rs, cs, rso);
 }
 
+template <bool LN, bool RSO>
+static int gemm_v6w4_go(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                        long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
+                        hipStream_t stream, const float* rs, const float* cs, float* rso) {
+  using Gm = pq::Geo<5, 2, 4>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_nt_v6w4_kernel<LN, RSO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Gm::LDS);
+    attr_set = true;
+  }
+  const int tiles_n = (N + Gm::BN - 1) / Gm::BN;
+  const int tiles_m = (M + Gm::BM - 1) / Gm::BM;
+  const long long T = (long long)tiles_m * tiles_n;
+  const int grid = (int)(T < 2 * num_cus() ? T : 2 * num_cus());
+  gemm_bf16_nt_v6w4_kernel<LN, RSO><<<grid, 256, Gm::LDS, stream>>>(
+      (const u16*)A, (const u16*)W, (u16*)C, (const u16*)bias, (const u16*)R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+      tiles_m, tiles_n, g_tile_group, rs, cs, rso);
+  return (int)hipGetLastError();
+}
+
 static int gemm_v6_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                           long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha,
-                          hipStream_t stream, const float* rs = nullptr, const float* cs = nullptr) {
+                          hipStream_t stream, const float* rs = nullptr, const float* cs = nullptr, int ni = 4) {
+  if (ni == 1) {   // variant 20: 128 x 80 tiles, one wave group (plain / bias / residual or LayerNorm-folded)
+    if (epi & (EPI_GELU | EPI_GEGLU)) return (int)hipErrorInvalidValue;
+    if (epi & EPI_LNFOLD)
+      return gemm_v6w4_go<true, false>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs,
+                                       nullptr);
+    return gemm_v6w4_go<false, false>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, rs, cs,
+                                      nullptr);
+  }
   const int tiles_n = (N + pq::BN - 1) / pq::BN;
-  const int tiles_m = (M + pq::BM - 1) / pq::BM;
+  const int tiles_m = (M + 64 * ni - 1) / (64 * ni);
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
+  if (ni == 2) {   // 128 x 160 tiles (variant 19): plain / bias / residual or LayerNorm-folded, default DMA split
+    if (epi & (EPI_GELU | EPI_GEGLU)) return (int)hipErrorInvalidValue;
+    if (epi & EPI_LNFOLD)
+      gemm_v6_go<true, 1, false, false, false, 2>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+                                                  tiles_m, tiles_n, stream, rs, cs);
+    else
+      gemm_v6_go<false, 1, false, false, false, 2>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+                                                   tiles_m, tiles_n, stream, rs, cs);
+    return (int)hipGetLastError();
+  }
   int ds = v6_ds();
   if ((long long)M * lda * 2 >= (1ll << 31)) ds &= ~64;    // buffer-descriptor forms need < 2 GiB operands
   if ((long long)N * ldw * 2 >= (1ll << 31)) ds &= ~128;
@@ -857,20 +913,42 @@ CGS_EXPORT int cgs_gemm_bf16_gelu_gns(const void* A, const void* W, void* C, con
 // v6 GEMM (bias / residual epilogue) that also writes per-row LayerNorm statistics partials of its output
 // (pq::run RSO): part = [M][N / 80] (mean, M2) float pairs; cgs_ln_rs_from_partials turns them into the
 // (mean, rstd) rows a LayerNorm-folded GEMM reads. N % 160 == 0, K % 64 == 0, K >= 128.
+static int gemm_rowstats(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                         long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha, float* part,
+                         int ni, hipStream_t stream);
 CGS_EXPORT int cgs_gemm_bf16_rowstats(const void* A, const void* W, void* C, const void* bias, const void* R, int M,
                                       int N, int K, long long lda, long long ldw, long long ldc, long long ldr, int epi,
                                       float alpha, float* part, hipStream_t stream) {
+  return gemm_rowstats(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, part, 4, stream);
+}
+// variant 6 (256 x 160) or 19 (128 x 160 tiles)
+CGS_EXPORT int cgs_gemm_bf16_rowstats_v(const void* A, const void* W, void* C, const void* bias, const void* R, int M,
+                                        int N, int K, long long lda, long long ldw, long long ldc, long long ldr,
+                                        int epi, float alpha, float* part, int variant, hipStream_t stream) {
+  if (variant != 6 && variant != 19 && variant != 20) return (int)hipErrorInvalidValue;
+  return gemm_rowstats(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, part,
+                       variant == 20 ? 1 : variant == 19 ? 2 : 4, stream);
+}
+static int gemm_rowstats(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
+                         long long lda, long long ldw, long long ldc, long long ldr, int epi, float alpha, float* part,
+                         int ni, hipStream_t stream) {
   if (!part || N % 160 || K % 64 || K < 128 || (epi & ~(EPI_BIAS | EPI_RESIDUAL)) || lda % 8 || ldw % 8 ||
       ldc % 8 || ((epi & EPI_RESIDUAL) && ldr % 8) || ((uintptr_t)bias % 8) ||
       ((((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)R)) % 16) || ((uintptr_t)part % 8))
     return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
+  if (ni == 1) return gemm_v6w4_go<false, true>(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream,
+                                                nullptr, nullptr, part);
   const int tiles_n = N / pq::BN;
-  const int tiles_m = (M + pq::BM - 1) / pq::BM;
+  const int tiles_m = (M + 64 * ni - 1) / (64 * ni);
   const long long T = (long long)tiles_m * tiles_n;
   const int grid = (int)(T < num_cus() ? T : num_cus());
-  gemm_v6_go<false, 1, false, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m,
-                                           tiles_n, stream, nullptr, nullptr, part);
+  if (ni == 2)
+    gemm_v6_go<false, 1, false, false, true, 2>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha,
+                                                tiles_m, tiles_n, stream, nullptr, nullptr, part);
+  else
+    gemm_v6_go<false, 1, false, false, true>(grid, A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, tiles_m,
+                                             tiles_n, stream, nullptr, nullptr, part);
   return (int)hipGetLastError();
 }
 
@@ -1203,6 +1281,10 @@ static int gemm_dispatch(const void* A, const void* W, void* C, const void* bias
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 6 && (!(epi & EPI_GEGLU) || (N % 160 == 0 && !(epi & EPI_RESIDUAL))) &&
       ((uintptr_t)bias % 8 == 0))
     return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream);
+  if (v3_ok && K % 64 == 0 && K >= 128 && (variant == 19 || variant == 20) && !(epi & EPI_GEGLU) &&
+      ((uintptr_t)bias % 8 == 0))
+    return gemm_v6_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, stream, nullptr, nullptr,
+                          variant == 20 ? 1 : 2);
   if (v3_ok && K % 64 == 0 && K >= 128 && variant == 7 && !((epi & EPI_GEGLU) && (epi & EPI_RESIDUAL)) &&
       ((uintptr_t)bias % 8 == 0) && (long long)M * lda * 2 < (1ll << 32) && (long long)N * ldw * 2 < (1ll << 32))
     return gemm_v7_launch(A, W, C, bias, R, M, N, K, lda, ldw, ldc, ldr, epi, alpha, ws, ws_bytes, stream);
@@ -1297,6 +1379,11 @@ static int gemm_lnfold(const void* A, const void* W, void* C, const void* bias, 
                           rs, cs);
   const bool v6_ok = N % 160 == 0;   // incl. GEGLU (pq::run GG)
   if (variant == 6 && !v6_ok) return (int)hipErrorInvalidValue;
+  if (variant == 19 || variant == 20) {     // 128 x 160 / 128 x 80 tiles: no GEGLU form
+    if (N % 80 || (variant == 19 && !v6_ok) || (epi & EPI_GEGLU)) return (int)hipErrorInvalidValue;
+    return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs,
+                          variant == 20 ? 1 : 2);
+  }
   if (variant == 6 || (variant < 0 && v6_ok && !(epi & EPI_GEGLU) && N <= 1280))
     return gemm_v6_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, stream, rs, cs);
   return gemm_v7_launch(A, W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0, epi | EPI_LNFOLD, 1.0f, ws, ws_bytes, stream,

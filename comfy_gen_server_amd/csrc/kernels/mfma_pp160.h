@@ -45,12 +45,21 @@ constexpr int STAGE = A_BYTES + B_BYTES;
 constexpr int LDS = 3 * STAGE;     // 156 KiB
 // NJ = 4 (run<..., NJ>): the 256 x 128 form -- 2 groups x 64 columns, no column tile 4 -- for Cout = 128 convs
 // (the VAE's full-resolution ResnetBlocks: a 160-wide tile wastes 20 % of its columns there, a 256-wide one half).
-template <int NJ>
+// NI = 2 (run<..., NI>): 128-row tiles (the 4 row waves 32 rows each) -- twice the tiles where M is short (SDXL
+// batch 1: M = 2048 tokens at level 2 gives 64 256 x 160 tiles, 128 of 128 x 160).
+// W = 4 (run<..., W>): one wave group (4 waves, 256 threads) -- 128 x 80 tiles with NI = 2, two workgroups per CU
+// (each SIMD pairs waves of two workgroups); the batch-1 grids (M = 2048 x N = 1280: 256 tiles, one per CU).
+template <int NJ, int NI = 4, int W = 8>
 struct Geo {
-  static constexpr int BN = 32 * NJ, GW = 16 * NJ;             // tile / wave-group columns
+  static constexpr int GW = 16 * NJ, BN = GW * (W / 4);         // wave-group / tile columns
+  static constexpr int BM = 64 * NI;                            // tile rows (4 row waves x 16 NI)
+  static constexpr int PR = 8 * W;                              // rows per DMA piece (W waves x 8 rows x 128 B)
+  static constexpr int NA = BM / PR;                            // A DMA pieces
+  static constexpr int A_BYTES = BM * 128;
   static constexpr int B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES, LDS = 3 * STAGE;
-  static constexpr int NBG = (BN + 63) / 64;                    // 64-row B DMA pieces (the last: group 0 only
-  static constexpr bool B_HALF = BN % 64 != 0;                  //   when BN % 64 == 32)
+  static constexpr int NBG = (BN + PR - 1) / PR;                // B DMA pieces; the last one, when BN % PR != 0,
+  static constexpr int REM = BN % PR;                           //   only by the waves below REM / 8
+  static constexpr bool B_HALF = REM != 0;
 };
 
 // Tile column staged at B row r. Wave group g reads rows g*80 + 16j + (4fq + t) as MFMA column tile
@@ -106,17 +115,20 @@ __device__ __forceinline__ int gg_row160(int r) {
 // `prefetch` -- with the last two K-tiles peeled (1), or only bias / LN statistics, inside the K loop (2: the
 // conv gathers, whose peeled loop and whose prefetched residual spilled), or loaded in the epilogue (0).
 template <class AL, bool LN = false, int DS = 0, int GNS = 0, bool GG = false, bool ACT = false,
-          bool RSO = false, int PFE = 1, int NJ = 5>
+          bool RSO = false, int PFE = 1, int NJ = 5, int NI = 4, int NW = 8>
 __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long ldw, int M, int N, int K,
                                     const mc::Epi& e, unsigned char* smem, int tiles_m, int tiles_n, int group_m) {
   static_assert(NJ == 5 || NJ == 4, "column tiles per wave group");
   static_assert(NJ == 5 || (!GG && !RSO && !LN), "NJ = 4: plain / residual / GroupNorm-statistics epilogues");
-  using Gm = Geo<NJ>;
-  constexpr int BN = Gm::BN, GW = Gm::GW, STAGE = Gm::STAGE;
+  static_assert(NI == 4 || NI == 2, "16-row MFMA blocks per wave");
+  static_assert(NI == 4 || GNS == 0, "NI = 2: the GroupNorm partials are laid out in 64-row blocks");
+  static_assert(NW == 8 || NW == 4, "waves per workgroup");
+  using Gm = Geo<NJ, NI, NW>;
+  constexpr int BN = Gm::BN, GW = Gm::GW, STAGE = Gm::STAGE, BMv = Gm::BM, A_BYTESv = Gm::A_BYTES;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2;
+  const int grp = NW == 8 ? wave >> 2 : 0;
   const int wm = wave & 3;
   const int nk = K / BK;
   const int T = tiles_m * tiles_n;
@@ -127,7 +139,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   auto coords = [&](int l, int& m0, int& n0) {
     int tm, tn;
     grouped_tile(l, tiles_m, tiles_n, group_m, tm, tn);
-    m0 = tm * BM;
+    m0 = tm * BMv;
     n0 = tn * BN;
   };
 
@@ -145,10 +157,10 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   auto setup = [&](int m0, int n0) {
     if constexpr (mc::own_dma<AL>::value) al.tile(m0);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) al.setup(g, m0 + g * 64 + lrow);
+    for (int g = 0; g < Gm::NA; ++g) al.setup(g, m0 + g * Gm::PR + lrow);
 #pragma unroll
     for (int g = 0; g < Gm::NBG; ++g) {
-      const int r = g * 64 + lrow;
+      const int r = g * Gm::PR + lrow;
       int n = n0 + (GG ? gg_row160(r < BN ? r : BN - 1) : b_col160<NJ>(r < BN ? r : BN - 1));
       n = n < N ? n : N - 1;
       if constexpr ((DS & 128) != 0) boff[g] = (uint32_t)(((long long)n * ldw + 8 * (lch ^ ((r >> 1) & 7))) * 2);
@@ -157,17 +169,18 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   };
   // A slot g / B row group g of K-tile kt into ring slot `slot`
   auto dma_a = [&](int g, int kt, int slot) {
-    if constexpr (mc::own_dma<AL>::value) al.dma(g, kt * BK, smem + slot * STAGE + wave * 1024 + g * 8192);
-    else mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * 8192);
+    if (g >= Gm::NA) return;
+    if constexpr (mc::own_dma<AL>::value) al.dma(g, kt * BK, smem + slot * STAGE + wave * 1024 + g * (Gm::PR * 128));
+    else mc::lds_dma16(al.src(g, kt * BK), smem + slot * STAGE + wave * 1024 + g * (Gm::PR * 128));
   };
   auto dma_b = [&](int g, int kt, int slot) {
     if (g >= Gm::NBG) return;
-    if (!Gm::B_HALF || g < Gm::NBG - 1 || grp == 0) {  // BN = 160: B rows 128..159 by group 0 only
+    if (!Gm::B_HALF || g < Gm::NBG - 1 || wave < Gm::REM / 8) {  // BN = 160: B rows 128..159 by group 0 only
       if constexpr ((DS & 128) != 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (mc_lds_void*)(smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192),
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (mc_lds_void*)(smem + slot * STAGE + wave * 1024 + A_BYTESv + g * (Gm::PR * 128)),
                                                  16, boff[g], kt * BK * 2, 0, 0);
       else
-        mc::lds_dma16((const void*)(bsrc[g] + kt * BK), smem + slot * STAGE + wave * 1024 + A_BYTES + g * 8192);
+        mc::lds_dma16((const void*)(bsrc[g] + kt * BK), smem + slot * STAGE + wave * 1024 + A_BYTESv + g * (Gm::PR * 128));
     }
   };
   // the phase-0 (part 0) / phase-1 (part 1) DMAs of K-tile kt: DS & 3 = 0 all in phase 0, 1 A | B,
@@ -207,21 +220,21 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     if constexpr ((DS & 3) != 0) stage_part(1, kt, slot);
   };
   auto wait_tile = [&]() {   // all but one K-tile's DMAs (BN = 160: 7 in group 0, 6 in group 1) retired
-    if (grp == 0) mc::wait_vmcnt<4 + Gm::NBG>();
-    else mc::wait_vmcnt<4 + Gm::NBG - (Gm::B_HALF ? 1 : 0)>();
+    if (!Gm::B_HALF || wave < Gm::REM / 8) mc::wait_vmcnt<Gm::NA + Gm::NBG>();
+    else mc::wait_vmcnt<Gm::NA + Gm::NBG - 1>();
   };
 
-  f32x4 acc[4][NJ];
+  f32x4 acc[NI][NJ];
   const int fr = lane & 15, fq = lane >> 4;
-  bf16x8 af[4], bfr[NJ];
+  bf16x8 af[NI], bfr[NJ];
   auto read_frags = [&](const unsigned char* S, int kk) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + 16 * i + fr;
+    for (int i = 0; i < NI; ++i) {
+      const int r = wm * (16 * NI) + 16 * i + fr;
       const int c = (4 * kk + fq) ^ ((r >> 1) & 7);
       af[i] = *reinterpret_cast<const bf16x8*>(S + r * 128 + 16 * c);
     }
-    const unsigned char* SB = S + A_BYTES;
+    const unsigned char* SB = S + A_BYTESv;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int r = grp * GW + 16 * j + fr;
@@ -232,7 +245,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   auto mma = [&]() {   // C^T tiles: lane (fr, fq) accumulates C[16i + fr][16j + 4fq + 0..3]
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
@@ -253,11 +266,11 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   // wait-count analysis does not credit the counted waits behind the per-group LDS-DMAs).
   u32x2v pbias[NJ];
   u32x4v pcs[NJ];
-  u32x2v prs[4];
-  u32x4v prw4[4][2];
-  u32x2v prw2[4];
+  u32x2v prs[NI];
+  u32x4v prw4[NI][2];
+  u32x2v prw2[NI];
   auto prefetch = [&](int m0, int n0, bool hb, bool hr, bool tracked = PFE == 0) {
-    const int m_w = m0 + wm * 64, n_w = n0 + grp * GW;
+    const int m_w = m0 + wm * (16 * NI), n_w = n0 + grp * GW;
     if (hb) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -276,7 +289,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         else pcs[j] = *reinterpret_cast<const u32x4v*>(e.cs + col);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         int row = m_w + 16 * i + fr;
         row = row < M ? row : M - 1;
         if (!tracked) untracked_load(prs[i], e.rs + 2 * (long long)row);
@@ -284,7 +297,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
     } else if (hr) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         int row = m_w + 16 * i + fr;
         row = row < M ? row : M - 1;
         const u16* rrow = e.R + (long long)row * e.ldr;
@@ -307,7 +320,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   // epilogue variants are separate straight-line paths (flags are wave-uniform)
   auto epilogue_t = [&](int m0, int n0, auto has_bias_c, auto has_res_c) {
     constexpr bool HB = decltype(has_bias_c)::value, HR = decltype(has_res_c)::value;
-    const int m_w = m0 + wm * 64, n_w = n0 + grp * GW;
+    const int m_w = m0 + wm * (16 * NI), n_w = n0 + grp * GW;
     if constexpr (PFE == 0) prefetch(m0, n0, HB, HR);
     else if constexpr (PFE == 2) prefetch(m0, n0, false, HR, true);    // the residual
     // column tile 4 (8 B per lane and row): row blocks i / i+1 are paired with v_permlane16_swap so a
@@ -331,7 +344,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         cv[j] = float4{__uint_as_float(pcs[j].x), __uint_as_float(pcs[j].y), __uint_as_float(pcs[j].z),
                        __uint_as_float(pcs[j].w)};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const float2 st = float2{__uint_as_float(prs[i].x), __uint_as_float(prs[i].y)};
         const float mr = st.x * st.y;
 #pragma unroll
@@ -343,10 +356,10 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         }
       }
     }
-    uint2 rw[4][NJ];   // residual words
+    uint2 rw[NI][NJ];   // residual words
     if (HR) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           rw[i][2 * p] = uint2{prw4[i][p].x, prw4[i][p].y};
@@ -373,7 +386,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       const int oc0 = n0 / 2 + grp * 40 + 4 * (fq & 1);
       const int Nout = N / 2;
 #pragma unroll
-      for (int i = 0; i < 4; i += 2) {
+      for (int i = 0; i < NI; i += 2) {
         const int row = m_w + 16 * (i + (fq >> 1)) + fr;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -393,13 +406,13 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       return;
     }
     if constexpr (GNS) {
-      uint2 pk[4][NJ];
+      uint2 pk[NI][NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) pk[i][j] = val(i, j);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const int row = m_w + 16 * i + fr;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -411,7 +424,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
       if constexpr (NJ == 5) {
 #pragma unroll
-        for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
+        for (int i = 0; i < NI; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
       }
       if (m_w >= M) return;       // a partial last tile (GEMM rows: M % 256 != 0) -- no block past the tensor
       const int img = m_w / e.hw;
@@ -422,7 +435,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         for (int j = 0; j < NJ; ++j) {
           float4 q = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < NI; ++i) {
             const float4 u = unpack4_bf16(pk[i][j]);
             q.x += u.x * u.x; q.y += u.y * u.y; q.z += u.z * u.z; q.w += u.w * u.w;
           }
@@ -437,7 +450,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       for (int j = 0; j < NJ; ++j) {
         float4 u[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) u[i] = unpack4_bf16(pk[i][j]);
+        for (int i = 0; i < NI; ++i) u[i] = unpack4_bf16(pk[i][j]);
         float4 mu = u[0];
 #pragma unroll
         for (int i = 1; i < 4; ++i) { mu.x += u[i].x; mu.y += u[i].y; mu.z += u[i].z; mu.w += u[i].w; }
@@ -445,7 +458,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         mu = float4{row16_sum(mu.x) * inv, row16_sum(mu.y) * inv, row16_sum(mu.z) * inv, row16_sum(mu.w) * inv};
         float4 q = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NI; ++i) {
           const float dx = u[i].x - mu.x, dy = u[i].y - mu.y, dz = u[i].z - mu.z, dw = u[i].w - mu.w;
           q.x += dx * dx; q.y += dy * dy; q.z += dz * dz; q.w += dw * dw;
         }
@@ -460,13 +473,13 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       return;
     }
     if constexpr (RSO) {
-      uint2 pk[4][5];
+      uint2 pk[NI][5];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 5; ++j) pk[i][j] = val(i, j);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const int row = m_w + 16 * i + fr;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -477,12 +490,12 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
         }
       }
 #pragma unroll
-      for (int i = 0; i < 4; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
+      for (int i = 0; i < NI; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
       // row (16 i + fr) of this wave's 80 columns: 20 values in each of the 4 lanes fr + 16 fq
       const int P = N / 80;
       const int chunk = n_w / 80;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const float sh = __shfl(unpack4_bf16(pk[i][0]).x, fr, 64);   // shift: the chunk's value of lane fr
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -506,7 +519,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       return;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int row = m_w + 16 * i + fr;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
@@ -519,14 +532,14 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     if constexpr (NJ == 4) {
     } else if constexpr ((DS & 32) != 0) {   // A/B reference: 8-B stores for column tile 4
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const int row = m_w + 16 * i + fr, col = n_w + 64 + 4 * fq;
         const uint2 w4 = val(i, 4);
         if (row < M && col < N) *reinterpret_cast<uint2*>(e.C + (long long)row * e.ldc + col) = w4;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; i += 2) store_t4(i, val(i, 4), val(i + 1, 4));
+      for (int i = 0; i < NI; i += 2) store_t4(i, val(i, 4), val(i + 1, 4));
     }
   };
   using T0 = std::false_type;
@@ -554,7 +567,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
   stage(nk > 1 ? 1 : 0, 1);
   wait_tile();
   pp::barrier();
-  if (grp == 1) pp::barrier();   // stagger: group 1 runs one segment behind group 0
+  if (NW == 8 && grp == 1) pp::barrier();   // stagger: group 1 runs one segment behind group 0
 
   int slot = 0;                  // ring slot of the K-tile being consumed
   while (true) {
@@ -563,7 +576,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     int nm0 = 0, nn0 = 0;
     if (has_next) coords(ln, nm0, nn0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // one K-tile; PF: the unit's second-to-last, which issues the epilogue-operand prefetch after its counted wait
@@ -612,7 +625,7 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
     m0 = nm0;
     n0 = nn0;
   }
-  if (grp == 0) pp::barrier();   // balance the stagger
+  if (NW == 8 && grp == 0) pp::barrier();   // balance the stagger
   mc::wait_vmcnt<0>();           // the trailing dummy DMAs must land before the LDS is released
 }
 

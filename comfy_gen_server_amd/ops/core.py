@@ -145,12 +145,13 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             o = dst if dst is not None else torch.empty((M, N), device=x.device, dtype=x.dtype)
             if isinstance(variant, str):                       # split-K (batch-1 grids)
                 return _splitk_run(a, w, o, bias, r, None, None, M, N, K, epi, variant)
-            if (final and row_stats and variant == 6 and not gelu and N % 160 == 0 and K % 64 == 0 and K >= 128
-                    and _RSO and _native.has_kernel("cgs_gemm_bf16_rowstats")):
+            if (final and row_stats and variant in (6, 19, 20) and not gelu and N % 160 == 0 and K % 64 == 0
+                    and K >= 128 and _RSO and _native.has_kernel("cgs_gemm_bf16_rowstats_v")):
                 part = torch.empty((M, N // 80, 2), device=x.device, dtype=torch.float32)
-                _check(_lib().cgs_gemm_bf16_rowstats(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),
-                                                     M, N, K, a.stride(0), K, N, N if r is not None else 0, epi, 1.0,
-                                                     part.data_ptr(), _stream()), "cgs_gemm_bf16_rowstats")
+                _check(_lib().cgs_gemm_bf16_rowstats_v(a.data_ptr(), w.data_ptr(), o.data_ptr(), _ptr(bias), _ptr(r),
+                                                       M, N, K, a.stride(0), K, N, N if r is not None else 0, epi,
+                                                       1.0, part.data_ptr(), variant, _stream()),
+                       "cgs_gemm_bf16_rowstats_v")
                 rs_part.append(part)
                 return o
             if M <= 128 and variant in (-1, -2) and K % 32 == 0 and (a.data_ptr() | w.data_ptr()) % 16 == 0:
@@ -193,6 +194,10 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
                 cands.append(("v8", lambda: run_hip(8)))      # 128 x 128 tiles (short M / N grids)
                 if _underfilled(M, N):    # 64x128 / 128x64 tiles, 4- and 6-stage rings (batch-1 grids)
                     cands += [(f"v{v}", (lambda v=v: run_hip(v))) for v in _SMALL_TILE]
+                    if K % 64 == 0 and K >= 128 and N % 160 == 0 and not gelu:   # 128 x 160 v6 tiles
+                        cands.append(("v6m128", lambda: run_hip(V6_M128)))
+                    if K % 64 == 0 and K >= 128 and N % 80 == 0 and not gelu:    # 128 x 80, 4-wave v6
+                        cands.append(("v6w4", lambda: run_hip(V6_W4)))
                     if (a.stride(0) % 8 == 0 and (bias is None or bias.data_ptr() % 16 == 0)
                             and (r is None or r.data_ptr() % 16 == 0)):
                         cands += _splitk_cands(M, N, K, epi, run_hip)
@@ -207,7 +212,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
             return run_lib().view(*x.shape[:-1], N)
         count("gemm", "hip")
         variant = choice if choice in _SPLITK else {"v7": 7, "v6": 6, "v5": 5, "v4": 4, "v8": 8, "w6": W6,
-                                                    "w6n160": W6_160, **_SMALL_NAMES}.get(choice, -2)
+                                                    "w6n160": W6_160, "v6m128": V6_M128, "v6w4": V6_W4,
+                                                    **_SMALL_NAMES}.get(choice, -2)
         y = run_hip(variant, final=True).view(*x.shape[:-1], N)
         if rs_part:
             # (no version counter: inference-mode tensors have none; the consumers take the partials only
@@ -1439,10 +1445,13 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
         cands = [("v7", lambda: run(-1)), ("v8", lambda: run(8))] + [(f"v{v}", (lambda v=v: run(v))) for v in _SMALL_TILE]
         if N % 160 == 0:    # 256x160 tiles (plain or GEGLU): whole rounds where 256x256 leaves a partial one
             cands.append(("v6", lambda: run(6)))
+            if not geglu:   # 128 x 160 tiles, and 128 x 80 with one wave group
+                cands += [("v6m128", lambda: run(V6_M128)), ("v6w4", lambda: run(V6_W4))]
         if not geglu:
             cands += _splitk_cands(M, N, K, epi | EPI_LNFOLD, run)
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi), cands + w6, default="v7")
         variant = choice if choice in _SPLITK else {"v8": 8, "v6": 6, "w6": W6, "w6n160": W6_160,
+                                                    "v6m128": V6_M128, "v6w4": V6_W4,
                                                     **_SMALL_NAMES}.get(choice, -1)
     elif geglu and N % 160 == 0 and _native.has_kernel("cgs_gemm_bf16_lnfold_v"):
         choice = autotune.choose(("gemm_lnfold", M, N, K, epi),
@@ -1461,6 +1470,8 @@ def linear_lnfold(x: torch.Tensor, rs: torch.Tensor, w2: torch.Tensor, cs: torch
 
 
 W6, W6_160 = 16, 17      # gemm_w6.hip (256 / 160-wide tiles) through cgs_gemm_bf16_v / _lnfold_v
+V6_M128 = 19             # v6 with 128 x 160 tiles (pq::run NI = 2): the short-M grids
+V6_W4 = 20               # v6 with 128 x 80 tiles, 4 waves, two workgroups per CU (pq::run NW = 4): batch-1 grids
 
 
 def _w6_ok(M, N, K, epi, bn=256) -> bool:

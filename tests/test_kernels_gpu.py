@@ -1372,6 +1372,52 @@ def test_gemm_rowstats_epilogue(cuda, M, N, K, res):
     assert ((rs[:, 1] - rstd).abs() / rstd).max().item() < 1e-3
 
 
+# v6 with 128 x 160 tiles (variant 19, pq::run NI = 2) and its one-wave-group 128 x 80 form (variant 20, NW = 4):
+# partial M tiles, every epilogue they carry (bias, residual, LayerNorm fold, row-statistics partials) against fp32.
+@pytest.mark.parametrize("M,N,K", [(300, 160, 128), (2048, 1280, 1280), (8200, 640, 640), (129, 320, 2560)])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_res", "ln", "rowstats"])
+@pytest.mark.parametrize("variant", [19, 20], ids=["v6m128", "v6w4"])
+def test_gemm_v6_m128(cuda, M, N, K, epi, variant):
+    torch.manual_seed(11)
+    lib = core._lib()
+    s = core._stream()
+    a = (torch.randn(M, K, device=cuda) * (2 if epi == "ln" else 1) + (1 if epi == "ln" else 0)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16) if epi != "none" else None
+    r = torch.randn(M, N, device=cuda).to(torch.bfloat16) if epi in ("bias_res", "rowstats") else None
+    y = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    if epi == "ln":
+        mu = a.float().mean(1)
+        rstd = torch.rsqrt(a.float().var(1, unbiased=False) + 1e-5)
+        rs = torch.stack([mu, rstd], 1).contiguous()
+        cs = w.float().sum(1).contiguous()
+        assert lib.cgs_gemm_bf16_lnfold_v(a.data_ptr(), w.data_ptr(), y.data_ptr(), b.data_ptr(), rs.data_ptr(),
+                                          cs.data_ptr(), M, N, K, K, K, N, 1, None, 0, variant, s) == 0
+        ref = ((a.float() - mu[:, None]) * rstd[:, None]) @ w.float().t() + b.float()
+    else:
+        e = (1 if b is not None else 0) | (2 if r is not None else 0)
+        if epi == "rowstats":
+            part = torch.empty(M, N // 80, 2, device=cuda, dtype=torch.float32)
+            assert lib.cgs_gemm_bf16_rowstats_v(a.data_ptr(), w.data_ptr(), y.data_ptr(), b.data_ptr(), r.data_ptr(),
+                                                M, N, K, K, K, N, N, e, 1.0, part.data_ptr(), variant, s) == 0
+            y6 = torch.empty_like(y)
+            assert lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), y6.data_ptr(), b.data_ptr(), r.data_ptr(), M, N, K,
+                                       K, K, N, N, e, 1.0, variant, s) == 0
+            rsp = torch.empty(M, 2, device=cuda, dtype=torch.float32)
+            assert lib.cgs_ln_rs_from_partials(part.data_ptr(), rsp.data_ptr(), M, N // 80, 1e-5, s) == 0
+        else:
+            assert lib.cgs_gemm_bf16_v(a.data_ptr(), w.data_ptr(), y.data_ptr(), core._ptr(b), core._ptr(r), M, N, K,
+                                       K, K, N, N if r is not None else 0, e, 1.0, variant, s) == 0
+        ref = a.float() @ w.float().t() + (b.float() if b is not None else 0) + (r.float() if r is not None else 0)
+    torch.cuda.synchronize()
+    assert _rel(y, ref) < 1e-2
+    if epi == "rowstats":
+        assert torch.equal(y, y6)
+        yf = y.float()
+        assert torch.allclose(rsp[:, 0], yf.mean(1), atol=1e-3, rtol=1e-3)
+        assert torch.allclose(rsp[:, 1], torch.rsqrt(yf.var(1, unbiased=False) + 1e-5), rtol=2e-3)
+
+
 def test_transformer_block_rowstats_matches(cuda, monkeypatch):
     """SDXL transformer block with the LayerNorm statistics taken from the producing GEMMs' epilogues vs the
     statistics pass (CGS_LN_ROWSTATS off): same output; the block output carries its partials."""
