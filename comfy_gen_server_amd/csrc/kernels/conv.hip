@@ -715,6 +715,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                                               a.group_m);
 }
 
+// One-wave-group form (pq::run NW = 4, NI = 2): 128 x 80 tiles, 4 waves, two workgroups per CU -- variant 21,
+// for the batch-1 grids (SDXL level 2 at batch 2: M = 2048 output pixels x Cout = 1280 is 256 tiles).
+template <int LD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_nhwc_v6w4_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.N * a.Ho * a.Wo;
+  const int K = a.kh * a.kw * a.Cin;
+  typename std::conditional<
+      LD == 3, ConvGatherKU,
+      typename std::conditional<LD == 2, ConvGatherKD,
+                                typename std::conditional<LD == 1, ConvGatherK<true>, ConvGatherA8>::type>::type>::type al;
+  al.a = &a;
+  if constexpr (LD >= 2) al.init();
+  mc::Epi e{a.out, a.bias, a.res, a.Cout, a.Cout, a.flags & (EPI_BIAS | EPI_RESIDUAL), 1.0f};
+  using Gm = pq::Geo<5, 2, 4>;
+  pq::run<decltype(al), false, 51, false, false, false, false, 0, 5, 2, 4>(al, a.w, K, M, a.Cout, K, e, smem,
+                                                                          (M + Gm::BM - 1) / Gm::BM, a.tiles_n,
+                                                                          a.group_m);
+}
+
 static int conv_num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -740,6 +760,31 @@ static void conv_v6_launch(ConvArgs& a, int grid, hipStream_t stream) {
 }
 
 
+
+static void conv_v6w4_go(ConvArgs& a, hipStream_t stream) {
+  using Gm = pq::Geo<5, 2, 4>;
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = (a.Cout + Gm::BN - 1) / Gm::BN;
+  const long long T = (long long)((M + Gm::BM - 1) / Gm::BM) * a.tiles_n;
+  const int grid = (int)(T < 2 * conv_num_cus() ? T : 2 * conv_num_cus());
+  int ld = conv_fast_ok(a) ? (conv_kd(a) ? 2 : 1) : ((a.flags & CONV_UP2X) && conv_kd(a) ? 3 : 0);
+  if (g_conv_v6_ld >= 0 && g_conv_v6_ld < ld) ld = ld == 3 ? 0 : g_conv_v6_ld;
+  if (ld) conv_magic(a);
+  auto go = [&](auto lc) {
+    constexpr int L = decltype(lc)::value;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv_nhwc_v6w4_kernel<L>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Gm::LDS);
+      attr = true;
+    }
+    conv_nhwc_v6w4_kernel<L><<<grid, 256, Gm::LDS, stream>>>(a);
+  };
+  if (ld == 3) go(std::integral_constant<int, 3>{});
+  else if (ld == 2) go(std::integral_constant<int, 2>{});
+  else if (ld == 1) go(std::integral_constant<int, 1>{});
+  else go(std::integral_constant<int, 0>{});
+}
 
 static void conv_v6_go(ConvArgs& a, hipStream_t stream, bool n128 = false) {
   const int M = a.N * a.Ho * a.Wo;
@@ -852,6 +897,11 @@ static int conv_v3_launch(ConvArgs& a, int variant, hipStream_t stream, void* ws
   if (variant == 6 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
       ((uintptr_t)a.bias % 8) == 0) {
     conv_v6_go(a, stream);
+    return (int)hipGetLastError();
+  }
+  if (variant == 21 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&
+      ((uintptr_t)a.bias % 8) == 0 && a.Cout % 80 == 0 && a.gnp == nullptr) {
+    conv_v6w4_go(a, stream);
     return (int)hipGetLastError();
   }
   if (variant == 18 && a.Cin % 64 == 0 && (a.in2 == nullptr || a.C1 % 64 == 0) && a.kh * a.kw * a.Cin >= 128 &&

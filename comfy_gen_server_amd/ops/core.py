@@ -940,9 +940,12 @@ def _conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, st
                           ("v2", lambda: run(2))]
                 if Cout % 128 == 0 and Cout % 160 and kh * kw * Cin >= 128:
                     cands.append(("v6n128", lambda: run(18)))   # 256 x 128 tiles (e.g. the VAE's Cout = 128)
+                if Cout % 80 == 0 and kh * kw * Cin >= 128 and M <= 32768:
+                    cands.append(("v6w4", lambda: run(21)))      # 128 x 80 tiles, 4 waves (batch-1 grids)
             choice = autotune.choose(("conv", N, H, W, Cin, Cout, kh, stride, padding, flags, int(r is not None))
                                      + ((("dual", C1),) if x2c is not None else ()), cands, default="auto")
-            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7, "v8": 8, "v6n128": 18, "auto": -2}[choice]
+            variant = {"v2": 2, "v4": 4, "v5": 5, "v6": 6, "v7": 7, "v8": 8, "v6n128": 18, "v6w4": 21,
+                       "auto": -2}[choice]
         if (gn_stats and variant == 6 and _GNS and (Ho * Wo) % 256 == 0 and Cin % 64 == 0 and C1 % 64 == 0
                 and Cout % 8 == 0 and kh * kw * Cin >= 128 and (bias is None or bias.data_ptr() % 8 == 0)
                 and _native.has_kernel("cgs_conv2d_nhwc_gns")):

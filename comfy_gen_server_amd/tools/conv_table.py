@@ -48,7 +48,7 @@ VAE = [
     ("vae 2x-up 256 512->1024", 8, 512, 512, 256, 256, 3, 1),
 ]
 # v7s: v7 + split-K tail; v6k: v6 with the older per-lane-address gather (ConvGatherK) instead of ConvGatherKD
-VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v6k": 16, "v6n128": 18, "v7": 7, "v7s": 8}
+VARIANTS = {"v2": 2, "v5": 5, "v6": 6, "v6k": 16, "v6n128": 18, "v6w4": 21, "v7": 7, "v7s": 8}
 
 
 def _time(fn, iters):

@@ -1,6 +1,6 @@
 """Re-measure the packaged tuning table's conv entries on this GPU (after a conv-kernel change).
 
-python -m comfy_gen_server_amd.tools.retune out.json [--apply]
+python -m comfy_gen_server_amd.tools.retune out.json [--n 1,2] [--apply]
 
 Every ``conv|...`` key of ``data/tune_mi355x.json`` is rebuilt as a real problem (shapes, dual-input
 concat, nearest-2x upsample flag, residual) and run once through ``ops.conv2d`` with the packaged table
@@ -34,6 +34,9 @@ def main(argv):
     with open(autotune.DEFAULT_TABLE) as f:
         table = json.load(f)
     keys = sorted(k for k in table if k.startswith("conv|"))
+    if "--n" in argv:           # only the keys of these batch sizes (first key field)
+        only = {int(v) for v in argv[argv.index("--n") + 1].split(",")}
+        keys = [k for k in keys if int(k.split("|")[1]) in only]
     out = {}
     for key in keys:
         N, H, W, Cin, Cout, kh, stride, pad, flags, res, C1 = _problem(key)

@@ -332,8 +332,8 @@ def test_elementwise(cuda):
     assert torch.equal(up, F.interpolate(im, scale_factor=2.0, mode="nearest"))
 
 
-@pytest.fixture(params=[2, 3, 4, 5, 6, 7, 8, 18],
-                ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160", "cv7ppk", "cv8t128", "cv6n128"])
+@pytest.fixture(params=[2, 3, 4, 5, 6, 7, 8, 18, 21],
+                ids=["cv2", "cv3w4", "cv3w8", "cv5pp", "cv6pp160", "cv7ppk", "cv8t128", "cv6n128", "cv6w4"])
 def conv_variant(request):
     lib = _native.load_kernels()
     lib.cgs_conv_set_variant(request.param)
@@ -348,7 +348,7 @@ def conv_variant(request):
                                                   (2, 96, 20, 20, 160, 3, 1, 1), (1, 320, 33, 17, 640, 3, 2, 1)])
 @pytest.mark.parametrize("epi", ["bias", "bias_res", "none"])
 def test_conv2d(cuda, N, Cin, H, W, Cout, k, s, p, epi, conv_variant):
-    if conv_variant in (2, 5, 6, 18) and Cin % 64:
+    if conv_variant in (2, 5, 6, 18, 21) and Cin % 64:
         pytest.skip("v2/v5/v6 need Cin % 64")
     torch.manual_seed(0)
     x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
