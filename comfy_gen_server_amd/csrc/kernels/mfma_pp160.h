@@ -491,12 +491,23 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
       }
 #pragma unroll
       for (int i = 0; i < NI; i += 2) store_t4(i, pk[i][4], pk[i + 1][4]);
-      // row (16 i + fr) of this wave's 80 columns: 20 values in each of the 4 lanes fr + 16 fq
+      // row (16 i + fr) of this wave's 80 columns: 20 values in each of the 4 lanes fr + 16 fq. Each lane takes
+      // (mean, M2) of its 20 (shifted by its own first value), then Chan-combines with lane l ^ 16 and l ^ 32
+      // through v_permlane16/32_swap (VALU; the former __shfl_xor / __shfl broadcast were 5 LDS permutes per row
+      // block: the epilogue cost 5-15 us per GEMM on the SDXL residual shapes, profiles/r06/rso_cost.log).
+      // Both lanes of a pair see the (lower, upper) operands in the same order: identical results.
       const int P = N / 80;
       const int chunk = n_w / 80;
+      auto comb = [](float& mean, float& m2, float n, auto swp) {   // two equal halves of n values each
+        const auto rm = swp(__float_as_uint(mean));
+        const auto rq = swp(__float_as_uint(m2));
+        const float ma = __uint_as_float(rm[0]), mb = __uint_as_float(rm[1]), d = mb - ma;
+        mean = 0.5f * (ma + mb);
+        m2 = __uint_as_float(rq[0]) + __uint_as_float(rq[1]) + d * d * (0.5f * n);
+      };
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const float sh = __shfl(unpack4_bf16(pk[i][0]).x, fr, 64);   // shift: the chunk's value of lane fr
+        const float sh = unpack4_bf16(pk[i][0]).x;
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -505,16 +516,13 @@ __device__ __forceinline__ void run(AL& al, const u16* __restrict__ W, long long
           s1 += (d0 + d1) + (d2 + d3);
           s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
         }
-        s1 += __shfl_xor(s1, 16, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 32, 64);
+        constexpr float i20 = 1.f / 20.f;
+        float mean = sh + s1 * i20, m2 = fmaxf(s2 - s1 * s1 * i20, 0.f);
+        comb(mean, m2, 20.f, [](unsigned v) { return __builtin_amdgcn_permlane16_swap(v, v, false, false); });
+        comb(mean, m2, 40.f, [](unsigned v) { return __builtin_amdgcn_permlane32_swap(v, v, false, false); });
         const int row = m_w + 16 * i + fr;
-        if (fq == 0 && row < M) {
-          constexpr float inv = 1.f / 80.f;
-          *reinterpret_cast<float2*>(e.gnp + ((long long)row * P + chunk) * 2) =
-              float2{sh + s1 * inv, fmaxf(s2 - s1 * s1 * inv, 0.f)};
-        }
+        if (fq == 0 && row < M)
+          *reinterpret_cast<float2*>(e.gnp + ((long long)row * P + chunk) * 2) = float2{mean, m2};
       }
       return;
     }
