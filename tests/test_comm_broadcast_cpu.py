@@ -16,6 +16,20 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+def _plain(o):
+    if isinstance(o, torch.Tensor):
+        return ("tensor", str(o.dtype), o.float().tolist())
+    if isinstance(o, dict):
+        return {k: _plain(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return type(o)(_plain(v) for v in o)
+    return o
+
+
+def _same(plain, t):
+    return plain == ("tensor", str(t.dtype), t.float().tolist())
+
+
 def _worker(rank, world, port, tmp, q):
     import datetime
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -54,7 +68,9 @@ def _worker(rank, world, port, tmp, q):
         out["missing"] = type(ex).__name__
     out["reads"] = reads
     out["received"] = ctx.loads_received
-    q.put((rank, out))
+    # plain Python values only: a tensor in the queue travels as a shared-memory fd that the parent may try to
+    # receive after this process has exited (connection reset)
+    q.put((rank, _plain(out)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -78,9 +94,9 @@ def test_spmd_checkpoint_broadcast_flat_nested_and_failure(tmp_path):
     for r in (0, 1):
         o = res[r]
         assert set(o["flat"]) == {"w", "b"}
-        assert torch.equal(o["flat"]["w"], flat["w"]) and torch.equal(o["flat"]["b"], flat["b"])
+        assert _same(o["flat"]["w"], flat["w"]) and _same(o["flat"]["b"], flat["b"])
         assert o["flat_meta"] == {"k": "v"}
-        assert torch.equal(o["nested"]["params_ema"]["conv.weight"], nested["params_ema"]["conv.weight"])
+        assert _same(o["nested"]["params_ema"]["conv.weight"], nested["params_ema"]["conv.weight"])
         assert o["nested"]["activation_func"] == "relu" and o["nested_meta"] == {"k": "v"}
         assert o["missing"] in ("FileNotFoundError", "RuntimeError"), o["missing"]
     # the flat checkpoint: rank 0 read it twice, rank 1 never (received twice); the nested one: both ranks
