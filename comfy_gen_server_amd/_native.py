@@ -174,6 +174,7 @@ KERNEL_SIGNATURES = {
     "cgs_v7_set_dbg": [_I],
     "cgs_v6_set_mode": [_I],
     "cgs_attn_set_prio": [_I],
+    "cgs_gn_set_blocks": [_I],
     "cgs_conv_smalln_set_lds": [_I],
     "cgs_attn_set_kv2_rows": [_I],
     "cgs_grn_set_rows": [_I],
@@ -219,7 +220,7 @@ KERNEL_SIGNATURES = {
 }
 
 
-_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_splitk_ws_bytes": ctypes.c_longlong, "cgs_groupnorm_f32_ws": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None, "cgs_conv_smalln_set_lds": None, "cgs_attn_set_kv2_rows": None, "cgs_grn_set_rows": None,
+_RESTYPE = {"cgs_groupnorm_workspace": ctypes.c_longlong, "cgs_splitk_ws_bytes": ctypes.c_longlong, "cgs_groupnorm_f32_ws": ctypes.c_longlong, "cgs_grn_slices": ctypes.c_int, "cgs_v7_ws_bytes": ctypes.c_longlong, "cgs_gemm_skinny_ws_bytes": ctypes.c_longlong, "cgs_gemm_set_variant": None, "cgs_v7_set_dbg": None, "cgs_v6_set_mode": None, "cgs_attn_set_prio": None, "cgs_gn_set_blocks": None, "cgs_conv_smalln_set_lds": None, "cgs_attn_set_kv2_rows": None, "cgs_grn_set_rows": None,
             "cgs_conv_set_variant": None, "cgs_set_tile_group": None, "cgs_conv_set_tile_group": None, "cgs_dwconv_set_px": None,
             "cgs_attn_set_variant": None,
             "cgs_conv_v6_set_loader": None}

@@ -15,11 +15,20 @@
 #define GN_THREADS 256
 #define GN_MAX_CHUNKS_PER_LANE 4   // <= 64*4*8 = 2048 channels of a row per block (wider rows: channel slices)
 
+// statistics blocks over the batch: CGS_GN_BLOCKS (default 2048) / cgs_gn_set_blocks (A/B; a smaller count only
+// shrinks the workspace cgs_groupnorm_workspace sized earlier)
+static int g_gn_blocks = -1;
+static int gn_blocks() {
+  if (g_gn_blocks < 0) g_gn_blocks = getenv("CGS_GN_BLOCKS") ? atoi(getenv("CGS_GN_BLOCKS")) : 2048;
+  return g_gn_blocks > 0 ? g_gn_blocks : 2048;
+}
+CGS_EXPORT void cgs_gn_set_blocks(int n) { g_gn_blocks = n; }
+
 static inline int gn_pix_per_block(int N, int HW) {
   // ~2048 statistics blocks over the batch, >= 16 pixels each -- >= 64 at batch <= 4: there 16-pixel blocks
   // (1024 per image at 128^2) made the finalize pass (one block per (image, group)) walk 10-40 k partials
   // each (~16 us per GroupNorm at SDXL batch 1; profiles/r04/groupnorm_b1_r04ai.log)
-  int target_blocks_per_n = (2048 + N - 1) / N;
+  int target_blocks_per_n = (gn_blocks() + N - 1) / N;
   int ppb = (HW + target_blocks_per_n - 1) / target_blocks_per_n;
   if (ppb < 16) ppb = 16;
   if (N <= 4 && ppb < 64) ppb = 64;

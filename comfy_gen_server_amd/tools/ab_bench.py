@@ -26,7 +26,7 @@ import torch
 # environment at launch): name -> (setter, default)
 _NATIVE_KNOBS = {"CGS_TILE_GROUP": ("cgs_set_tile_group", 4), "CGS_CONV_TILE_GROUP": ("cgs_conv_set_tile_group", 8),
                  "CGS_DW_PX": ("cgs_dwconv_set_px", 4), "CGS_ATTN_KV2_ROWS": ("cgs_attn_set_kv2_rows", 0),
-                 "CGS_GRN_ROWS": ("cgs_grn_set_rows", 1)}
+                 "CGS_GRN_ROWS": ("cgs_grn_set_rows", 1), "CGS_GN_BLOCKS": ("cgs_gn_set_blocks", 2048)}
 
 
 _LIBS: dict = {}
