@@ -27,7 +27,8 @@ SHAPES = [
     ("kv_ctx1280", 1232, 2560, 2048, False, False),
 ]
 
-VARIANTS = {"v5": 5, "v6": 6, "v7": 7, "v7s": 8, "v4": 4, "auto": -1}   # v7s: v7 + split-K tail
+VARIANTS = {"v5": 5, "v6": 6, "v7": 7, "v7s": 8, "v4": 4, "w6": 16, "w6n160": 17, "v6w4": 20, "auto": -1}
+# v7s: v7 + split-K tail; w6: one wave per SIMD, 256 x 256 (w6n160: 256 x 160); v6w4: 128 x 80, 4 waves
 
 
 def _time(fn, iters):
