@@ -1,13 +1,16 @@
 """Re-measure the packaged tuning table's GEMM entries on this GPU (after a GEMM-kernel change, e.g. new
 candidates such as the split-K forms).
 
-python -m comfy_gen_server_amd.tools.gemm_retune out.json [--m M1,M2,...] [--apply]
+python -m comfy_gen_server_amd.tools.gemm_retune out.json [--m M1,M2,...] [--apply [--replace-splitk]]
 
 Every ``gemm|M|N|K|epi`` / ``gemm_lnfold|M|N|K|epi`` key of ``data/tune_mi355x.json`` (optionally only
 the listed M) is rebuilt as a random problem and run once through ``ops.linear`` / ``ops.linear_lnfold``
 with the packaged table NOT loaded, so ``autotune.choose`` times every legal candidate afresh.
 ``out.json`` gets ``{key: {"old": ..., "choice": ..., "ms": {...}}}``; ``--apply`` also rewrites those
-entries of the packaged table (run that on the development copy, not on a GPU box's snapshot).
+entries of the packaged table (run that on the development copy, not on a GPU box's snapshot). Entries that
+hold a split-K choice are left alone unless ``--replace-splitk``: those were set from in-job A/Bs, and the
+isolated time of a split-K launch pair disagrees with its in-job cost (round 6: the Cascade batch-1 K = 8192
+projection re-timed to v14 here ran 3.9 % slower per job, profiles/r06/ab_tables_r06.log).
 """
 from __future__ import annotations
 
@@ -61,7 +64,10 @@ def main(argv):
     with open(argv[0], "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     if "--apply" in argv:
+        keep_sk = "--replace-splitk" not in argv
         for k, v in out.items():
+            if keep_sk and v["old"] in core._SPLITK:
+                continue
             if v["choice"]:
                 table[k] = v["choice"]
         with open(autotune.DEFAULT_TABLE, "w") as f:
