@@ -564,8 +564,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_d64_kernel(
 // while the current one computes, so K / V are staged once per 128 * QI queries and the Q stream stays
 // in flight: at QI = 1 a workgroup's life was one K/V + Q load latency for ~1 us of math (SDXL
 // cross-attention ran at ~2.5 TB/s of its Q + O traffic).
+// QI = 1, NKT <= 3 is built for 5 waves per SIMD (launch bounds: <= 102 registers instead of ~110, 4 -> 5 workgroups per
+// CU): SDXL level-2 cross-attention 25.7 -> 24.4 us (profiles/r06/skv_lb_ab.log; 6 waves measured no better).
 template <int NKT, bool PRIO = true, int QI = 1>
-__global__ __launch_bounds__(256) void attn_fwd_d64_shortkv_kernel(
+__global__ __launch_bounds__(256, (QI == 1 && NKT <= 3) ? 5 : 1) void attn_fwd_d64_shortkv_kernel(
     const u16* __restrict__ qp, const u16* __restrict__ kp, const u16* __restrict__ vp, u16* __restrict__ op,
     int H, int Sq, int Sk, long long qsb, long long qss, long long qsh, long long ksb, long long kss,
     long long ksh, long long vsb, long long vss, long long vsh, long long osb, long long oss, long long osh,
