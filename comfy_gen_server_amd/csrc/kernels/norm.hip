@@ -47,7 +47,7 @@ template <int DT, int KM, int PK = 1>
 __global__ __launch_bounds__(GN_THREADS) void gn_partial_kernel(const u16* __restrict__ x, const u16* __restrict__ x2,
                                                                int C1, float* __restrict__ part,
                                                                int HW, int C, int ppb, int nb, int CS) {
-  // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget).
+  // blockIdx.z selects a channel slice [c0, c0 + CS) (CS <= 2048: the per-lane register budget; gn_slices).
   // KM = 16-byte chunk rounds per lane (ceil(CS / 512)); each wave keeps GN_UNROLL rows of loads in
   // flight before accumulating (one row per wave per trip left the HBM pipe half empty).
   // PK > 1 (narrow rows, CS / 8 <= 64 / PK chunks, KM = 1): the wave's lanes split into PK groups of
@@ -347,13 +347,34 @@ CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
 static int gn_apply_launch(const void* x, const void* x2, int C1, void* y, const float* ab, int N, int HW, int C,
                            int silu, int dtype, hipStream_t stream);
 
+// Channel slices of the statistics pass (blockIdx.z). Up to 1024 channels a slice is the whole row (KM <= 2);
+// wider rows are cut into equal 8-aligned slices of <= 512 channels whose chunk count fills the wave (KM = 1, or
+// the pixel-packed PK forms): the KM = 3 / 4 forms held 161-210 VGPRs. Full GroupNorm + SiLU at SDXL sizes
+// (profiles/r06/gn_slices_ab.log): C = 1920 at 64^2 269 -> 219 us, C = 2560 at 32^2 78 -> 68 us, C = 1280
+// 48 -> 45 us; at C = 640 the 128-channel slices measured slower than the KM = 2 row (67.6 vs 70.6 us).
+static int gn_slices(int C) {
+  const int ns0 = (C + 2047) / 2048;
+  if (C <= 1024 || C % 8) return ns0;
+  const int tot = C / 8;
+  int best = ns0;
+  float bu = -1.f;
+  for (int ns = (C + 511) / 512; ns <= tot; ++ns) {
+    if (tot % ns) continue;
+    const int nch = tot / ns;
+    const int lanes = nch <= 8 ? 8 : nch <= 16 ? 16 : nch <= 32 ? 32 : 64;
+    const float u = (float)nch / (float)lanes;
+    if (u >= 0.9f) return ns;
+    if (u > bu) { bu = u; best = ns; }
+  }
+  return best;
+}
+
 // x, y: [N, HW, C] (NHWC); gamma/beta [C] in the activation dtype; pre_add [N, C] (act dtype) or null.
 // ws: workspace of cgs_groupnorm_workspace() bytes (torch-allocated so it is graph-capturable).
 static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const void* gamma, const void* beta,
                           const void* pre_add, void* ws, int N, int HW, int C, int G, float eps, int silu, int dtype,
                           hipStream_t stream, int pld) {
-  // channel slices of <= 2048 (the per-lane register budget of gn_partial), equal and 8-aligned
-  const int ns = (C + 2047) / 2048;
+  const int ns = gn_slices(C);      // equal, 8-aligned channel slices
   if (C % 8 || C % G || C % (8 * ns) || C > 8192 || C1 % 8 || C1 > C) return (int)hipErrorInvalidValue;
   const int CS = C / ns;
   int ppb = gn_pix_per_block(N, HW);
@@ -387,7 +408,7 @@ static int groupnorm_impl(const void* x, const void* x2, int C1, void* y, const 
 // The statistics half of groupnorm_impl: per-(n, g) (mean, M2) of the given rows into stats [N][G][2].
 static int groupnorm_stats_impl(const void* x, const void* x2, int C1, const void* pre_add, void* ws, float* stats,
                                 int N, int HW, int C, int G, int dtype, hipStream_t stream) {
-  const int ns = (C + 2047) / 2048;
+  const int ns = gn_slices(C);
   if (C % 8 || C % G || C % (8 * ns) || C > 8192 || C1 % 8 || C1 > C) return (int)hipErrorInvalidValue;
   const int CS = C / ns;
   int ppb = gn_pix_per_block(N, HW);
