@@ -347,13 +347,14 @@ CGS_EXPORT long long cgs_groupnorm_workspace(int N, int HW, int C) {
 static int gn_apply_launch(const void* x, const void* x2, int C1, void* y, const float* ab, int N, int HW, int C,
                            int silu, int dtype, hipStream_t stream);
 
-// Channel slices of the statistics pass (blockIdx.z). Up to 1024 channels a slice is the whole row (KM <= 2);
-// wider rows are cut into equal 8-aligned slices of <= 512 channels whose chunk count fills the wave (KM = 1, or
-// the pixel-packed PK forms): the KM = 3 / 4 forms held 161-210 VGPRs. Full GroupNorm + SiLU at SDXL sizes
-// (profiles/r06/gn_slices_ab.log): C = 1920 at 64^2 269 -> 219 us, C = 2560 at 32^2 78 -> 68 us, C = 1280
-// 48 -> 45 us; at C = 640 the 128-channel slices measured slower than the KM = 2 row (67.6 vs 70.6 us).
+// Channel slices of the statistics pass (blockIdx.z). Up to 512 channels a slice is the whole row, 513-1024 two
+// halves (KM = 1 each); wider rows are cut into equal 8-aligned slices of <= 512 channels whose chunk count fills
+// the wave (KM = 1, or the pixel-packed PK forms): the KM = 2..4 forms held 112-210 VGPRs. Full GroupNorm + SiLU
+// at SDXL sizes (profiles/r06/gn_slices_ab.log, gn_mid_ab.log): C = 1920 at 64^2 269 -> 219 us, C = 2560 at
+// 32^2 78 -> 68 us, C = 1280 48 -> 45 us, C = 640 68 -> 63 us (its 128-channel PK slices measured 71 us).
 static int gn_slices(int C) {
   const int ns0 = (C + 2047) / 2048;
+  if (C > 512 && C <= 1024 && C % 16 == 0) return 2;   // two KM = 1 slices: C = 640 68.2 -> 63.4 us (gn_mid_ab.log)
   if (C <= 1024 || C % 8) return ns0;
   const int tot = C / 8;
   int best = ns0;
